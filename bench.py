@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: data-parallel MLP 1024-4096-4096-1024 training on MI355X.
+
+BASELINE.json config 3: bf16 MLP, BFP-compressed all-reduce of every layer's gradient bucket with the SGD
+weight update fused into the all-gather epilogue, comm overlapped with backward on a side HIP stream.
+Metric: whole-job training throughput in samples/s (weak scaling: per-GPU batch fixed as N grows).
+
+Contract: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under torch.distributed.run, one rank per
+GPU over RCCL). W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
+torch.cuda.synchronize() on both sides; max time over ranks; rank 0 prints ONE JSON line.
+
+Synthetic data (random bf16 inputs, random labels) and random-init weights of the named architecture.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from fpga_ai_nic_amd.models.mlp import MLP  # noqa: E402
+from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine  # noqa: E402
+from fpga_ai_nic_amd.parallel.transport import NativeTransport, ThreadFabric, TorchDistTransport  # noqa: E402
+from fpga_ai_nic_amd.utils import dist as D  # noqa: E402
+
+SIZES = [1024, 4096, 4096, 1024]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mb-per-gpu", type=int, default=2048)
+    ap.add_argument("--compress", default="bfp", choices=["bfp", "raw", "raw_bf16", "rccl", "local"])
+    ap.add_argument("--rounding", default="rne", choices=["rne", "trunc"])
+    ap.add_argument("--algo", default="mesh", choices=["mesh", "ring"])
+    ap.add_argument("--rings", type=int, default=1)
+    ap.add_argument("--transport", default="torch", choices=["torch", "native"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--lr", type=float, default=0.01)
+    a = ap.parse_args()
+
+    rank, world, local, device = D.init_distributed()
+    if world != a.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if device.type != "cuda":
+        print("[bench] no GPU visible: running the CPU path (functional only)", file=sys.stderr)
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    if world > 1:
+        transport = NativeTransport() if a.transport == "native" else TorchDistTransport()
+    else:
+        transport = ThreadFabric(1).transport(0)
+    kind = "local" if a.compress == "local" else a.compress
+    engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings)
+    pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
+    model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
+    if world > 1:
+        for l in model.layers:
+            transport.broadcast_(l.master, 0)
+        model.sync_lp()
+    trainer = DataParallelTrainer(model, engine, lr=a.lr)
+    mb = a.mb_per_gpu
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = (torch.rand(mb, SIZES[0], generator=g) * 2 - 1).to(device=device, dtype=dtype)
+    y = torch.randint(0, SIZES[-1], (mb,), generator=g, dtype=torch.int32).to(device)
+
+    for _ in range(a.warmup):
+        trainer.step(x, y)
+    trainer.finish()
+    D.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss_rows = trainer.step(x, y)
+    trainer.finish()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    D.barrier()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0)
+    loss = float(loss_rows.float().mean().item())
+
+    ms = elapsed / a.steps * 1e3
+    global_batch = mb * world
+    value = global_batch * a.steps / elapsed
+    flops = model.flops_per_sample() * global_batch * a.steps / elapsed
+    grad_bytes = sum(l.n for l in model.layers) * 4
+    if rank == 0:
+        rec = {
+            "metric": "MLP training samples/sec (1024-4096-4096-1024, BFP all-reduce + fused SGD)",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (random inputs/labels, random-init weights)",
+            "config": {
+                "model": "mlp-1024-4096-4096-1024",
+                "global_batch": global_batch,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "mb_per_gpu": mb,
+                "compress": a.compress,
+                "rounding": a.rounding,
+                "algo": a.algo,
+                "rings": engine.rings if engine is not None else 0,
+                "transport": a.transport if world > 1 else "none",
+                "fused_sgd": True,
+            },
+            "extra": {
+                "achieved_tflops": round(flops / 1e12, 2),
+                "grad_bytes_f32_per_step": grad_bytes,
+                "effective_allreduce_algo_bw_GBps": round(grad_bytes / (ms / 1e3) / 1e9, 2),
+                "final_loss": round(loss, 5),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    D.cleanup()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+// Torch-facing bindings for the GEMM, NN and planner components.
+#include "bindings_common.h"
+#include "bfp/bfp_format.h"
+#include "comm/planner.h"
+#include "gemm/gemm.h"
+#include "nn/nn.h"
+
+namespace fan {
+
+namespace {
+
+int dcode(const at::Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return kF32;
+  if (t.scalar_type() == at::kBFloat16) return kBF16;
+  TORCH_CHECK(false, "expected float32 or bfloat16 tensor");
+}
+
+// Row-major 2-D view helpers: returns leading dimension (elements) of a 2-D tensor with unit column stride.
+int64_t ld_of(const at::Tensor& t) {
+  TORCH_CHECK(t.dim() == 2, "expected a 2-D tensor");
+  TORCH_CHECK(t.stride(1) == 1, "expected unit stride in the last dim");
+  return t.stride(0);
+}
+
+// C = op(A) op(B) with fused epilogue.
+//   a_t: if true, A is given as a [K][M] tensor (MN-contiguous), else [M][K]
+//   b_t: if true, B is given as a [N][K] tensor (K-contiguous), else [K][N]
+void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tensor& C, int64_t epilogue,
+          const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux, bool accumulate,
+          int64_t split_k, const c10::optional<at::Tensor>& workspace) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
+  TORCH_CHECK(A.scalar_type() == B.scalar_type(), "A and B dtype mismatch");
+  GemmArgs g{};
+  g.A = A.data_ptr();
+  g.B = B.data_ptr();
+  g.C = C.data_ptr();
+  g.lda = ld_of(A);
+  g.ldb = ld_of(B);
+  g.ldc = ld_of(C);
+  g.M = (int)(a_t ? A.size(1) : A.size(0));
+  g.K = (int)(a_t ? A.size(0) : A.size(1));
+  g.N = (int)(b_t ? B.size(0) : B.size(1));
+  const int64_t kb = b_t ? B.size(1) : B.size(0);
+  TORCH_CHECK(kb == g.K, "gemm: inner dimensions differ (", g.K, " vs ", kb, ")");
+  TORCH_CHECK(C.size(0) == g.M && C.size(1) == g.N, "gemm: bad C shape");
+  g.a_kcontig = !a_t;
+  g.b_kcontig = b_t;
+  g.epilogue = (int)epilogue;
+  g.c_bf16 = C.scalar_type() == at::kBFloat16;
+  g.accumulate = accumulate;
+  g.split_k = (int)std::max<int64_t>(1, split_k);
+  if (bias) {
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() >= g.N, "bad bias");
+    g.bias = bias->data_ptr();
+  }
+  if (aux) {
+    TORCH_CHECK(aux->scalar_type() == C.scalar_type(), "aux dtype must match C");
+    g.aux = aux->data_ptr();
+    g.ldaux = ld_of(*aux);
+  }
+  if (workspace) g.workspace = workspace->data_ptr();
+  if (A.scalar_type() == at::kBFloat16) {
+    TORCH_CHECK(bias ? bias->scalar_type() == at::kBFloat16 : true, "bias must be bf16");
+    TORCH_CHECK(gemm_bf16_supported(g), "gemm_bf16: unsupported shape M=", g.M, " N=", g.N, " K=", g.K,
+                " split_k=", g.split_k);
+    launch_gemm_bf16(g, fan_stream());
+  } else {
+    TORCH_CHECK(A.scalar_type() == at::kFloat, "gemm: A must be bf16 or f32");
+    TORCH_CHECK(gemm_f32_supported(g), "gemm_f32: unsupported shape M=", g.M, " N=", g.N, " K=", g.K);
+    launch_gemm_f32(g, fan_stream());
+  }
+}
+
+bool gemm_supported(int64_t M, int64_t N, int64_t K, bool bf16, int64_t split_k) {
+  GemmArgs g{};
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = g.ldb = 64;
+  g.ldc = N;
+  g.split_k = (int)split_k;
+  g.workspace = (void*)16;
+  return bf16 ? gemm_bf16_supported(g) : gemm_f32_supported(g);
+}
+
+void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, at::Tensor& dlogits, at::Tensor& loss_rows,
+                  double grad_scale) {
+  TORCH_CHECK(logits.is_cuda() && labels.is_cuda() && dlogits.is_cuda() && loss_rows.is_cuda(), "GPU tensors");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous(), "labels must be int32");
+  TORCH_CHECK(loss_rows.scalar_type() == at::kFloat, "loss_rows must be f32");
+  const int M = (int)logits.size(0), Cc = (int)logits.size(1);
+  TORCH_CHECK(dlogits.size(0) == M && dlogits.size(1) == Cc, "dlogits shape");
+  launch_softmax_xent(dcode(logits), logits.data_ptr(), ld_of(logits), labels.data_ptr<int32_t>(), dcode(dlogits),
+                      dlogits.data_ptr(), ld_of(dlogits), loss_rows.data_ptr<float>(), M, Cc, (float)grad_scale,
+                      fan_stream());
+}
+
+void col_sum(const at::Tensor& x, at::Tensor& out, double scale, bool accumulate, at::Tensor& workspace) {
+  TORCH_CHECK(x.is_cuda() && out.is_cuda() && workspace.is_cuda(), "GPU tensors");
+  const int M = (int)x.size(0), N = (int)x.size(1);
+  TORCH_CHECK(out.numel() >= N && out.is_contiguous(), "out too small");
+  TORCH_CHECK(workspace.scalar_type() == at::kFloat && (size_t)workspace.numel() >= col_sum_workspace_floats(M, N),
+              "workspace too small");
+  launch_col_sum(dcode(x), x.data_ptr(), ld_of(x), M, N, dcode(out), out.data_ptr(), (float)scale, accumulate,
+                 workspace.data_ptr<float>(), fan_stream());
+}
+
+}  // namespace
+
+void register_gemm(pybind11::module_& m) {
+  m.def("gemm", &gemm, "MFMA GEMM with fused epilogue", pybind11::arg("A"), pybind11::arg("a_t"), pybind11::arg("B"),
+        pybind11::arg("b_t"), pybind11::arg("C"), pybind11::arg("epilogue") = 0, pybind11::arg("bias") = pybind11::none(),
+        pybind11::arg("aux") = pybind11::none(), pybind11::arg("accumulate") = false, pybind11::arg("split_k") = 1,
+        pybind11::arg("workspace") = pybind11::none());
+  m.def("gemm_supported", &gemm_supported);
+  m.attr("EPI_NONE") = (int)kEpiNone;
+  m.attr("EPI_BIAS") = (int)kEpiBias;
+  m.attr("EPI_BIAS_RELU") = (int)kEpiBiasRelu;
+  m.attr("EPI_RELU_MASK") = (int)kEpiReluMask;
+}
+
+void register_nn(pybind11::module_& m) {
+  m.def("softmax_xent", &softmax_xent, "fused softmax + cross-entropy fwd/bwd");
+  m.def("col_sum", &col_sum, "bias-gradient column sum");
+  m.def("col_sum_workspace_floats", [](int64_t M, int64_t N) { return (int64_t)col_sum_workspace_floats((int)M, (int)N); });
+}
+
+void register_planner(pybind11::module_& m) {
+  m.def("ring_geometry", [](int64_t n, int world, int64_t max_slice) {
+    auto g = ring_geometry(n, world, max_slice);
+    return pybind11::make_tuple(g.n, g.slice_elems, g.blocks, g.n_pad);
+  });
+  m.def("ring_plan", [](int world, int position, int64_t blocks) {
+    auto rounds = ring_plan(world, position, blocks);
+    std::vector<std::vector<int32_t>> out;
+    out.reserve(rounds.size());
+    for (auto& r : rounds) out.push_back({r.send_slice, r.send_src, r.recv_slice, r.recv_full, r.owned});
+    return out;
+  });
+  m.def("ring_orders", &ring_orders, pybind11::arg("world"), pybind11::arg("max_rings"));
+}
+
+}  // namespace fan

@@ -1,0 +1,58 @@
+// Native RCCL communicator (own ncclComm_t, independent of torch's ProcessGroup).
+//
+// The MI355X-native stand-in for the reference's NIC link layer + CSR driver (sw/mlp_mpi_example_f32.cpp:35-180,
+// hw/all_reduce.sv ETH ports): point-to-point xGMI transfers between ring neighbours (ncclSend/ncclRecv in one
+// group per round) and the direct full-mesh collectives that a fully connected 8-GPU xGMI node favours.
+// Bootstrap: the 128-byte ncclUniqueId is exchanged through torch.distributed's store (no MPI).
+#pragma once
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "common/hip_common.h"
+
+namespace fan {
+
+#define FAN_NCCL_CHECK(expr)                                                                              \
+  do {                                                                                                    \
+    ncclResult_t _r = (expr);                                                                             \
+    if (_r != ncclSuccess)                                                                                \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " + __FILE__ + \
+                               ":" + std::to_string(__LINE__) + ": " #expr);                              \
+  } while (0)
+
+struct P2POp {
+  void* ptr;
+  size_t bytes;
+  int peer;
+};
+
+class NativeComm {
+ public:
+  NativeComm(const std::string& uid_bytes, int rank, int world, int device);
+  ~NativeComm();
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  // One RCCL group with every send and recv (ring round / multi-ring round).
+  void sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>& recvs, hipStream_t s);
+  void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s);
+  void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s);
+  void all_reduce(void* buf, size_t count, int dtype /*0 f32, 1 bf16*/, hipStream_t s);
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, hipStream_t s);
+  void broadcast(void* buf, size_t bytes, int root, hipStream_t s);
+  // Returns an empty string when healthy, else the RCCL async error text.
+  std::string async_error();
+  void abort();
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_ = 0, world_ = 1;
+  bool aborted_ = false;
+};
+
+std::string nccl_unique_id_bytes();
+int nccl_version();
+
+}  // namespace fan

@@ -1,0 +1,43 @@
+// MFMA GEMM entry points (gfx950).
+//
+// C[M][N] (row-major, ldc) = sum_k A(m,k) * B(k,n), with fused epilogues. Operand layouts:
+//   A K-contiguous : A stored [M][K] (lda)      A MN-contiguous : A stored [K][M] (lda)
+//   B K-contiguous : B stored [N][K] (ldb)      B MN-contiguous : B stored [K][N] (ldb)
+// so forward (X·W, W=[in][out]), backward-data (dZ·Wᵀ) and backward-weight (Xᵀ·dZ) of the
+// MLP all run without a transpose pass (reference: libxsmm fc fwd/bwd, sw/mlp_mpi_example_f32.cpp:708, 741, 770).
+#pragma once
+#include "common/hip_common.h"
+
+namespace fan {
+
+enum GemmEpilogue : int {
+  kEpiNone = 0,
+  kEpiBias = 1,       // + bias[n]
+  kEpiBiasRelu = 2,   // relu(x + bias[n])
+  kEpiReluMask = 3,   // x * (aux[m][n] > 0)   (ReLU backward fused into the bwd-data GEMM)
+};
+
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;
+  const void* bias;  // dtype = operand dtype
+  const void* aux;   // bf16/f32 (same as C dtype), [M][N] with ldaux
+  int64_t lda, ldb, ldc, ldaux;
+  int M, N, K;
+  bool a_kcontig, b_kcontig;
+  int epilogue;
+  bool c_bf16;       // output dtype (bf16 or f32)
+  bool accumulate;   // C += result (f32 output only)
+  int split_k;       // >1: K split over workgroups, fp32 partial slabs + ordered reduce
+  void* workspace;   // split-K slabs: split_k * M * N floats
+};
+
+// Returns false if the shape is not supported by the MFMA path (caller must then error out).
+bool gemm_bf16_supported(const GemmArgs& a);
+void launch_gemm_bf16(const GemmArgs& a, hipStream_t stream);
+
+bool gemm_f32_supported(const GemmArgs& a);
+void launch_gemm_f32(const GemmArgs& a, hipStream_t stream);
+
+}  // namespace fan

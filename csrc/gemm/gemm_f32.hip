@@ -1,0 +1,190 @@
+// fp32 MFMA GEMM for gfx950 (v_mfma_f32_16x16x4_f32: exact f32 fma chain, no xf32 on CDNA4).
+//
+// Serves the reference-equivalent f32 MLP (sw/mlp_mpi_example_f32.cpp: libxsmm fc fwd/bwd in f32).
+// Block tile 128x128x32, 4 waves (2x2), each wave 64x64 = 4x4 tiles of 16x16.
+// LDS image for BOTH operands is [outer][k] (128-B rows of 32 f32), 16-B chunk c of row r stored at
+// c ^ ((r>>1)&7). K-contiguous operands are staged with global_load_lds_dwordx4 (swizzle on the
+// source address); MN-contiguous operands are register-staged and transposed on the LDS write.
+// Within each 16-wide k chunk lane l feeds k = 4*(l>>4) + i to MFMA i (a consistent permutation of
+// the k order for A and B), so every fragment read is one ds_read_b128.
+#include "gemm/gemm.h"
+
+namespace fan {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+constexpr int TILE_BYTES = 128 * BK * 4;  // 16 KiB
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+template <bool KCONTIG>
+__device__ __forceinline__ void stage(const float* __restrict__ g, int64_t ld, int o0, int k0, char* tile, int wave,
+                                      int lane) {
+  const int t = wave * 64 + lane;
+  if (KCONTIG) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = i * 32 + (t >> 3);
+      const int cs = t & 7;
+      const int c = cs ^ swz(row);
+      const float* src = g + (int64_t)(o0 + row) * ld + k0 + c * 4;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(tile + i * 4096 + wave * 1024), 16, 0, 0);
+    }
+  } else {
+    float4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int krow = i * 8 + (t >> 5);
+      const int oc = (t & 31) * 4;
+      v[i] = *reinterpret_cast<const float4*>(g + (int64_t)(k0 + krow) * ld + o0 + oc);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int krow = i * 8 + (t >> 5);
+      const int oc = (t & 31) * 4;
+      const float vv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int o = oc + u;
+        const int off = o * 128 + (((krow >> 2) ^ swz(o)) << 4) + (krow & 3) * 4;
+        *reinterpret_cast<float*>(tile + off) = vv[u];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ f32x4 frag(const char* tile, int o, int kc, int lane) {
+  const int row = o + (lane & 15);
+  const int c = kc * 4 + (lane >> 4);
+  return *reinterpret_cast<const f32x4*>(tile + row * 128 + ((c ^ swz(row)) << 4));
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid % kNumXCD;
+  const int q = nwg / kNumXCD, r = nwg % kNumXCD;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / kNumXCD;
+}
+
+template <bool AK, bool BKC, int EPI, bool ACCUM>
+__global__ void __launch_bounds__(NT, 2)
+    gemm_f32_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
+                    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, const float* __restrict__ aux,
+                    int64_t ldaux, int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_n = N / BN;
+  const int nwg = (M / BM) * tiles_n;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nk = K / BK;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage<AK>(A, lda, m0, 0, smem, wave, lane);
+  stage<BKC>(B, ldb, n0, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    char* sa = smem + cur * STAGE_BYTES;
+    char* sb = sa + TILE_BYTES;
+    if (kt + 1 < nk) {
+      char* na = smem + (cur ^ 1) * STAGE_BYTES;
+      stage<AK>(A, lda, m0, (kt + 1) * BK, na, wave, lane);
+      stage<BKC>(B, ldb, n0, (kt + 1) * BK, na + TILE_BYTES, wave, lane);
+    }
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      f32x4 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag(sa, wm * 64 + i * 16, kc, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag(sb, wn * 64 + j * 16, kc, lane);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][u], bfr[j][u], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + j * 16 + col_l;
+    const float bv = (EPI == kEpiBias || EPI == kEpiBiasRelu) ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + i * 16 + row_l + r;
+        float v = acc[i][j][r] + bv;
+        if (EPI == kEpiBiasRelu) v = fmaxf(v, 0.f);
+        if (EPI == kEpiReluMask) v = aux[(int64_t)row * ldaux + col] > 0.f ? v : 0.f;
+        float* p = C + (int64_t)row * ldc + col;
+        if (ACCUM) v += *p;
+        *p = v;
+      }
+  }
+}
+
+template <bool AK, bool BKC>
+void launch_layout(const GemmArgs& a, hipStream_t s) {
+  const int grid = (a.M / BM) * (a.N / BN);
+#define FAN_F32_CASE(E)                                                                                       \
+  case E:                                                                                                     \
+    if (a.accumulate)                                                                                         \
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC, E, true>), grid, NT, LDS_BYTES, s, (const float*)a.A, a.lda, \
+                         (const float*)a.B, a.ldb, (float*)a.C, a.ldc, (const float*)a.bias, (const float*)a.aux,    \
+                         a.ldaux, a.M, a.N, a.K);                                                            \
+    else                                                                                                      \
+      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC, E, false>), grid, NT, LDS_BYTES, s, (const float*)a.A, a.lda, \
+                         (const float*)a.B, a.ldb, (float*)a.C, a.ldc, (const float*)a.bias, (const float*)a.aux,     \
+                         a.ldaux, a.M, a.N, a.K);                                                             \
+    break;
+  switch (a.epilogue) {
+    FAN_F32_CASE(kEpiNone)
+    FAN_F32_CASE(kEpiBias)
+    FAN_F32_CASE(kEpiBiasRelu)
+    FAN_F32_CASE(kEpiReluMask)
+    default: FAN_CHECK(false, "bad epilogue");
+  }
+#undef FAN_F32_CASE
+}
+
+}  // namespace
+
+bool gemm_f32_supported(const GemmArgs& a) {
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
+  if (a.M % BM || a.N % BN || a.K % BK) return false;
+  if (a.lda % 4 || a.ldb % 4) return false;
+  if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return false;
+  if (a.c_bf16 || a.split_k > 1) return false;
+  return true;
+}
+
+void launch_gemm_f32(const GemmArgs& a, hipStream_t s) {
+  FAN_CHECK(gemm_f32_supported(a), "gemm_f32: unsupported shape/layout (need M,N % 128 == 0, K % 32 == 0)");
+  if (a.a_kcontig && a.b_kcontig) launch_layout<true, true>(a, s);
+  else if (a.a_kcontig) launch_layout<true, false>(a, s);
+  else if (a.b_kcontig) launch_layout<false, true>(a, s);
+  else launch_layout<false, false>(a, s);
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fan

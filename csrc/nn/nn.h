@@ -1,0 +1,17 @@
+// Non-GEMM NN kernels (softmax + cross-entropy, bias-gradient column sums).
+#pragma once
+#include "bfp/bfp_format.h"
+
+namespace fan {
+
+// Writes per-row loss (lse - x[label]) and dlogits = (softmax - onehot) * grad_scale.
+void launch_softmax_xent(int in_dtype, const void* logits, int64_t ld, const int32_t* labels, int out_dtype,
+                         void* dlogits, int64_t ldd, float* loss_rows, int M, int C, float grad_scale,
+                         hipStream_t s);
+
+size_t col_sum_workspace_floats(int M, int N);
+// out[n] (+)= scale * sum_m x[m][n]
+void launch_col_sum(int in_dtype, const void* x, int64_t ld, int M, int N, int out_dtype, void* out, float scale,
+                    bool accumulate, float* workspace, hipStream_t s);
+
+}  // namespace fan

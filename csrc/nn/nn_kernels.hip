@@ -1,0 +1,208 @@
+// Non-GEMM training kernels for the MLP (gfx950):
+//   softmax_xent : fused softmax + cross-entropy forward AND backward (one wave per row, online
+//                  max/sum in one read, gradient written in a second pass over the L1/L2-resident row).
+//                  Reference: libxsmm smax fwd/bwd with loss_weight (sw/mlp_mpi_example_f32.cpp:525-531,
+//                  718-728).
+//   col_sum      : bias gradient db[n] = sum_m dZ[m][n], two-pass deterministic (row-chunk partials in a
+//                  workspace, then an ordered sum). Reference: libxsmm fc bwd dbias (sw:741-742).
+#include "nn/nn.h"
+
+namespace fan {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float v[8]);
+template <>
+__device__ __forceinline__ void ld8<float>(const float* p, float v[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <>
+__device__ __forceinline__ void ld8<bf16_t>(const bf16_t* p, float v[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float v[8]);
+template <>
+__device__ __forceinline__ void st8<float>(float* p, const float v[8]) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <>
+__device__ __forceinline__ void st8<bf16_t>(bf16_t* p, const float v[8]) {
+  uint4 u;
+  u.x = pack_bf16x2(v[0], v[1]);
+  u.y = pack_bf16x2(v[2], v[3]);
+  u.z = pack_bf16x2(v[4], v[5]);
+  u.w = pack_bf16x2(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// One wave per row; 4 waves per block. C % 8 == 0.
+template <typename TIN, typename TOUT>
+__global__ void __launch_bounds__(256)
+    softmax_xent_kernel(const TIN* __restrict__ logits, int64_t ld, const int32_t* __restrict__ labels,
+                        TOUT* __restrict__ dlogits, int64_t ldd, float* __restrict__ loss_rows, int M, int C,
+                        float grad_scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const TIN* x = logits + (int64_t)row * ld;
+  float m = -INFINITY, s = 0.f;
+  for (int c = lane * 8; c < C; c += 64 * 8) {
+    float v[8];
+    ld8<TIN>(x + c, v);
+    float cm = v[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) cm = fmaxf(cm, v[j]);
+    const float nm = fmaxf(m, cm);
+    float cs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs += __expf(v[j] - nm);
+    s = s * __expf(m - nm) + cs;
+    m = nm;
+  }
+  const float gm = wave_max(m);
+  s = wave_sum(s * __expf(m - gm));
+  const float inv = 1.f / s;
+  const float lse = gm + __logf(s);
+  const int lab = labels[row];
+  if (lane == 0) {
+    float xl = 0.f;
+    if (sizeof(TIN) == 4) xl = reinterpret_cast<const float*>(x)[lab];
+    else xl = bf16_to_f32(reinterpret_cast<const bf16_t*>(x)[lab]);
+    loss_rows[row] = lse - xl;
+  }
+  TOUT* d = dlogits + (int64_t)row * ldd;
+  for (int c = lane * 8; c < C; c += 64 * 8) {
+    float v[8];
+    ld8<TIN>(x + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float p = __expf(v[j] - gm) * inv;
+      v[j] = (p - (c + j == lab ? 1.f : 0.f)) * grad_scale;
+    }
+    st8<TOUT>(d + c, v);
+  }
+}
+
+// Partial column sums over a chunk of rows: block = 256 threads covers 64 columns (16 thr x 4 cols)
+// and 16 row lanes; grid = (N/64, chunks).
+template <typename T>
+__global__ void __launch_bounds__(256)
+    col_sum_partial_kernel(const T* __restrict__ x, int64_t ld, int M, int N, int rows_per_chunk,
+                           float* __restrict__ part) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int col = blockIdx.x * 64 + tx * 4;
+  const int r0 = blockIdx.y * rows_per_chunk;
+  const int r1 = min(M, r0 + rows_per_chunk);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = r0 + ty; r < r1; r += 16) {
+    const T* p = x + (int64_t)r * ld + col;
+    if (sizeof(T) == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(p);
+      acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+    } else {
+      const uint2 u = *reinterpret_cast<const uint2*>(p);
+      acc[0] += __uint_as_float(u.x << 16);
+      acc[1] += __uint_as_float(u.x & 0xFFFF0000u);
+      acc[2] += __uint_as_float(u.y << 16);
+      acc[3] += __uint_as_float(u.y & 0xFFFF0000u);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) red[ty][tx * 4 + u] = acc[u];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+    part[(int64_t)blockIdx.y * N + blockIdx.x * 64 + threadIdx.x] = s;
+  }
+}
+
+template <typename TO>
+__global__ void __launch_bounds__(256)
+    col_sum_final_kernel(const float* __restrict__ part, int chunks, int N, TO* __restrict__ out, float scale,
+                         int accumulate) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[(int64_t)c * N + n];
+  s *= scale;
+  if (sizeof(TO) == 4) {
+    float* o = reinterpret_cast<float*>(out) + n;
+    *o = accumulate ? *o + s : s;
+  } else {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + n;
+    *o = f32_to_bf16(accumulate ? bf16_to_f32(*o) + s : s);
+  }
+}
+
+}  // namespace
+
+void launch_softmax_xent(int in_dtype, const void* logits, int64_t ld, const int32_t* labels, int out_dtype,
+                         void* dlogits, int64_t ldd, float* loss_rows, int M, int C, float grad_scale,
+                         hipStream_t s) {
+  FAN_CHECK(C % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0, "softmax_xent needs C, ld % 8 == 0");
+  const int grid = (M + 3) / 4;
+  if (in_dtype == kF32 && out_dtype == kF32)
+    hipLaunchKernelGGL((softmax_xent_kernel<float, float>), grid, 256, 0, s, (const float*)logits, ld, labels,
+                       (float*)dlogits, ldd, loss_rows, M, C, grad_scale);
+  else if (in_dtype == kF32 && out_dtype == kBF16)
+    hipLaunchKernelGGL((softmax_xent_kernel<float, bf16_t>), grid, 256, 0, s, (const float*)logits, ld, labels,
+                       (bf16_t*)dlogits, ldd, loss_rows, M, C, grad_scale);
+  else if (in_dtype == kBF16 && out_dtype == kBF16)
+    hipLaunchKernelGGL((softmax_xent_kernel<bf16_t, bf16_t>), grid, 256, 0, s, (const bf16_t*)logits, ld, labels,
+                       (bf16_t*)dlogits, ldd, loss_rows, M, C, grad_scale);
+  else
+    hipLaunchKernelGGL((softmax_xent_kernel<bf16_t, float>), grid, 256, 0, s, (const bf16_t*)logits, ld, labels,
+                       (float*)dlogits, ldd, loss_rows, M, C, grad_scale);
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+size_t col_sum_workspace_floats(int M, int N) {
+  const int chunks = (M + 255) / 256;
+  return (size_t)chunks * N;
+}
+
+void launch_col_sum(int in_dtype, const void* x, int64_t ld, int M, int N, int out_dtype, void* out, float scale,
+                    bool accumulate, float* workspace, hipStream_t s) {
+  FAN_CHECK(N % 64 == 0 && ld % 4 == 0, "col_sum needs N % 64 == 0");
+  const int rows_per_chunk = 256;
+  const int chunks = (M + rows_per_chunk - 1) / rows_per_chunk;
+  dim3 grid(N / 64, chunks);
+  if (in_dtype == kF32)
+    hipLaunchKernelGGL((col_sum_partial_kernel<float>), grid, 256, 0, s, (const float*)x, ld, M, N, rows_per_chunk,
+                       workspace);
+  else
+    hipLaunchKernelGGL((col_sum_partial_kernel<bf16_t>), grid, 256, 0, s, (const bf16_t*)x, ld, M, N,
+                       rows_per_chunk, workspace);
+  if (out_dtype == kF32)
+    hipLaunchKernelGGL((col_sum_final_kernel<float>), (N + 255) / 256, 256, 0, s, workspace, chunks, N, (float*)out,
+                       scale, accumulate ? 1 : 0);
+  else
+    hipLaunchKernelGGL((col_sum_final_kernel<bf16_t>), (N + 255) / 256, 256, 0, s, workspace, chunks, N,
+                       (bf16_t*)out, scale, accumulate ? 1 : 0);
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fan

@@ -1,0 +1,159 @@
+"""N-layer fully connected MLP + softmax cross-entropy (the reference's only model family).
+
+Reference: sw/mlp_mpi_example_f32.cpp — layers C[0] -> C[1] -> ... -> C[L] with ReLU (fuse_type), a softmax
+layer over C[L+1] = C[L] classes (sw:322, 525-531), libxsmm fc fwd/bwd (sw:498-510).
+
+MI355X-first memory layout: every layer owns ONE flat, padded parameter bucket
+``[W (C_i x C_{i+1}, row-major) | b (C_{i+1}) | pad]`` in HBM, in three dtype planes:
+``master`` (fp32, optimizer state of record), ``lp`` (bf16 compute copy, bf16 models only) and ``grad`` (fp32).
+The bucket is exactly the unit the all-reduce engine moves, so gradients are produced by the bwd-weight
+GEMM directly into the wire-ready buffer and the fused SGD epilogue writes the weights in place —
+no gather/scatter copies, no separate optimizer pass.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from ..ops import gemm as G
+from ..ops import nn as NN
+
+
+@dataclass
+class LayerBucket:
+    cin: int
+    cout: int
+    n: int            # valid elements (W + b)
+    n_pad: int
+    master: torch.Tensor
+    grad: torch.Tensor
+    lp: torch.Tensor | None
+    mom: torch.Tensor | None
+
+    @property
+    def w_master(self):
+        return self.master[: self.cin * self.cout].view(self.cin, self.cout)
+
+    @property
+    def b_master(self):
+        return self.master[self.cin * self.cout: self.n]
+
+    @property
+    def w(self):  # compute weights
+        src = self.lp if self.lp is not None else self.master
+        return src[: self.cin * self.cout].view(self.cin, self.cout)
+
+    @property
+    def b(self):
+        src = self.lp if self.lp is not None else self.master
+        return src[self.cin * self.cout: self.n]
+
+    @property
+    def gw(self):
+        return self.grad[: self.cin * self.cout].view(self.cin, self.cout)
+
+    @property
+    def gb(self):
+        return self.grad[self.cin * self.cout: self.n]
+
+
+class MLP:
+    """Manual-backprop MLP whose hot ops are the framework's HIP kernels (on GPU)."""
+
+    def __init__(self, sizes, *, dtype=torch.bfloat16, device="cpu", pad_fn=None, seed: int = 1,
+                 momentum: bool = False, init_scale: float | None = None):
+        if len(sizes) < 2:
+            raise ValueError("need at least one layer")
+        self.sizes = list(sizes)
+        self.L = len(sizes) - 1
+        self.dtype = dtype
+        self.device = torch.device(device)
+        pad_fn = pad_fn or (lambda n: (n + 255) // 256 * 256)
+        gen = torch.Generator().manual_seed(seed)
+        self.layers: list[LayerBucket] = []
+        for i in range(self.L):
+            cin, cout = sizes[i], sizes[i + 1]
+            n = cin * cout + cout
+            n_pad = pad_fn(n)
+            master = torch.zeros(n_pad, dtype=torch.float32)
+            bound = init_scale if init_scale is not None else 1.0 / math.sqrt(cin)
+            master[: cin * cout] = (torch.rand(cin * cout, generator=gen) * 2 - 1) * bound
+            master[cin * cout: n] = (torch.rand(cout, generator=gen) * 2 - 1) * bound
+            master = master.to(self.device)
+            lp = master.to(torch.bfloat16) if dtype == torch.bfloat16 else None
+            grad = torch.zeros(n_pad, dtype=torch.float32, device=self.device)
+            mom = torch.zeros(n_pad, dtype=torch.float32, device=self.device) if momentum else None
+            self.layers.append(LayerBucket(cin, cout, n, n_pad, master, grad, lp, mom))
+        self._act_mb = None
+
+    # ------------------------------------------------------------------ parameters
+    def num_params(self) -> int:
+        return sum(l.n for l in self.layers)
+
+    def flops_per_sample(self) -> int:
+        """fwd + bwd-data + bwd-weight FLOPs (2 per MAC), excluding layer 0's unneeded bwd-data
+        (the reference's GFLOP formula, sw:794-798)."""
+        f = 0
+        for i, l in enumerate(self.layers):
+            f += (6 if i > 0 else 4) * l.cin * l.cout
+        return f
+
+    def sync_lp(self):
+        for l in self.layers:
+            if l.lp is not None:
+                l.lp.copy_(l.master.to(torch.bfloat16))
+
+    def state_dict(self):
+        out = {}
+        for i, l in enumerate(self.layers):
+            out[f"fc{i}.weight"] = l.w_master.detach().clone()
+            out[f"fc{i}.bias"] = l.b_master.detach().clone()
+        return out
+
+    def load_state_dict(self, sd):
+        for i, l in enumerate(self.layers):
+            l.w_master.copy_(sd[f"fc{i}.weight"].to(l.master.dtype))
+            l.b_master.copy_(sd[f"fc{i}.bias"].to(l.master.dtype))
+        self.sync_lp()
+
+    # ------------------------------------------------------------------ activations
+    def alloc_activations(self, mb: int):
+        if self._act_mb == mb:
+            return
+        adt = self.dtype
+        dev = self.device
+        self.act = [torch.empty(mb, c, dtype=adt, device=dev) for c in self.sizes[:-1]]
+        self.logits = torch.empty(mb, self.sizes[-1], dtype=torch.float32, device=dev)
+        self.dz = [None] + [torch.empty(mb, c, dtype=adt, device=dev) for c in self.sizes[1:]]
+        self.loss_rows = torch.empty(mb, dtype=torch.float32, device=dev)
+        self._act_mb = mb
+
+    # ------------------------------------------------------------------ compute
+    def forward_layer(self, i: int):
+        l = self.layers[i]
+        out = self.act[i + 1] if i + 1 < self.L else self.logits
+        G.linear_fwd(self.act[i], l.w, l.b, out, relu=(i + 1 < self.L))
+
+    def loss_backward(self, labels, grad_scale: float):
+        NN.softmax_xent(self.logits, labels, self.dz[self.L], self.loss_rows, grad_scale)
+
+    def backward_weight(self, i: int):
+        l = self.layers[i]
+        G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
+        NN.col_sum(self.dz[i + 1], l.gb)
+
+    def backward_data(self, i: int):
+        if i == 0:
+            return
+        l = self.layers[i]
+        G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i], relu_input=self.act[i])
+
+    def forward(self, x):
+        """Inference forward (returns f32 logits)."""
+        self.alloc_activations(x.shape[0])
+        self.act[0].copy_(x)
+        for i in range(self.L):
+            self.forward_layer(i)
+        return self.logits

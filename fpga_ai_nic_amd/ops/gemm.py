@@ -1,0 +1,92 @@
+"""Fully-connected layer GEMMs on the hand-written MFMA kernels (csrc/gemm/).
+
+Weight layout is the reference's checkpoint layout: ``W[in][out]`` row-major (C[i] x C[i+1],
+sw/mlp_mpi_example_f32.cpp:396-401). The three products of a layer map onto the kernel's operand
+layouts without any transpose pass:
+
+* forward      Y[M,N]  = X[M,K] · W[K,N] (+bias, ReLU)           A K-contig, B MN-contig
+* bwd-data     dX[M,K] = dZ[M,N] · W[K,N]ᵀ  (⊙ ReLU mask of X)    A K-contig, B K-contig
+* bwd-weight   dW[K,N] = X[M,K]ᵀ · dZ[M,N]                        A MN-contig, B MN-contig
+
+GPU tensors always run the MFMA kernels (unsupported shapes raise); CPU tensors (the gloo / CPU test
+path only) use torch reference math in fp32.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
+
+_ws: dict = {}
+
+
+def _workspace(device, numel):
+    t = _ws.get(device)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        _ws[device] = t
+    return t
+
+
+def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
+    """Split K so small output grids still fill the 256 CUs (ordered, deterministic slab reduce)."""
+    tiles = (M // 128) * (N // 128)
+    if tiles == 0:
+        return 1
+    best = 1
+    for s in (2, 3, 4, 6, 8):
+        if tiles * best >= target_wg:
+            break
+        if K % (64 * s) == 0 and K // s >= 256:
+            best = s
+    return best
+
+
+def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux=None, accumulate=False,
+         split_k: int | None = None):
+    """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K]."""
+    if C.is_cuda:
+        Cx = _ext.require()
+        M = A.shape[1] if a_t else A.shape[0]
+        K = A.shape[0] if a_t else A.shape[1]
+        N = B.shape[0] if b_t else B.shape[1]
+        sk = choose_split_k(M, N, K) if split_k is None else split_k
+        if C.dtype == torch.float32 and A.dtype == torch.float32:
+            sk = 1
+        if not Cx.gemm_supported(M, N, K, A.dtype == torch.bfloat16, sk):
+            sk = 1
+        ws = _workspace(C.device, sk * M * N) if sk > 1 else None
+        Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws)
+        return C
+    # CPU reference path
+    a = (A.t() if a_t else A).float()
+    b = (B.t() if b_t else B).float()
+    r = a @ b
+    if epilogue in (EPI_BIAS, EPI_BIAS_RELU):
+        r = r + bias.float()
+    if epilogue == EPI_BIAS_RELU:
+        r = torch.relu(r)
+    if epilogue == EPI_RELU_MASK:
+        r = r * (aux.float() > 0)
+    if accumulate:
+        r = r + C.float()
+    C.copy_(r.to(C.dtype))
+    return C
+
+
+def linear_fwd(x, w, b, out, relu: bool):
+    return gemm(x, False, w, False, out, EPI_BIAS_RELU if relu else EPI_BIAS, bias=b)
+
+
+def linear_bwd_data(dz, w, out, relu_input=None):
+    """dX = dZ · Wᵀ, optionally masked by (relu_input > 0) (ReLU backward fused)."""
+    if relu_input is not None:
+        return gemm(dz, False, w, True, out, EPI_RELU_MASK, aux=relu_input)
+    return gemm(dz, False, w, True, out, EPI_NONE)
+
+
+def linear_bwd_weight(x, dz, out, accumulate=False):
+    """dW = Xᵀ · dZ (f32 out)."""
+    return gemm(x, True, dz, False, out, EPI_NONE, accumulate=accumulate)

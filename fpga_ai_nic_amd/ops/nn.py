@@ -1,0 +1,41 @@
+"""Loss and reduction kernels (csrc/nn/nn_kernels.hip) with CPU reference fallbacks."""
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+
+_ws: dict = {}
+
+
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, dlogits: torch.Tensor, loss_rows: torch.Tensor,
+                 grad_scale: float):
+    """Fused softmax + cross-entropy: writes per-row loss and dlogits = (softmax - onehot) * grad_scale."""
+    if logits.is_cuda:
+        _ext.require().softmax_xent(logits, labels, dlogits, loss_rows, float(grad_scale))
+        return
+    x = logits.float()
+    lse = torch.logsumexp(x, dim=1)
+    loss_rows.copy_(lse - x.gather(1, labels.long().view(-1, 1)).view(-1))
+    p = torch.softmax(x, dim=1)
+    p[torch.arange(x.shape[0]), labels.long()] -= 1.0
+    dlogits.copy_((p * grad_scale).to(dlogits.dtype))
+
+
+def col_sum(x: torch.Tensor, out: torch.Tensor, scale: float = 1.0, accumulate: bool = False):
+    """out[n] (+)= scale * sum_m x[m][n] (bias gradient)."""
+    if x.is_cuda:
+        C = _ext.require()
+        M, N = x.shape
+        need = C.col_sum_workspace_floats(M, N)
+        ws = _ws.get(x.device)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(max(need, 1 << 16), dtype=torch.float32, device=x.device)
+            _ws[x.device] = ws
+        C.col_sum(x, out, float(scale), bool(accumulate), ws)
+        return out
+    s = x.float().sum(0) * scale
+    if accumulate:
+        s = s + out.float()
+    out.copy_(s.to(out.dtype))
+    return out

@@ -1,0 +1,159 @@
+"""Data-parallel trainer: per-layer gradient all-reduce overlapped with backward on a side HIP stream.
+
+Reference schedule (sw/mlp_mpi_example_f32.cpp:701-787): forward all layers; softmax fwd/bwd; for layer
+i = L-1..0: backward, then issue the NIC all-reduce(+SGD) of layer i asynchronously while layer i-1's
+backward runs. MI355X mapping:
+
+* main stream: fwd GEMMs (bias+ReLU fused), softmax-xent, bwd-weight GEMM of layer i, then bwd-data GEMM;
+* comm stream (high priority): as soon as dW_i is written, the engine packs + exchanges layer i's bucket
+  (overlapping the bwd-data GEMM of layer i and the whole backward of layers < i);
+* the fused SGD epilogue of layer i waits (GPU-side event) for the bwd-data GEMM that still reads W_i;
+* the NEXT step's forward of layer i waits (GPU-side event) for that epilogue — the host never blocks.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..models.mlp import MLP
+from ..ops import wire
+from ..utils import tracing
+from .allreduce import CompressedAllReduce, Handle, _round_up
+from .transport import Transport
+
+
+class RcclAllReduce(CompressedAllReduce):
+    """Uncompressed baseline: transport all-reduce (RCCL ring/tree) + a separate SGD kernel
+    (BASELINE config 2; the reference's commented MPI_Iallreduce path, sw:615-647)."""
+
+    def __init__(self, transport: Transport, **kw):
+        kw.pop("codec", None)
+        kw.pop("algo", None)
+        super().__init__(transport, codec="raw_f32", algo="mesh", **kw)
+        self.algo = "rccl"
+
+    def layout(self, n):
+        from .allreduce import BucketLayout
+
+        n_pad = _round_up(max(n, 1), 256 * self.world)
+        return BucketLayout(n=n, n_pad=n_pad, algo="rccl", world=self.world, shard=n_pad)
+
+    def wire_bytes(self, L):
+        N = self.world
+        return 0 if N == 1 else int(2 * (N - 1) / N * L.n_pad * 4)
+
+    def _run(self, L, grad, finish, owner_fp32, allow_compat=True):
+        g = grad.view(-1)[: L.n_pad]
+        self.transport.all_reduce_(g)
+        return [lambda: finish(wire.as_bytes(g), L.n_pad, 1, 0, L.n_pad)]
+
+
+def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str = "rne", algo: str = "mesh",
+                rings: int = 1, max_slice_elems: int = 1 << 22, compat_owner_fp32: bool = False,
+                timeout_s: float = 600.0):
+    """kind: 'bfp' (compressed engine), 'raw' (engine, uncompressed fp32 wire), 'rccl' (baseline),
+    'local' (no communication: world 1)."""
+    if kind == "local" or transport is None:
+        return None
+    if kind == "rccl":
+        return RcclAllReduce(transport, timeout_s=timeout_s)
+    codec = {"bfp": f"bfp_{rounding}", "raw": "raw_f32", "raw_bf16": "raw_bf16"}[kind]
+    return CompressedAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
+                               compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s)
+
+
+class DataParallelTrainer:
+    def __init__(self, model: MLP, engine: CompressedAllReduce | None, *, lr: float = 0.1,
+                 weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
+                 loss_scale: float = 1.0, average: bool = True, profile: bool = False):
+        self.m = model
+        self.engine = engine
+        self.world = engine.world if engine is not None else 1
+        self.lr, self.wd, self.momentum, self.nesterov = lr, weight_decay, momentum, nesterov
+        self.loss_scale = loss_scale
+        # gradients are of the LOCAL mean loss; the all-reduce sums over ranks -> average with 1/N
+        self.grad_scale = (1.0 / self.world) if average else 1.0
+        self.pending: list[Handle | None] = [None] * model.L
+        self.cuda = model.device.type == "cuda"
+        self.profile = profile
+        self.times = {"fwd": 0.0, "loss": 0.0, "bwd": 0.0, "bwd_first": 0.0, "steps": 0}
+        self.step_count = 0
+
+    def _sgd_local(self, l):
+        wire.sgd(wire.as_bytes(l.grad), l.n_pad, 1, l.master, codec="raw_f32", lp=l.lp, mom=l.mom, lr=self.lr,
+                 grad_scale=self.grad_scale, weight_decay=self.wd, momentum=self.momentum, nesterov=self.nesterov,
+                 n_valid=l.n)
+
+    def step(self, x: torch.Tensor, labels: torch.Tensor):
+        m = self.m
+        mb = x.shape[0]
+        m.alloc_activations(mb)
+        m.act[0] = x
+        prof = self.profile
+        t0 = time.perf_counter()
+        with tracing.range("fwd"):
+            for i in range(m.L):
+                h = self.pending[i]
+                if h is not None:
+                    if self.cuda:
+                        h.wait()
+                    else:
+                        h.synchronize()
+                    self.pending[i] = None
+                m.forward_layer(i)
+        if prof:
+            self._sync()
+            t1 = time.perf_counter()
+            self.times["fwd"] += t1 - t0
+            t0 = t1
+        with tracing.range("loss"):
+            m.loss_backward(labels, grad_scale=self.loss_scale / mb)
+        if prof:
+            self._sync()
+            t1 = time.perf_counter()
+            self.times["loss"] += t1 - t0
+            t0 = t1
+        for i in reversed(range(m.L)):
+            l = m.layers[i]
+            with tracing.range(f"bwd{i}"):
+                m.backward_weight(i)
+                h = None
+                if self.engine is not None:
+                    h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
+                                                  grad_scale=self.grad_scale, weight_decay=self.wd,
+                                                  momentum=self.momentum, nesterov=self.nesterov, defer=True,
+                                                  name=f"fc{i}")
+                m.backward_data(i)
+                if h is not None:
+                    ev = None
+                    if self.cuda:
+                        ev = torch.cuda.Event()
+                        ev.record()
+                    self.pending[i] = h.commit(update_after=ev)
+                else:
+                    self._sgd_local(l)
+            if prof and i == m.L - 1:
+                self._sync()
+                t1 = time.perf_counter()
+                self.times["bwd_first"] += t1 - t0
+                self.times["bwd"] += t1 - t0
+                t0 = t1
+        if prof:
+            self._sync()
+            self.times["bwd"] += time.perf_counter() - t0
+        self.times["steps"] += 1
+        self.step_count += 1
+        return m.loss_rows
+
+    def _sync(self):
+        if self.cuda:
+            torch.cuda.synchronize()
+
+    def finish(self, timeout: float | None = None):
+        """Wait (host) for every outstanding all-reduce/update."""
+        for i, h in enumerate(self.pending):
+            if h is not None:
+                h.synchronize(timeout)
+                self.pending[i] = None
+        self._sync()

@@ -1,0 +1,299 @@
+"""Transports: how wire bytes move between ranks.
+
+All transports expose the same byte-level interface used by the all-reduce engine:
+``all_to_all``, ``all_gather``, ``sendrecv`` (one grouped round of point-to-point messages),
+``all_reduce_`` (uncompressed baseline), ``broadcast_``, ``barrier``.
+
+* :class:`TorchDistTransport` — ``torch.distributed`` (RCCL "nccl" backend on GPU over xGMI, gloo on CPU).
+  One process per GPU; ops are enqueued on the caller's current stream (host never blocks).
+* :class:`NativeTransport`   — the engine's own RCCL communicator (``_C.NativeComm``), bootstrapped
+  through the torch.distributed store; no ProcessGroup in the data path.
+* :class:`ThreadFabric` / :class:`ThreadTransport` — N virtual ranks as N threads of one process
+  (CPU or one GPU). This is the framework's answer to the reference's 3-NIC RTL ring testbench
+  (readme.pdf p.3 §3.2): the full engine runs against a simulated fabric without N GPUs.
+
+Reference: the NIC ring links (hw/all_reduce.sv ETH ports; sw/setup_route.sh) + Intel MPI bootstrap
+(sw/mlp_mpi_example_f32.cpp:195-309).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Sequence
+
+import torch
+import torch.distributed as dist
+
+from .. import _ext
+
+
+class Transport:
+    rank: int = 0
+    world: int = 1
+    name: str = "base"
+
+    def all_to_all(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    def all_gather(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    def sendrecv(self, sends: Sequence[tuple[torch.Tensor, int]], recvs: Sequence[tuple[torch.Tensor, int]]) -> None:
+        raise NotImplementedError
+
+    def all_reduce_(self, t: torch.Tensor) -> None:
+        raise NotImplementedError
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> None:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    def async_error(self) -> str:
+        return ""
+
+    def abort(self) -> None:
+        pass
+
+
+def _u8(t: torch.Tensor) -> torch.Tensor:
+    return t.view(torch.uint8).view(-1) if t.dtype != torch.uint8 else t.view(-1)
+
+
+class TorchDistTransport(Transport):
+    """torch.distributed (gloo on CPU, RCCL on GPU)."""
+
+    name = "torch"
+
+    def __init__(self, group=None):
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+
+    def all_to_all(self, send, recv):
+        if self.world == 1:
+            recv.copy_(send)
+            return
+        dist.all_to_all_single(_u8(recv), _u8(send), group=self.group)
+
+    def all_gather(self, send, recv):
+        if self.world == 1:
+            recv.copy_(send)
+            return
+        s, r = _u8(send), _u8(recv)
+        try:
+            dist.all_gather_into_tensor(r, s, group=self.group)
+        except (RuntimeError, NotImplementedError, AttributeError):
+            dist.all_gather(list(r.chunk(self.world)), s, group=self.group)
+
+    def sendrecv(self, sends, recvs):
+        ops = []
+        for t, peer in sends:
+            ops.append(dist.P2POp(dist.isend, _u8(t), peer, self.group))
+        for t, peer in recvs:
+            ops.append(dist.P2POp(dist.irecv, _u8(t), peer, self.group))
+        if not ops:
+            return
+        for w in dist.batch_isend_irecv(ops):
+            if w is not None:
+                w.wait()
+
+    def all_reduce_(self, t):
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+
+    def broadcast_(self, t, root=0):
+        if self.world > 1:
+            dist.broadcast(t, root, group=self.group)
+
+    def barrier(self):
+        if self.world > 1:
+            if self.backend == "nccl" and torch.cuda.is_available():
+                dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+            else:
+                dist.barrier(group=self.group)
+
+
+class NativeTransport(Transport):
+    """The engine's own RCCL communicator (ncclSend/ncclRecv groups, ncclAllToAll, ncclAllGather)."""
+
+    name = "native"
+
+    def __init__(self, rank: int | None = None, world: int | None = None, device: int | None = None, store=None):
+        C = _ext.require()
+        if rank is None:
+            rank, world = dist.get_rank(), dist.get_world_size()
+        device = torch.cuda.current_device() if device is None else device
+        key = "fan_native_comm_uid"
+        if store is None:
+            # exchange the unique id through a torch.distributed broadcast of a CPU byte tensor (gloo-free:
+            # works with any backend because we use object broadcast on the default group)
+            obj = [C.nccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
+        else:
+            if rank == 0:
+                store.set(key, C.nccl_unique_id())
+            uid = store.get(key)
+        self.rank, self.world = rank, world
+        self.comm = C.NativeComm(uid, rank, world, device)
+
+    def all_to_all(self, send, recv):
+        if self.world == 1:
+            recv.copy_(send)
+        else:
+            self.comm.all_to_all(_u8(send), _u8(recv))
+
+    def all_gather(self, send, recv):
+        if self.world == 1:
+            recv.copy_(send)
+        else:
+            self.comm.all_gather(_u8(send), _u8(recv))
+
+    def sendrecv(self, sends, recvs):
+        if sends or recvs:
+            self.comm.sendrecv([(_u8(t), p) for t, p in sends], [(_u8(t), p) for t, p in recvs])
+
+    def all_reduce_(self, t):
+        if self.world > 1:
+            self.comm.all_reduce(t)
+
+    def broadcast_(self, t, root=0):
+        if self.world > 1:
+            self.comm.broadcast(_u8(t), root)
+
+    def barrier(self):
+        one = torch.ones(1, device="cuda")
+        self.comm.all_reduce(one)
+        torch.cuda.current_stream().synchronize()
+
+    def async_error(self):
+        return self.comm.async_error()
+
+    def abort(self):
+        self.comm.abort()
+
+
+class ThreadFabric:
+    """Shared state of N virtual ranks running as threads in one process."""
+
+    def __init__(self, world: int, timeout_s: float = 120.0):
+        self.world = world
+        self.timeout = timeout_s
+        self._barrier = threading.Barrier(world, timeout=timeout_s)
+        self._slots: list = [None] * world
+        self.fault_drop_round: int | None = None  # fault injection: drop messages of this round
+
+    def transport(self, rank: int) -> "ThreadTransport":
+        return ThreadTransport(self, rank)
+
+    def run(self, fn, *args, **kwargs):
+        """Run fn(transport, *args) on every virtual rank; returns the per-rank results."""
+        results: list = [None] * self.world
+        errors: list = []
+
+        def body(r):
+            try:
+                if torch.cuda.is_available():
+                    torch.cuda.set_device(0)
+                results[r] = fn(self.transport(r), *args, **kwargs)
+            except BaseException as e:  # pragma: no cover - surfaced below
+                errors.append((r, e))
+                self._barrier.abort()
+
+        ths = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(self.world)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errors:
+            raise RuntimeError(f"virtual rank {errors[0][0]} failed: {errors[0][1]!r}") from errors[0][1]
+        return results
+
+
+class ThreadTransport(Transport):
+    name = "thread"
+
+    def __init__(self, fabric: ThreadFabric, rank: int):
+        self.f = fabric
+        self.rank = rank
+        self.world = fabric.world
+        self.round = 0
+
+    def _sync_dev(self, t: torch.Tensor | None = None):
+        if torch.cuda.is_available():
+            torch.cuda.current_stream().synchronize()
+
+    def _exchange(self, payload):
+        """Publish payload, wait for everyone, return all payloads (then a second barrier after use)."""
+        self._sync_dev()
+        self.f._slots[self.rank] = payload
+        self.f._barrier.wait()
+        return list(self.f._slots)
+
+    def _done(self):
+        self._sync_dev()
+        self.f._barrier.wait()
+
+    def all_to_all(self, send, recv):
+        s, r = _u8(send), _u8(recv)
+        n = s.numel() // self.world
+        allp = self._exchange(s)
+        for src in range(self.world):
+            r[src * n:(src + 1) * n].copy_(allp[src][self.rank * n:(self.rank + 1) * n])
+        self._done()
+
+    def all_gather(self, send, recv):
+        s, r = _u8(send), _u8(recv)
+        n = s.numel()
+        allp = self._exchange(s)
+        for src in range(self.world):
+            r[src * n:(src + 1) * n].copy_(allp[src])
+        self._done()
+
+    def sendrecv(self, sends, recvs):
+        rnd = self.round
+        self.round += 1
+        drop = self.f.fault_drop_round is not None and rnd == self.f.fault_drop_round
+        allp = self._exchange([(_u8(t), peer) for t, peer in sends])
+        # match recvs from each src in posting order
+        cursor: dict[int, int] = {}
+        for t, src in recvs:
+            k = cursor.get(src, 0)
+            mine = [m for m in allp[src] if m[1] == self.rank]
+            if k >= len(mine):
+                raise RuntimeError(f"rank {self.rank}: no message #{k} from {src}")
+            if not drop:
+                _u8(t).copy_(mine[k][0])
+            cursor[src] = k + 1
+        self._done()
+
+    def all_reduce_(self, t):
+        allp = self._exchange(t)
+        acc = torch.zeros_like(t, dtype=torch.float32)
+        for x in allp:
+            acc += x.to(torch.float32)
+        self._done()
+        t.copy_(acc.to(t.dtype))
+
+    def broadcast_(self, t, root=0):
+        allp = self._exchange(t)
+        src = allp[root].clone()
+        self._done()
+        t.copy_(src)
+
+    def barrier(self):
+        self._exchange(None)
+        self._done()
+
+
+def make_transport(kind: str = "torch", **kw) -> Transport:
+    if kind == "torch":
+        return TorchDistTransport(kw.get("group"))
+    if kind == "native":
+        return NativeTransport(**kw)
+    raise ValueError(f"unknown transport {kind!r}")

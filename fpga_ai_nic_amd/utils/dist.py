@@ -1,0 +1,65 @@
+"""Process-group bootstrap: one process per GPU (torchrun env), RCCL on GPU, gloo on CPU.
+
+Replaces the reference's MPI bootstrap (MPI_Init_thread / Comm_rank / Comm_size, sw/mlp_mpi_example_f32.cpp:195-300)
+and the IKL ring wiring (sw/setup_route.sh): on a fully connected xGMI node no route setup is needed; ring
+orders are computed by the planner.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank_world():
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), int(
+        os.environ.get("LOCAL_RANK", "0"))
+
+
+def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
+    """Initialise torch.distributed from the torchrun environment (no-op for world 1 without env).
+
+    Returns (rank, world, local_rank, device)."""
+    rank, world, local = env_rank_world()
+    use_cuda = torch.cuda.is_available() and backend != "gloo"
+    if use_cuda:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        be = backend or ("nccl" if use_cuda else "gloo")
+        kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    return rank, world, local, device
+
+
+def barrier():
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def max_over_ranks(x: float) -> float:
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return x
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cleanup():
+    if dist.is_initialized():
+        try:
+            barrier()
+        finally:
+            dist.destroy_process_group()

@@ -1,0 +1,188 @@
+"""GPU numerics of every hand-written HIP kernel against the NumPy oracle / a plain fp32 PyTorch reference."""
+import numpy as np
+import pytest
+import torch
+
+from fpga_ai_nic_amd.ops import bfp_oracle as O
+from fpga_ai_nic_amd.ops import gemm as G
+from fpga_ai_nic_amd.ops import nn as NN
+from fpga_ai_nic_amd.ops import wire
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _special_vector(n, seed=0):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal(n) * np.exp2(rng.integers(-30, 30, n))).astype(np.float32)
+    x[:16] = 0.0                                        # all-zero group
+    x[16:32] = np.float32(1e-40)                        # denormals
+    x[32:48] = rng.standard_normal(16).astype(np.float32)
+    x[40] = np.float32(3e38)                            # huge max -> others flush
+    x[48:64] = -np.float32(1.0)                         # -1 exact: trunc gives -128 edge
+    x[64:80] = np.float32(2.0) ** -126
+    x[80:96] = np.linspace(-1, 1, 16, dtype=np.float32) * 2.0 ** 100
+    return x
+
+
+@pytest.mark.parametrize("codec", ["bfp_trunc", "bfp_rne", "raw_f32", "raw_bf16"])
+@pytest.mark.parametrize("in_dtype", [torch.float32, torch.bfloat16])
+def test_pack_unpack_bitexact(C, codec, in_dtype):
+    n_s, shards = 4096, 3
+    x = _special_vector(n_s * shards)
+    xt = torch.from_numpy(x).to(in_dtype)
+    xin = xt.float().numpy()  # what the kernel sees (bf16-rounded when bf16)
+    sb = O.shard_bytes(codec, n_s)
+    out = torch.zeros(sb * shards, dtype=torch.uint8, device=DEV)
+    wire.pack(xt.to(DEV), out, n_s, codec)
+    ref = O.pack(xin, n_s, codec)
+    assert np.array_equal(out.cpu().numpy(), ref), f"pack mismatch for {codec}"
+    for od in (torch.float32, torch.bfloat16):
+        dec = torch.empty(n_s * shards, dtype=od, device=DEV)
+        wire.unpack(out, dec, n_s, codec)
+        r = O.unpack(ref, n_s * shards, n_s, codec)
+        if od == torch.bfloat16:
+            r = O.bf16_bits_to_f32(O.f32_to_bf16_bits(r))
+        got = dec.float().cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), r.view(np.uint32)) or np.array_equal(
+            np.nan_to_num(got), np.nan_to_num(r)), f"unpack mismatch {codec} {od}"
+
+
+def test_pack_random_large(C):
+    n_s = 1 << 20
+    x = torch.randn(n_s * 2, device=DEV) * 1e-3
+    out = torch.empty(O.shard_bytes("bfp_rne", n_s) * 2, dtype=torch.uint8, device=DEV)
+    wire.pack(x, out, n_s, "bfp_rne")
+    assert np.array_equal(out.cpu().numpy(), O.pack(x.cpu().numpy(), n_s, "bfp_rne"))
+
+
+@pytest.mark.parametrize("codec", ["bfp_trunc", "bfp_rne", "raw_f32", "raw_bf16"])
+@pytest.mark.parametrize("local_dtype", [torch.float32, torch.bfloat16])
+def test_reduce_bitexact(C, codec, local_dtype):
+    n_s, N, me = 2048, 5, 2
+    rng = np.random.default_rng(1)
+    parts = [rng.standard_normal(n_s).astype(np.float32) * (r + 1) for r in range(N)]
+    slots = np.concatenate([O.pack(p, n_s, codec) for p in parts])
+    local = torch.from_numpy(parts[me]).to(local_dtype)
+    sb = O.shard_bytes(codec, n_s)
+    ow = torch.zeros(sb, dtype=torch.uint8, device=DEV)
+    of = torch.zeros(n_s, dtype=torch.float32, device=DEV)
+    wire.reduce(torch.from_numpy(slots).to(DEV), N, me, local.to(DEV), ow, of, n_s, codec)
+    acc = O.reduce_slots([slots[r * sb:(r + 1) * sb] for r in range(N)], local.float().numpy(), me, codec, n_s)
+    assert np.array_equal(of.cpu().numpy(), acc)
+    assert np.array_equal(ow.cpu().numpy(), O.pack(acc, n_s, codec))
+
+
+@pytest.mark.parametrize("codec", ["bfp_trunc", "bfp_rne", "raw_f32"])
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_sgd_epilogue(C, codec, momentum):
+    n_s, N = 1024, 4
+    n_valid = n_s * N - 77
+    rng = np.random.default_rng(2)
+    g = rng.standard_normal(n_s * N).astype(np.float32)
+    w = rng.standard_normal(n_s * N).astype(np.float32)
+    m = rng.standard_normal(n_s * N).astype(np.float32) if momentum else None
+    buf = O.pack(g, n_s, codec)
+    wt = torch.from_numpy(w.copy()).to(DEV)
+    lp = torch.zeros(n_s * N, dtype=torch.bfloat16, device=DEV)
+    mt = torch.from_numpy(m.copy()).to(DEV) if momentum else None
+    wire.sgd(torch.from_numpy(buf).to(DEV), n_s, N, wt, codec=codec, lp=lp, mom=mt, lr=0.1, grad_scale=0.25,
+             weight_decay=1e-4, momentum=momentum, n_valid=n_valid, skip_shard=1, skip_period=N)
+    gd = O.unpack(buf, n_s * N, n_s, codec)
+    ref_w = w.copy()
+    for s in range(N):
+        if s == 1:
+            continue
+        lo, hi = s * n_s, min((s + 1) * n_s, n_valid)
+        nw, _ = O.sgd(w[lo:hi], gd[lo:hi], 0.1, 0.25, 1e-4, momentum, None if m is None else m[lo:hi])
+        ref_w[lo:hi] = nw
+    got = wt.cpu().numpy()
+    # fma emulated in float64 (double rounding is possible but vanishingly rare): allow 1 ulp
+    ulp = np.abs(got.view(np.int32).astype(np.int64) - ref_w.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1
+    assert np.array_equal(got[n_valid:], w[n_valid:]), "padding must not be touched"
+    assert np.array_equal(got[n_s:2 * n_s], w[n_s:2 * n_s]), "skipped shard must not be touched"
+    assert torch.equal(lp[:n_s].float().cpu(), wt[:n_s].to(torch.bfloat16).float().cpu())
+
+
+def _ref_mm(a, b):
+    return a.double() @ b.double()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (2048, 1024, 4096), (512, 4096, 1024)])
+def test_gemm_layouts_vs_fp32(C, dt, M, N, K):
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=DEV).to(dt)
+    Bkn = torch.randn(K, N, device=DEV).to(dt)
+    ref = _ref_mm(A.float(), Bkn.float())
+    tol = (2e-2 if dt == torch.bfloat16 else 1e-4) * (K ** 0.5)
+    for a_t in (False, True):
+        for b_t in (False, True):
+            Ain = A.t().contiguous() if a_t else A
+            Bin = Bkn.t().contiguous() if b_t else Bkn
+            Cout = torch.empty(M, N, device=DEV, dtype=torch.float32)
+            G.gemm(Ain, a_t, Bin, b_t, Cout, split_k=1)
+            err = (Cout.double() - ref).abs().max().item()
+            assert err < tol, f"layout a_t={a_t} b_t={b_t}: max err {err}"
+
+
+def test_gemm_asymmetric_identity(C):
+    # A = I with an asymmetric B catches C-write transposes (guide: "always A=I-check with asymmetric B")
+    n = 256
+    A = torch.eye(n, device=DEV).to(torch.bfloat16)
+    B = (torch.arange(n * n, device=DEV).float().view(n, n) % 97).to(torch.bfloat16)
+    Cout = torch.empty(n, n, device=DEV)
+    G.gemm(A, False, B, False, Cout)
+    assert torch.equal(Cout, B.float())
+
+
+def test_gemm_epilogues_and_splitk(C):
+    torch.manual_seed(1)
+    M, N, K = 512, 256, 2048
+    X = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    W = (torch.randn(K, N, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    ref = (X.float() @ W.float() + b.float())
+    for sk in (1, 2, 4):
+        Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        G.gemm(X, False, W, False, Y, G.EPI_BIAS_RELU, bias=b, split_k=sk)
+        assert (Y.float() - torch.relu(ref)).abs().max().item() < 5e-2
+    # ReLU-mask epilogue (bwd-data) with bf16 aux
+    dZ = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    act = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    dX = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    G.linear_bwd_data(dZ, W, dX, relu_input=act)
+    r = (dZ.float() @ W.float().t()) * (act.float() > 0)
+    assert (dX.float() - r).abs().max().item() < 5e-2
+    # accumulate into f32
+    dW = torch.ones(K, N, device=DEV)
+    G.linear_bwd_weight(act, dZ, dW, accumulate=True)
+    r = act.float().t() @ dZ.float() + 1.0
+    assert (dW - r).abs().max().item() < 2e-1
+
+
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.bfloat16), (torch.float32, torch.float32),
+                                          (torch.bfloat16, torch.bfloat16)])
+def test_softmax_xent(C, in_dt, out_dt):
+    torch.manual_seed(2)
+    M, Cc = 300, 1024
+    x = (torch.randn(M, Cc, device=DEV) * 3).to(in_dt)
+    y = torch.randint(0, Cc, (M,), device=DEV, dtype=torch.int32)
+    d = torch.empty(M, Cc, device=DEV, dtype=out_dt)
+    loss = torch.empty(M, device=DEV)
+    NN.softmax_xent(x, y, d, loss, 0.5)
+    xf = x.float()
+    ref_loss = torch.nn.functional.cross_entropy(xf, y.long(), reduction="none")
+    assert (loss - ref_loss).abs().max().item() < 1e-3
+    p = torch.softmax(xf, 1)
+    p[torch.arange(M), y.long()] -= 1
+    assert (d.float() - p * 0.5).abs().max().item() < 1e-2
+
+
+def test_col_sum(C):
+    torch.manual_seed(3)
+    x = torch.randn(1000, 640, device=DEV).to(torch.bfloat16)
+    out = torch.zeros(640, device=DEV)
+    NN.col_sum(x, out, 2.0)
+    assert (out - x.float().sum(0) * 2).abs().max().item() < 1e-2
