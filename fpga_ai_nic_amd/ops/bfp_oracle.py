@@ -171,11 +171,11 @@ def sgd(w: np.ndarray, g: np.ndarray, lr: float, grad_scale: float = 1.0, weight
     w = np.asarray(w, np.float32)
     g = (np.asarray(g, np.float32) * np.float32(grad_scale)).astype(np.float32)
     if weight_decay:
-        g = (np.float64(weight_decay) * w.astype(np.float64) + g).astype(np.float32)
+        g = (np.float64(np.float32(weight_decay)) * w.astype(np.float64) + g).astype(np.float32)
     new_mom = None
     if momentum:
-        m = (np.float64(momentum) * mom.astype(np.float64) + g).astype(np.float32)
+        m = (np.float64(np.float32(momentum)) * mom.astype(np.float64) + g).astype(np.float32)
         new_mom = m
-        g = (np.float64(momentum) * m.astype(np.float64) + g).astype(np.float32) if nesterov else m
+        g = (np.float64(np.float32(momentum)) * m.astype(np.float64) + g).astype(np.float32) if nesterov else m
     w = (np.float64(-np.float32(lr)) * g.astype(np.float64) + w.astype(np.float64)).astype(np.float32)
     return w, new_mom

@@ -6,6 +6,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 echo "[gpu_round] host $(hostname) start $(date)"
+# refuse to run with a stale extension (sources newer than the .so)
+if [ -n "$(find csrc -newer fpga_ai_nic_amd/_C.so -type f 2>/dev/null)" ] || [ ! -f fpga_ai_nic_amd/_C.so ]; then
+  echo "[gpu_round] _C.so is stale or missing: rebuilding"; python tools/build_ext.py -j 16 || exit 1
+fi
 python -c "import torch;print('torch', torch.__version__, torch.cuda.get_device_name(0))" &&
 timeout -k 10 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -5 gpurun_out/pytest_gpu.log
