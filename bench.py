@@ -79,6 +79,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss_rows = trainer.step(x, y)
+    t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
     trainer.finish()
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -120,6 +121,7 @@ def main():
             },
             "extra": {
                 "achieved_tflops": round(flops / 1e12, 2),
+                "host_enqueue_ms_per_step": round(t_enqueue / a.steps * 1e3, 4),
                 "grad_bytes_f32_per_step": grad_bytes,
                 "effective_allreduce_algo_bw_GBps": round(grad_bytes / (ms / 1e3) / 1e9, 2),
                 "final_loss": round(loss, 5),

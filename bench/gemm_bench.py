@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""GEMM micro-benchmark: the framework's MFMA kernels vs torch.matmul (hipBLASLt) on the MLP's shapes.
+
+Interleaved rounds in one process (guide §5.4 rule 24), random operands (rule 25), median of rounds.
+Prints one JSON line per shape.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fpga_ai_nic_amd.ops import gemm as G  # noqa: E402
+
+# (name, M, N, K, a_t, b_t, epilogue) for MLP 1024-4096-4096-1024 at MB=2048
+MLP_SHAPES = [
+    ("fwd0", 2048, 4096, 1024, False, False, G.EPI_BIAS_RELU),
+    ("fwd1", 2048, 4096, 4096, False, False, G.EPI_BIAS_RELU),
+    ("fwd2", 2048, 1024, 4096, False, False, G.EPI_BIAS),
+    ("bwdw2", 4096, 1024, 2048, True, False, G.EPI_NONE),
+    ("bwdw1", 4096, 4096, 2048, True, False, G.EPI_NONE),
+    ("bwdw0", 1024, 4096, 2048, True, False, G.EPI_NONE),
+    ("bwdd2", 2048, 4096, 1024, False, True, G.EPI_RELU_MASK),
+    ("bwdd1", 2048, 4096, 4096, False, True, G.EPI_RELU_MASK),
+    ("sq4k", 4096, 4096, 4096, False, True, G.EPI_NONE),
+    ("sq8k", 8192, 8192, 8192, False, True, G.EPI_NONE),
+]
+
+
+def time_fn(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--shapes", default="")
+    ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
+    a = ap.parse_args()
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    torch.manual_seed(0)
+    for name, M, N, K, a_t, b_t, epi in MLP_SHAPES:
+        if a.shapes and name not in a.shapes.split(","):
+            continue
+        if a.dtype == "f32" and K > 4096:
+            continue
+        A = (torch.rand(K, M, device="cuda") * 2 - 1).to(dt) if a_t else (torch.rand(M, K, device="cuda") * 2 - 1).to(dt)
+        B = (torch.rand(N, K, device="cuda") * 2 - 1).to(dt) if b_t else (torch.rand(K, N, device="cuda") * 2 - 1).to(dt)
+        out_dt = torch.float32 if epi == G.EPI_NONE else dt
+        C = torch.empty(M, N, device="cuda", dtype=out_dt)
+        bias = (torch.rand(N, device="cuda") - 0.5).to(dt)
+        aux = (torch.rand(M, N, device="cuda") - 0.5).to(out_dt)
+        kw = {}
+        if epi in (G.EPI_BIAS, G.EPI_BIAS_RELU):
+            kw["bias"] = bias
+        if epi == G.EPI_RELU_MASK:
+            kw["aux"] = aux
+        Am = A.t() if a_t else A
+        Bm = B.t() if b_t else B
+
+        def mine():
+            G.gemm(A, a_t, B, b_t, C, epi, **kw)
+
+        def ref():
+            r = torch.matmul(Am, Bm)
+            if epi in (G.EPI_BIAS, G.EPI_BIAS_RELU):
+                r = r + bias
+            if epi == G.EPI_BIAS_RELU:
+                r = torch.relu_(r)
+            return r
+
+        def ref_mm_only():
+            torch.matmul(Am, Bm)
+
+        if a.sweep and dt == torch.bfloat16:
+            res = {}
+            for tile in ((256, 256), (256, 128), (128, 256), (128, 128)):
+                for sk in (1, 2, 4):
+                    if M % tile[0] or N % tile[1] or K % (64 * sk):
+                        continue
+                    fn = lambda t=tile, s=sk: G.gemm(A, a_t, B, b_t, C, epi, split_k=s, tile=t, **kw)  # noqa: E731
+                    fn()
+                    res[f"{tile[0]}x{tile[1]}/s{sk}"] = round(
+                        statistics.median(time_fn(fn, a.iters) for _ in range(3)), 2)
+            best = min(res, key=res.get)
+            print(json.dumps({"shape": name, "sweep_us": res, "best": best,
+                              "auto_plan": G._ext.require().gemm_plan(M, N, K)}), flush=True)
+        mine(); ref(); torch.cuda.synchronize()
+        err = (C.float() - (ref().float() * ((aux > 0) if epi == G.EPI_RELU_MASK else 1))).abs().max().item()
+        tm, tr, tmm = [], [], []
+        for _ in range(a.rounds):
+            tm.append(time_fn(mine, a.iters))
+            tr.append(time_fn(ref, a.iters))
+            tmm.append(time_fn(ref_mm_only, a.iters))
+        flop = 2.0 * M * N * K
+        m, r, rm = statistics.median(tm), statistics.median(tr), statistics.median(tmm)
+        plan = G._ext.require().gemm_plan(M, N, K, 0) if dt == torch.bfloat16 else None
+        print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "a_t": a_t, "b_t": b_t, "epi": epi,
+                          "dtype": a.dtype, "plan": plan,
+                          "mine_us": round(m, 2), "mine_tflops": round(flop / m / 1e6, 1),
+                          "torch_fused_us": round(r, 2), "torch_matmul_only_us": round(rm, 2),
+                          "torch_matmul_tflops": round(flop / rm / 1e6, 1), "speedup_vs_torch_fused": round(r / m, 3),
+                          "max_abs_err": err}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -29,9 +29,18 @@ struct GemmArgs {
   int epilogue;
   bool c_bf16;       // output dtype (bf16 or f32)
   bool accumulate;   // C += result (f32 output only)
-  int split_k;       // >1: K split over workgroups, fp32 partial slabs + ordered reduce
+  int split_k;       // 0: auto; >=1: K split over workgroups (fp32 partial slabs + ordered reduce)
   void* workspace;   // split-K slabs: split_k * M * N floats
+  int tile_bm = 0;   // 0: automatic tile choice; else force BM x BN (128/256)
+  int tile_bn = 0;
 };
+
+struct GemmPlan {
+  int bm, bn, split_k;  // bm == 0: unsupported
+};
+
+// Tile / split-K choice for a shape (split_k <= 0: automatic).
+GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm = 0, int tile_bn = 0);
 
 // Returns false if the shape is not supported by the MFMA path (caller must then error out).
 bool gemm_bf16_supported(const GemmArgs& a);

@@ -1,18 +1,27 @@
 // bf16 MFMA GEMM for gfx950 (v_mfma_f32_16x16x32_bf16), LDS-tiled, global_load_lds staged.
 //
-// Block tile 128x128x64, 256 threads = 4 waves in a 2x2 arrangement, each wave a 64x64 sub-tile
-// (4x4 MFMA 16x16 tiles = 64 accumulator VGPRs). Operand tiles are staged global->LDS with
-// global_load_lds_dwordx4 (no VGPR round trip) into a double-buffered LDS ring (64 KiB):
-//   K-contiguous operand  : LDS image [128 rows][64 k] (128-B rows), 16-B chunk c of row r stored at
-//                           c ^ ((r>>1)&7)  -> ds_read_b128 fragment reads are conflict-free.
-//   MN-contiguous operand : LDS image [64 k][128 cols] (256-B rows), 32-B block b of row k stored at
-//                           b ^ ((k&3) | ((k>>3)&1)<<2) -> ds_read_b64_tr_b16 (hardware transpose)
-//                           fragment reads are conflict-free.
-// glds writes LDS linearly (wave base + lane*16), so the swizzle is applied to the per-lane GLOBAL
-// source address and the matching XOR on the read (both sides, one involution).
-// Workgroup -> tile mapping is XCD-aware: the 8 round-robin XCD groups each get a contiguous
-// run of tiles so neighbouring tiles (shared A rows) hit the same L2.
+// Structure (one workgroup = 8 waves = 512 threads; tile BM x BN x 64):
+//   * operand tiles are staged global->LDS by global_load_lds_dwordx4 (no VGPR round trip) into an
+//     S-deep LDS ring (S = 3 when it fits in 160 KiB, else 2). Each K-tile iteration does
+//         s_waitcnt vmcnt(G*(S-2)) ; s_barrier ; issue stage kt+S-1 ; ds_read + MFMA on stage kt
+//     i.e. ONE raw barrier per K-tile and a counted vmcnt that keeps the next stage's DMA in flight
+//     across the barrier (never __syncthreads() in the loop: it would drain vmcnt to 0).
+//   * K-contiguous operand image: [rows][64 k] (128-B rows), 16-B chunk c of row r at c ^ ((r>>1)&7):
+//     ds_read_b128 fragment reads are bank-conflict-free.
+//   * MN-contiguous operand image: 128-column halves, each [64 k][128] (256-B rows), 32-B block b of
+//     row k at b ^ ((k&3) | ((k>>3)&1)<<2): ds_read_b64_tr_b16 (hardware transpose) reads are conflict-free.
+//     glds writes LDS linearly, so every swizzle is applied to the per-lane GLOBAL source address and
+//     mirrored on the read (one involution on both sides).
+//   * waves are arranged WM x WN; each owns a (BM/WM) x (BN/WN) sub-tile of 16x16 MFMA tiles; MFMA
+//     clusters run at s_setprio 1.
+//   * workgroup -> tile map is XCD-aware (bijective): each of the 8 round-robin XCD groups gets a
+//     contiguous run of tiles so neighbouring tiles share A rows in one L2.
+//   * epilogue: accumulators are staged through LDS per 16-row block and written as coalesced 16-B
+//     (f32) / 8-B (bf16) row segments, with bias / ReLU / ReLU-mask (bwd-data) / accumulate fused.
+//   * split-K: K is split over workgroups, f32 partial slabs + an ordered (deterministic) reduce kernel
+//     that applies the same epilogue.
 #include "gemm/gemm.h"
+#include "gemm/glds.h"
 
 namespace fan {
 namespace {
@@ -24,53 +33,57 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
 
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile (16 KiB)
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;  // 64 KiB
+constexpr int BK = 64;
+constexpr int NT = 512;
+constexpr int NWAVE = 8;
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
-// Stage one operand tile (outer extent 128 starting at o0, k extent 64 starting at k0).
-template <bool KCONTIG>
-__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int64_t ld, int o0, int k0, char* lds_tile,
+template <int OUTER>
+struct OpTile {
+  static constexpr int BYTES = OUTER * BK * 2;
+  static constexpr int GLDS = BYTES / (NT * 16);  // glds instructions per thread per stage
+};
+
+// Stage one operand tile (outer extent OUTER from o0, k extent 64 from k0).
+template <bool KCONTIG, int OUTER>
+__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int64_t ld, int o0, int k0, char* lds,
                                            int wave, int lane) {
+  const int t = wave * 64 + lane;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int t = wave * 64 + lane;  // 0..255 within this block-instruction
+  for (int i = 0; i < OpTile<OUTER>::GLDS; ++i) {
     const bf16_t* src;
     if (KCONTIG) {
-      const int row = i * 32 + (t >> 3);
-      const int cs = t & 7;
-      const int c = cs ^ ((row >> 1) & 7);
+      const int row = i * 64 + (t >> 3);  // 8 KiB per block-instruction = 64 rows of 128 B
+      const int c = (t & 7) ^ ((row >> 1) & 7);
       src = g + (int64_t)(o0 + row) * ld + k0 + c * 8;
     } else {
-      const int krow = i * 16 + (t >> 4);
+      const int half = i >> 1;                  // 128-column half
+      const int krow = (i & 1) * 32 + (t >> 4);  // 8 KiB = 32 k-rows of 256 B
       const int cs = t & 15;
       const int blk = (cs >> 1) ^ mn_swz(krow);
-      src = g + (int64_t)(k0 + krow) * ld + o0 + blk * 16 + (cs & 1) * 8;
+      src = g + (int64_t)(k0 + krow) * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8;
     }
-    char* dst = lds_tile + i * 4096 + wave * 1024;  // wave-uniform base; hw adds lane*16
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)dst, 16, 0, 0);
+    glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + i * 8192 + wave * 1024)));
   }
 }
 
-// Fragment (8 bf16 along k) for a 16-row/col subtile at outer offset o (within the tile), k-step ks.
 template <bool KCONTIG>
-__device__ __forceinline__ s16x8 read_frag(const char* lds_tile, int o, int ks, int lane) {
+__device__ __forceinline__ s16x8 read_frag(const char* lds, int o, int ks, int lane) {
   if (KCONTIG) {
     const int row = o + (lane & 15);
     const int chunk = ks * 4 + (lane >> 4);
-    const int off = row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
-    return *reinterpret_cast<const s16x8*>(lds_tile + off);
+    return *reinterpret_cast<const s16x8*>(lds + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
   } else {
+    const char* h = lds + (o >> 7) * (64 * 256);
+    const int oo = o & 127;
     const int q = (lane & 15) >> 2, p = lane & 3;
     const int kb = ks * 32 + 8 * (lane >> 4) + q;
-    const int blk = o >> 4;
+    const int blk = oo >> 4;
     const int off0 = kb * 256 + ((blk ^ mn_swz(kb)) << 5) + 8 * p;
     const int off1 = (kb + 4) * 256 + ((blk ^ mn_swz(kb + 4)) << 5) + 8 * p;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(lds_tile + off0));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(lds_tile + off1));
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(h + off0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(h + off1));
     s16x8 r;
     r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
     r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -86,25 +99,71 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 template <typename TC>
-__device__ __forceinline__ void store_c(TC* p, float v);
+struct Out;
 template <>
-__device__ __forceinline__ void store_c<float>(float* p, float v) { *p = v; }
+struct Out<float> {
+  __device__ static __forceinline__ void load4(const float* p, float v[4]) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  __device__ static __forceinline__ void store4(float* p, const float v[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
 template <>
-__device__ __forceinline__ void store_c<bf16_t>(bf16_t* p, float v) { *p = f32_to_bf16(v); }
+struct Out<bf16_t> {
+  __device__ static __forceinline__ void load4(const bf16_t* p, float v[4]) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xFFFF0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xFFFF0000u);
+  }
+  __device__ static __forceinline__ void store4(bf16_t* p, const float v[4]) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+  }
+};
 
-template <typename TC>
-__device__ __forceinline__ float load_c(const TC* p);
-template <>
-__device__ __forceinline__ float load_c<float>(const float* p) { return *p; }
-template <>
-__device__ __forceinline__ float load_c<bf16_t>(const bf16_t* p) { return bf16_to_f32(*p); }
+template <int EPI, typename TC, bool ACCUM>
+__device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
+                                     const TC* __restrict__ aux, int64_t ldaux, int row, int col) {
+  if (EPI == kEpiBias || EPI == kEpiBiasRelu) {
+    const uint2 u = *reinterpret_cast<const uint2*>(bias + col);
+    v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xFFFF0000u);
+    v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xFFFF0000u);
+  }
+  if (EPI == kEpiBiasRelu) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = fmaxf(v[u], 0.f);
+  }
+  if (EPI == kEpiReluMask) {
+    float m[4];
+    Out<TC>::load4(aux + (int64_t)row * ldaux + col, m);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = m[u] > 0.f ? v[u] : 0.f;
+  }
+  TC* p = C + (int64_t)row * ldc + col;
+  if (ACCUM) {
+    float o[4];
+    Out<TC>::load4(p, o);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] += o[u];
+  }
+  Out<TC>::store4(p, v);
+}
 
-template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
 __global__ void __launch_bounds__(NT, 2)
     gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                      TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                      int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws) {
+  constexpr int A_BYTES = OpTile<BM>::BYTES, B_BYTES = OpTile<BN>::BYTES;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int S = (3 * STAGE <= 160 * 1024) ? 3 : 2;
+  constexpr int G = OpTile<BM>::GLDS + OpTile<BN>::GLDS;
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave sub-tile
+  constexpr int MI = WTM / 16, NJ = WTN / 16;
+  static_assert(WM * WN == NWAVE, "8 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+
   const int tiles_n = N / BN;
   const int tiles = (M / BM) * tiles_n;
   const int nwg = tiles * split_k;
@@ -119,86 +178,115 @@ __global__ void __launch_bounds__(NT, 2)
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue
-  stage_tile<AK>(A, lda, m0, kbeg, smem, wave, lane);
-  stage_tile<BKC>(B, ldb, n0, kbeg, smem + TILE_BYTES, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // prologue: stages 0..S-2 in flight
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) {
+    if (s < nk) {
+      char* st = smem + s * STAGE;
+      stage_tile<AK, BM>(A, lda, m0, kbeg + s * BK, st, wave, lane);
+      stage_tile<BKC, BN>(B, ldb, n0, kbeg + s * BK, st + A_BYTES, wave, lane);
+    }
+  }
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    char* sa = smem + cur * STAGE_BYTES;
-    char* sb = sa + TILE_BYTES;
-    if (kt + 1 < nk) {
-      char* na = smem + (cur ^ 1) * STAGE_BYTES;
-      stage_tile<AK>(A, lda, m0, kbeg + (kt + 1) * BK, na, wave, lane);
-      stage_tile<BKC>(B, ldb, n0, kbeg + (kt + 1) * BK, na + TILE_BYTES, wave, lane);
+    // retire stage kt (this wave's DMA), leaving the younger stages in flight
+    if (S == 3 && kt + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      s16x8 af[4], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag<AK>(sa, wm * 64 + i * 16, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag<BKC>(sb, wn * 64 + j * 16, ks, lane);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
-                                                              __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();  // every wave retired stage kt and finished computing kt-1
+    if (kt + S - 1 < nk) {
+      char* st = smem + ((kt + S - 1) % S) * STAGE;
+      stage_tile<AK, BM>(A, lda, m0, kbeg + (kt + S - 1) * BK, st, wave, lane);
+      stage_tile<BKC, BN>(B, ldb, n0, kbeg + (kt + S - 1) * BK, st + A_BYTES, wave, lane);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    const char* sa = smem + (kt % S) * STAGE;
+    const char* sb = sa + A_BYTES;
+    if constexpr (MI * NJ <= 16) {
+      // issue the fragment reads of BOTH k-steps up front: the k-step-1 reads overlap the k-step-0 MFMAs
+      // (hipcc emits counted lgkmcnt waits per consumer)
+      s16x8 af[2][MI], bfr[2][NJ];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[ks][i] = read_frag<AK>(sa, wm * WTM + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[ks][j] = read_frag<BKC>(sb, wn * WTN + j * 16, ks, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ks][i]),
+                                                                __builtin_bit_cast(bf16x8, bfr[ks][j]), acc[i][j],
+                                                                0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else {
+      // 128-accumulator tiles: one k-step of fragments live at a time (keeps VGPRs < 256 and leaves
+      // register-file room for a co-resident communication wave on each SIMD)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        s16x8 af[MI], bfr[NJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = read_frag<AK>(sa, wm * WTM + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<BKC>(sb, wn * WTN + j * 16, ks, lane);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                                __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0,
+                                                                0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
   }
 
-  // epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile
-  const int col_l = lane & 15;
-  const int row_l = (lane >> 4) * 4;
-  if (SPLIT) {
-    float* slab = ws + (int64_t)ksplit * M * N;
+  // ---------------- epilogue through LDS (per wave region, one 16-row block at a time)
+  __syncthreads();  // all waves done reading the operand ring
+  constexpr int EW = WTN + 4;  // staged row stride in floats (16-B aligned, breaks bank aliasing)
+  float* stg = reinterpret_cast<float*>(smem) + wave * (16 * EW);
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  constexpr int C4 = WTN / 4;          // float4 chunks per staged row
+  constexpr int RPI = 64 / C4;         // rows covered per pass by the wave
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + j * 16 + col_l;
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * 64 + i * 16 + row_l + r;
-          slab[(int64_t)row * N + col] = acc[i][j][r];
-        }
-      }
-    return;
-  }
+      for (int r = 0; r < 4; ++r) stg[(row_l + r) * EW + j * 16 + col_l] = acc[i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own LDS writes landed (wave-private region)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wn * 64 + j * 16 + col_l;
-    float bv = 0.f;
-    if (EPI == kEpiBias || EPI == kEpiBiasRelu) bv = bf16_to_f32(bias[col]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + row_l + r;
-        float v = acc[i][j][r];
-        if (EPI == kEpiBias || EPI == kEpiBiasRelu) v += bv;
-        if (EPI == kEpiBiasRelu) v = fmaxf(v, 0.f);
-        if (EPI == kEpiReluMask) v = load_c<TC>(aux + (int64_t)row * ldaux + col) > 0.f ? v : 0.f;
-        TC* p = C + (int64_t)row * ldc + col;
-        if (ACCUM) v += load_c<TC>(p);
-        store_c<TC>(p, v);
+    for (int pass = 0; pass < 16 / RPI; ++pass) {
+      const int rr = pass * RPI + lane / C4;
+      const int cc = (lane % C4) * 4;
+      const float4 q = *reinterpret_cast<const float4*>(stg + rr * EW + cc);
+      float v[4] = {q.x, q.y, q.z, q.w};
+      const int row = m0 + wm * WTM + i * 16 + rr;
+      const int col = n0 + wn * WTN + cc;
+      if (SPLIT) {
+        float* slab = ws + (int64_t)ksplit * M * N;
+        *reinterpret_cast<float4*>(slab + (int64_t)row * N + col) = q;
+      } else {
+        epi4<EPI, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
       }
     }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 }
 
@@ -217,48 +305,44 @@ __global__ void __launch_bounds__(256)
       s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
     float v[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (EPI == kEpiBias || EPI == kEpiBiasRelu) v[u] += bf16_to_f32(bias[col + u]);
-      if (EPI == kEpiBiasRelu) v[u] = fmaxf(v[u], 0.f);
-      if (EPI == kEpiReluMask) v[u] = load_c<TC>(aux + (int64_t)row * ldaux + col + u) > 0.f ? v[u] : 0.f;
-      TC* p = C + (int64_t)row * ldc + col + u;
-      if (ACCUM) v[u] += load_c<TC>(p);
-      store_c<TC>(p, v[u]);
-    }
+    epi4<EPI, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
   }
 }
 
-template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
-void launch_typed(const GemmArgs& a, hipStream_t s) {
+template <int BM, int BN>
+constexpr int lds_bytes() {
+  constexpr int st = (BM + BN) * BK * 2;
+  return ((3 * st <= 160 * 1024) ? 3 : 2) * st;
+}
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
+void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   const int tiles = (a.M / BM) * (a.N / BN);
-  const int sk = a.split_k > 1 ? a.split_k : 1;
   const int grid = tiles * sk;
+  constexpr int lds = lds_bytes<BM, BN>();
   if (sk > 1) {
-    hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKC, EPI, TC, ACCUM, true>), grid, NT, LDS_BYTES, s,
-                       (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
+    auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, true>;
+    FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL(k, grid, NT, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
                        (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace);
     hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
                        (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
                        a.ldaux, a.M, a.N);
   } else {
-    hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKC, EPI, TC, ACCUM, false>), grid, NT, LDS_BYTES, s,
-                       (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
+    auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>;
+    FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL(k, grid, NT, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
                        (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1, (float*)nullptr);
   }
 }
 
-template <bool AK, bool BKC>
-void launch_layout(const GemmArgs& a, hipStream_t s) {
-#define FAN_EPI_CASE(E)                                                       \
-  case E:                                                                     \
-    if (a.c_bf16) {                                                           \
-      launch_typed<AK, BKC, E, bf16_t, false>(a, s);                          \
-    } else if (a.accumulate) {                                                \
-      launch_typed<AK, BKC, E, float, true>(a, s);                            \
-    } else {                                                                  \
-      launch_typed<AK, BKC, E, float, false>(a, s);                           \
-    }                                                                         \
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC>
+void launch_epi(const GemmArgs& a, int sk, hipStream_t s) {
+#define FAN_EPI_CASE(E)                                                        \
+  case E:                                                                      \
+    if (a.c_bf16) launch_typed<BM, BN, WM, WN, AK, BKC, E, bf16_t, false>(a, sk, s); \
+    else if (a.accumulate) launch_typed<BM, BN, WM, WN, AK, BKC, E, float, true>(a, sk, s); \
+    else launch_typed<BM, BN, WM, WN, AK, BKC, E, float, false>(a, sk, s);  \
     break;
   switch (a.epilogue) {
     FAN_EPI_CASE(kEpiNone)
@@ -270,28 +354,71 @@ void launch_layout(const GemmArgs& a, hipStream_t s) {
 #undef FAN_EPI_CASE
 }
 
+template <bool AK, bool BKC>
+void launch_tile(const GemmArgs& a, int bm, int bn, int sk, hipStream_t s) {
+  if (bm == 256 && bn == 256) launch_epi<256, 256, 2, 4, AK, BKC>(a, sk, s);
+  else if (bm == 256 && bn == 128) launch_epi<256, 128, 4, 2, AK, BKC>(a, sk, s);
+  else if (bm == 128 && bn == 256) launch_epi<128, 256, 2, 4, AK, BKC>(a, sk, s);
+  else launch_epi<128, 128, 2, 4, AK, BKC>(a, sk, s);
+}
+
 }  // namespace
 
+GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn) {
+  GemmPlan p{0, 0, 1};
+  if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % BK) return p;
+  // Measured on MI355X (bench/gemm_bench.py --sweep, MLP shapes + 4k/8k squares): take the largest tile
+  // that still gives >= one workgroup per CU (256), preferring 128x256 over 256x128; split K only when
+  // even 128x128 tiles leave more than half the CUs idle (split-K costs an f32 slab round trip).
+  const int cand[4][2] = {{256, 256}, {128, 256}, {256, 128}, {128, 128}};
+  int best = -1;
+  for (int c = 0; c < 4 && best < 0; ++c) {
+    const int bm = cand[c][0], bn = cand[c][1];
+    if (M % bm || N % bn) continue;
+    if (tile_bm > 0 && (bm != tile_bm || bn != tile_bn)) continue;
+    if (tile_bm > 0 || (M / bm) * (N / bn) >= kNumCU) best = c;
+  }
+  if (best < 0) {  // small output: the tile with the most workgroups
+    for (int c = 3; c >= 0 && best < 0; --c) {
+      const int bm = cand[c][0], bn = cand[c][1];
+      if (M % bm || N % bn) continue;
+      if (tile_bm > 0 && (bm != tile_bm || bn != tile_bn)) continue;
+      best = c;
+    }
+  }
+  if (best < 0) return p;
+  const int tiles = (M / cand[best][0]) * (N / cand[best][1]);
+  int sk = 1;
+  if (split_k > 0) {
+    sk = split_k;
+    if (K % (BK * sk)) return p;
+  } else if (tiles * 2 <= kNumCU) {
+    while (tiles * sk < kNumCU && sk < 8 && K % (BK * sk * 2) == 0 && K / (sk * 2) >= 512) sk *= 2;
+  }
+  p.bm = cand[best][0];
+  p.bn = cand[best][1];
+  p.split_k = sk;
+  return p;
+}
+
 bool gemm_bf16_supported(const GemmArgs& a) {
-  const int sk = a.split_k > 1 ? a.split_k : 1;
-  if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
-  if (a.M % BM || a.N % BN || a.K % (BK * sk)) return false;
-  // 16-byte alignment of every staged row (glds dwordx4) and of the bases.
-  if (a.lda % 8 || a.ldb % 8) return false;
+  const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn);
+  if (p.bm == 0) return false;
+  if (a.lda % 8 || a.ldb % 8 || a.ldc % 4 || (a.aux && a.ldaux % 4)) return false;
   if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return false;
+  if (((uintptr_t)a.C) & (a.c_bf16 ? 7 : 15)) return false;
   if (a.accumulate && a.c_bf16) return false;
-  if (sk > 1 && (a.workspace == nullptr || (a.N % 4) || (a.ldc != a.N))) return false;
+  if (p.split_k > 1 && a.workspace == nullptr) return false;
   return true;
 }
 
 void launch_gemm_bf16(const GemmArgs& a, hipStream_t s) {
   FAN_CHECK(gemm_bf16_supported(a), "gemm_bf16: unsupported shape/layout (need M,N % 128 == 0, K % 64 == 0)");
-  static bool attr_set = false;
-  (void)attr_set;
-  if (a.a_kcontig && a.b_kcontig) launch_layout<true, true>(a, s);
-  else if (a.a_kcontig && !a.b_kcontig) launch_layout<true, false>(a, s);
-  else if (!a.a_kcontig && a.b_kcontig) launch_layout<false, true>(a, s);
-  else launch_layout<false, false>(a, s);
+  const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn);
+  if (a.a_kcontig && a.b_kcontig) launch_tile<true, true>(a, p.bm, p.bn, p.split_k, s);
+  else if (a.a_kcontig && !a.b_kcontig) launch_tile<true, false>(a, p.bm, p.bn, p.split_k, s);
+  else if (!a.a_kcontig && a.b_kcontig) launch_tile<false, true>(a, p.bm, p.bn, p.split_k, s);
+  else launch_tile<false, false>(a, p.bm, p.bn, p.split_k, s);
   FAN_HIP_CHECK(hipGetLastError());
 }
 

@@ -8,6 +8,7 @@
 // Within each 16-wide k chunk lane l feeds k = 4*(l>>4) + i to MFMA i (a consistent permutation of
 // the k order for A and B), so every fragment read is one ds_read_b128.
 #include "gemm/gemm.h"
+#include "gemm/glds.h"
 
 namespace fan {
 namespace {
@@ -33,7 +34,7 @@ __device__ __forceinline__ void stage(const float* __restrict__ g, int64_t ld, i
       const int cs = t & 7;
       const int c = cs ^ swz(row);
       const float* src = g + (int64_t)(o0 + row) * ld + k0 + c * 4;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(tile + i * 4096 + wave * 1024), 16, 0, 0);
+      glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(tile + i * 4096 + wave * 1024)));
     }
   } else {
     float4 v[4];

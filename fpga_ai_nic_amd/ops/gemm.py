@@ -45,20 +45,26 @@ def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
 
 
 def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux=None, accumulate=False,
-         split_k: int | None = None):
-    """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K]."""
+         split_k: int | None = None, tile: tuple | None = None):
+    """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
+    ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only)."""
     if C.is_cuda:
         Cx = _ext.require()
         M = A.shape[1] if a_t else A.shape[0]
         K = A.shape[0] if a_t else A.shape[1]
         N = B.shape[0] if b_t else B.shape[1]
-        sk = choose_split_k(M, N, K) if split_k is None else split_k
-        if C.dtype == torch.float32 and A.dtype == torch.float32:
+        ws = None
+        sk = 0 if split_k is None else int(split_k)
+        tbm, tbn = tile if tile is not None else (0, 0)
+        if A.dtype == torch.bfloat16:
+            bm, bn, sk = Cx.gemm_plan(M, N, K, sk, tbm, tbn)
+            if bm == 0:
+                raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
+            if sk > 1:
+                ws = _workspace(C.device, sk * M * N)
+        else:
             sk = 1
-        if not Cx.gemm_supported(M, N, K, A.dtype == torch.bfloat16, sk):
-            sk = 1
-        ws = _workspace(C.device, sk * M * N) if sk > 1 else None
-        Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws)
+        Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, tbm, tbn)
         return C
     # CPU reference path
     a = (A.t() if a_t else A).float()

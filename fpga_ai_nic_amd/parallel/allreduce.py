@@ -191,10 +191,13 @@ class CompressedAllReduce:
         self.cuda = self.device.type == "cuda"
         self.orders = ring_orders(self.world, rings) if algo == "ring" else [list(range(self.world))]
         self.rings = len(self.orders)
-        if self.cuda:
+        # world 1: nothing to overlap -> run inline on the caller's stream (no side stream, no event packets)
+        self.inline = self.world == 1
+        if self.cuda and not self.inline:
             self.stream = stream or torch.cuda.Stream(device=self.device, priority=stream_priority)
         else:
             self.stream = None
+        self._events: list = []
         self._scratch: dict = {}
         self._slot = 0
         self.fault = faults.FaultInjector.from_env()
@@ -288,11 +291,11 @@ class CompressedAllReduce:
         self.stats["requests"] += 1
         self.stats["wire_bytes"] += self.wire_bytes(L)
         self.stats["logical_bytes"] += L.n * 4
-        if not self.cuda:
+        if not self.cuda or self.inline:
             thunks = comm_fn()
             h = Handle(self, slot, None, name, pending=thunks)
             return h if defer else h.commit()
-        ready = torch.cuda.Event()
+        ready = self._event()
         ready.record(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ready)
@@ -300,8 +303,18 @@ class CompressedAllReduce:
         h = Handle(self, slot, None, name, pending=thunks)
         return h if defer else h.commit(update_after)
 
+    def _event(self):
+        """Events are recycled round-robin (a pool deeper than the requests in flight)."""
+        if len(self._events) < 4 * NUM_SLOTS:
+            e = torch.cuda.Event()
+            self._events.append(e)
+            return e
+        e = self._events.pop(0)
+        self._events.append(e)
+        return e
+
     def _run_thunks(self, thunks, update_after=None):
-        if not self.cuda:
+        if not self.cuda or self.inline:
             for t in thunks:
                 t()
             return None
@@ -310,7 +323,7 @@ class CompressedAllReduce:
                 self.stream.wait_event(update_after)
             for t in thunks:
                 t()
-            done = torch.cuda.Event()
+            done = self._event()
             done.record(self.stream)
         return done
 

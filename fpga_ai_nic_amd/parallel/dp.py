@@ -75,6 +75,7 @@ class DataParallelTrainer:
         # gradients are of the LOCAL mean loss; the all-reduce sums over ranks -> average with 1/N
         self.grad_scale = (1.0 / self.world) if average else 1.0
         self.pending: list[Handle | None] = [None] * model.L
+        self.last_handle: Handle | None = None
         self.cuda = model.device.type == "cuda"
         self.profile = profile
         self.times = {"fwd": 0.0, "loss": 0.0, "bwd": 0.0, "bwd_first": 0.0, "steps": 0}
@@ -93,14 +94,19 @@ class DataParallelTrainer:
         prof = self.profile
         t0 = time.perf_counter()
         with tracing.range("fwd"):
+            # Weights of every layer must be updated before its forward. All requests of a step run in issue
+            # order (L-1 .. 0) on the engine's single comm stream, so on GPU ONE wait on the last-issued handle
+            # covers them all (each cross-stream wait costs a barrier packet on the compute queue).
+            if self.last_handle is not None:
+                if self.cuda:
+                    self.last_handle.wait()
+                else:
+                    for h in self.pending:
+                        if h is not None:
+                            h.synchronize()
+                self.pending = [None] * m.L
+                self.last_handle = None
             for i in range(m.L):
-                h = self.pending[i]
-                if h is not None:
-                    if self.cuda:
-                        h.wait()
-                    else:
-                        h.synchronize()
-                    self.pending[i] = None
                 m.forward_layer(i)
         if prof:
             self._sync()
@@ -127,10 +133,11 @@ class DataParallelTrainer:
                 m.backward_data(i)
                 if h is not None:
                     ev = None
-                    if self.cuda:
-                        ev = torch.cuda.Event()
+                    if self.cuda and not self.engine.inline:
+                        ev = self.engine._event()
                         ev.record()
                     self.pending[i] = h.commit(update_after=ev)
+                    self.last_handle = self.pending[i]
                 else:
                     self._sgd_local(l)
             if prof and i == m.L - 1:
@@ -156,4 +163,5 @@ class DataParallelTrainer:
             if h is not None:
                 h.synchronize(timeout)
                 self.pending[i] = None
+        self.last_handle = None
         self._sync()
