@@ -139,6 +139,15 @@ class Handle:
             return False
         return self.event is None or self.event.query()
 
+    def latency_ms(self) -> float | None:
+        """Device-side latency of the request (start of its comm phase -> end of the epilogue); requires
+        ``engine.timing = True`` (the reference's get_all_reduce_latency(), sw/mlp_mpi_example_f32.cpp:100-106)."""
+        t = getattr(self, "_timing", None)
+        if t is None or self._pending is not None:
+            return None
+        t[1].synchronize()
+        return t[0].elapsed_time(t[1])
+
     def wait(self, stream=None):
         """GPU-side wait: make ``stream`` (default: current) wait for completion; host does not block."""
         self.commit()
@@ -198,6 +207,7 @@ class CompressedAllReduce:
         else:
             self.stream = None
         self._events: list = []
+        self.timing = False  # per-request device timestamps (Handle.latency_ms)
         self._scratch: dict = {}
         self._slot = 0
         self.fault = faults.FaultInjector.from_env()
@@ -297,10 +307,19 @@ class CompressedAllReduce:
             return h if defer else h.commit()
         ready = self._event()
         ready.record(torch.cuda.current_stream(self.device))
+        t_start = None
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ready)
+            if self.timing:
+                t_start = torch.cuda.Event(enable_timing=True)
+                t_start.record(self.stream)
             thunks = comm_fn()
+        if t_start is not None:
+            t_end = torch.cuda.Event(enable_timing=True)
+            thunks = list(thunks) + [lambda: t_end.record(self.stream)]
         h = Handle(self, slot, None, name, pending=thunks)
+        if t_start is not None:
+            h._timing = (t_start, t_end)
         return h if defer else h.commit(update_after)
 
     def _event(self):
