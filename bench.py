@@ -44,20 +44,24 @@ def main():
     ap.add_argument("--transport", default="torch", choices=["torch", "native"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="world 1 through the full multi-rank path (1-rank RCCL group, side-stream engine)")
     a = ap.parse_args()
 
-    rank, world, local, device = D.init_distributed()
+    rank, world, local, device = D.init_distributed(force=a.force_dist)
     if world != a.gpus and rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     if device.type != "cuda":
         print("[bench] no GPU visible: running the CPU path (functional only)", file=sys.stderr)
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    if world > 1:
-        transport = NativeTransport() if a.transport == "native" else TorchDistTransport()
+    if world > 1 or a.force_dist:
+        transport = NativeTransport(force_collectives=a.force_dist) if a.transport == "native" else \
+            TorchDistTransport(force_collectives=a.force_dist)
     else:
         transport = ThreadFabric(1).transport(0)
     kind = "local" if a.compress == "local" else a.compress
-    engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings)
+    engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings,
+                         force_comm=a.force_dist)
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
     if world > 1:

@@ -88,14 +88,20 @@ def main():
         if a.sweep and dt == torch.bfloat16:
             res = {}
             for tile in ((256, 256), (256, 128), (128, 256), (128, 128)):
-                for sk in (1, 2, 4):
-                    if M % tile[0] or N % tile[1] or K % (64 * sk):
-                        continue
-                    fn = lambda t=tile, s=sk: G.gemm(A, a_t, B, b_t, C, epi, split_k=s, tile=t, **kw)  # noqa: E731
-                    fn()
-                    res[f"{tile[0]}x{tile[1]}/s{sk}"] = round(
-                        statistics.median(time_fn(fn, a.iters) for _ in range(3)), 2)
-            best = min(res, key=res.get)
+                for waves in (8, 4):
+                    for sk in (1, 2):
+                        if M % tile[0] or N % tile[1] or K % (64 * sk):
+                            continue
+                        t3 = tile + (waves,)
+                        fn = lambda t=t3, s=sk: G.gemm(A, a_t, B, b_t, C, epi, split_k=s, tile=t, **kw)  # noqa: E731
+                        fn()
+                        torch.cuda.synchronize()
+                        ref_out = ref().float() * ((aux > 0) if epi == G.EPI_RELU_MASK else 1)
+                        ok = (C.float() - ref_out).abs().max().item() < 1.0
+                        res[f"{tile[0]}x{tile[1]}w{waves}/s{sk}"] = round(
+                            statistics.median(time_fn(fn, a.iters) for _ in range(3)), 2) if ok else "WRONG"
+            valid = {k: v for k, v in res.items() if v != "WRONG"}
+            best = min(valid, key=valid.get) if valid else None
             print(json.dumps({"shape": name, "sweep_us": res, "best": best,
                               "auto_plan": G._ext.require().gemm_plan(M, N, K)}), flush=True)
         mine(); ref(); torch.cuda.synchronize()

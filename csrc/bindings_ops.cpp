@@ -27,7 +27,8 @@ int64_t ld_of(const at::Tensor& t) {
 //   b_t: if true, B is given as a [N][K] tensor (K-contiguous), else [K][N]
 void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tensor& C, int64_t epilogue,
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux, bool accumulate,
-          int64_t split_k, const c10::optional<at::Tensor>& workspace, int64_t tile_bm, int64_t tile_bn) {
+          int64_t split_k, const c10::optional<at::Tensor>& workspace, int64_t tile_bm, int64_t tile_bn,
+          const c10::optional<at::Tensor>& colsum, int64_t tile_waves) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "A and B dtype mismatch");
   GemmArgs g{};
@@ -51,6 +52,13 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
   g.split_k = (int)std::max<int64_t>(0, split_k);
   g.tile_bm = (int)tile_bm;
   g.tile_bn = (int)tile_bn;
+  g.tile_waves = (int)tile_waves;
+  if (colsum) {
+    TORCH_CHECK(colsum->is_cuda() && colsum->is_contiguous() && colsum->scalar_type() == at::kFloat &&
+                    colsum->numel() >= g.N,
+                "colsum must be a contiguous f32 GPU tensor of >= N elements");
+    g.colsum = colsum->data_ptr<float>();
+  }
   if (bias) {
     TORCH_CHECK(bias->is_contiguous() && bias->numel() >= g.N, "bad bias");
     g.bias = bias->data_ptr();
@@ -73,9 +81,10 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
   }
 }
 
-pybind11::tuple gemm_plan(int64_t M, int64_t N, int64_t K, int64_t split_k, int64_t tile_bm, int64_t tile_bn) {
-  GemmPlan p = gemm_bf16_plan((int)M, (int)N, (int)K, (int)split_k, (int)tile_bm, (int)tile_bn);
-  return pybind11::make_tuple(p.bm, p.bn, p.split_k);
+pybind11::tuple gemm_plan(int64_t M, int64_t N, int64_t K, int64_t split_k, int64_t tile_bm, int64_t tile_bn,
+                          int64_t tile_waves) {
+  GemmPlan p = gemm_bf16_plan((int)M, (int)N, (int)K, (int)split_k, (int)tile_bm, (int)tile_bn, (int)tile_waves);
+  return pybind11::make_tuple(p.bm, p.bn, p.split_k, p.waves);
 }
 
 bool gemm_supported(int64_t M, int64_t N, int64_t K, bool bf16, int64_t split_k) {
@@ -118,11 +127,12 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm", &gemm, "MFMA GEMM with fused epilogue", pybind11::arg("A"), pybind11::arg("a_t"), pybind11::arg("B"),
         pybind11::arg("b_t"), pybind11::arg("C"), pybind11::arg("epilogue") = 0, pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("aux") = pybind11::none(), pybind11::arg("accumulate") = false, pybind11::arg("split_k") = 1,
-        pybind11::arg("workspace") = pybind11::none(), pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0);
+        pybind11::arg("workspace") = pybind11::none(), pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0,
+        pybind11::arg("colsum") = pybind11::none(), pybind11::arg("tile_waves") = 0);
   m.def("gemm_supported", &gemm_supported);
-  m.def("gemm_plan", &gemm_plan, "bf16 GEMM tile/split-K plan (bm, bn, split_k); bm == 0: unsupported",
+  m.def("gemm_plan", &gemm_plan, "bf16 GEMM tile/split-K plan (bm, bn, split_k, waves); bm == 0: unsupported",
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0,
-        pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0);
+        pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0, pybind11::arg("tile_waves") = 0);
   m.attr("EPI_NONE") = (int)kEpiNone;
   m.attr("EPI_BIAS") = (int)kEpiBias;
   m.attr("EPI_BIAS_RELU") = (int)kEpiBiasRelu;

@@ -33,14 +33,17 @@ struct GemmArgs {
   void* workspace;   // split-K slabs: split_k * M * N floats
   int tile_bm = 0;   // 0: automatic tile choice; else force BM x BN (128/256)
   int tile_bn = 0;
+  int tile_waves = 0;  // 0: default; 4 or 8 waves per workgroup
+  float* colsum = nullptr;  // optional: colsum[n] = sum_k B(k, n) (bias gradient fused into bwd-weight;
+                            // B MN-contiguous, no split-K); written, not accumulated
 };
 
 struct GemmPlan {
-  int bm, bn, split_k;  // bm == 0: unsupported
+  int bm, bn, split_k, waves;  // bm == 0: unsupported; waves: 8 (2/SIMD) or 4 (1/SIMD)
 };
 
 // Tile / split-K choice for a shape (split_k <= 0: automatic).
-GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm = 0, int tile_bn = 0);
+GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm = 0, int tile_bn = 0, int tile_waves = 0);
 
 // Returns false if the shape is not supported by the MFMA path (caller must then error out).
 bool gemm_bf16_supported(const GemmArgs& a);

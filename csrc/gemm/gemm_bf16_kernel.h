@@ -20,11 +20,12 @@
 //     (f32) / 8-B (bf16) row segments, with bias / ReLU / ReLU-mask (bwd-data) / accumulate fused.
 //   * split-K: K is split over workgroups, f32 partial slabs + an ordered (deterministic) reduce kernel
 //     that applies the same epilogue.
+#pragma once
 #include "gemm/gemm.h"
 #include "gemm/glds.h"
 
 namespace fan {
-namespace {
+namespace gemm_detail {
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -34,37 +35,39 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
 
 constexpr int BK = 64;
-constexpr int NT = 512;
-constexpr int NWAVE = 8;
+constexpr int kDefaultWaves = 8;
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
-template <int OUTER>
+template <int OUTER, int NT>
 struct OpTile {
   static constexpr int BYTES = OUTER * BK * 2;
-  static constexpr int GLDS = BYTES / (NT * 16);  // glds instructions per thread per stage
+  static constexpr int IB = NT * 16;              // bytes written by one block-wide glds instruction
+  static constexpr int GLDS = BYTES / IB;         // glds instructions per thread per stage
+  static constexpr int PER_HALF = (64 * 256) / IB;  // MN-contig: instructions per 128-column half
 };
 
-// Stage one operand tile (outer extent OUTER from o0, k extent 64 from k0).
-template <bool KCONTIG, int OUTER>
+// Stage one operand tile (outer extent OUTER from o0, k extent 64 from k0) with NT threads.
+template <bool KCONTIG, int OUTER, int NT>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int64_t ld, int o0, int k0, char* lds,
                                            int wave, int lane) {
+  using T = OpTile<OUTER, NT>;
   const int t = wave * 64 + lane;
 #pragma unroll
-  for (int i = 0; i < OpTile<OUTER>::GLDS; ++i) {
+  for (int i = 0; i < T::GLDS; ++i) {
     const bf16_t* src;
     if (KCONTIG) {
-      const int row = i * 64 + (t >> 3);  // 8 KiB per block-instruction = 64 rows of 128 B
+      const int row = i * (T::IB / 128) + (t >> 3);  // rows of 128 B
       const int c = (t & 7) ^ ((row >> 1) & 7);
       src = g + (int64_t)(o0 + row) * ld + k0 + c * 8;
     } else {
-      const int half = i >> 1;                  // 128-column half
-      const int krow = (i & 1) * 32 + (t >> 4);  // 8 KiB = 32 k-rows of 256 B
+      const int half = i / T::PER_HALF;                               // 128-column half
+      const int krow = (i % T::PER_HALF) * (T::IB / 256) + (t >> 4);  // k-rows of 256 B
       const int cs = t & 15;
       const int blk = (cs >> 1) ^ mn_swz(krow);
       src = g + (int64_t)(k0 + krow) * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8;
     }
-    glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + i * 8192 + wave * 1024)));
+    glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + i * T::IB + wave * 1024)));
   }
 }
 
@@ -89,6 +92,13 @@ __device__ __forceinline__ s16x8 read_frag(const char* lds, int o, int ks, int l
     r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
     return r;
   }
+}
+
+__device__ __forceinline__ float frag_sum(const s16x8& f) {
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s += __uint_as_float(((uint32_t)(uint16_t)f[e]) << 16);
+  return s;
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -150,18 +160,21 @@ __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc
   Out<TC>::store4(p, v);
 }
 
+// 8 waves (2 per SIMD) or 4 waves (1 per SIMD, up to 512 VGPR+AGPR per lane: large per-wave tiles).
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
-__global__ void __launch_bounds__(NT, 2)
+__global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
     gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                      TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
-                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws) {
-  constexpr int A_BYTES = OpTile<BM>::BYTES, B_BYTES = OpTile<BN>::BYTES;
+                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
+                     float* __restrict__ colsum) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int A_BYTES = OpTile<BM, NT>::BYTES, B_BYTES = OpTile<BN, NT>::BYTES;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int S = (3 * STAGE <= 160 * 1024) ? 3 : 2;
-  constexpr int G = OpTile<BM>::GLDS + OpTile<BN>::GLDS;
+  constexpr int G = OpTile<BM, NT>::GLDS + OpTile<BN, NT>::GLDS;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // per-wave sub-tile
   constexpr int MI = WTM / 16, NJ = WTN / 16;
-  static_assert(WM * WN == NWAVE, "8 waves");
+  static_assert(WM * WN == 8 || WM * WN == 4, "4 or 8 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = N / BN;
@@ -170,8 +183,16 @@ __global__ void __launch_bounds__(NT, 2)
   const int wg = xcd_remap(blockIdx.x, nwg);
   const int tile = wg % tiles;
   const int ksplit = wg / tiles;
-  const int m0 = (tile / tiles_n) * BM;
-  const int n0 = (tile % tiles_n) * BN;
+  // 2-D grouped order: consecutive tiles (one XCD's contiguous run after xcd_remap) walk GM tile-rows
+  // before moving right, so an XCD works on a compact GM x (run/GM) block of C and its L2 holds
+  // fewer distinct A/B panel slices per k-step.
+  const int tiles_m = M / BM;
+  const int GM = tiles_m >= 4 ? 4 : tiles_m;
+  const int grp = tile / (GM * tiles_n);
+  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
+  const int in_grp = tile % (GM * tiles_n);
+  const int m0 = (grp * GM + in_grp % gm) * BM;
+  const int n0 = (in_grp / gm) * BN;
   const int k_per = K / split_k;
   const int kbeg = ksplit * k_per;
   const int nk = k_per / BK;
@@ -179,6 +200,11 @@ __global__ void __launch_bounds__(NT, 2)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
+  // fused bias gradient: the waves of the first row-block sum the (MN-contiguous) B fragments they read
+  const bool do_colsum = !BKC && colsum != nullptr && m0 == 0 && wm == 0;
+  float cs[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
 
   f32x4 acc[MI][NJ];
 #pragma unroll
@@ -186,14 +212,20 @@ __global__ void __launch_bounds__(NT, 2)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto issue_stage = [&](int kt_stage, int buf) {
+    char* st = smem + buf * STAGE;
+    stage_tile<AK, BM, NT>(A, lda, m0, kbeg + kt_stage * BK, st, wave, lane);
+    stage_tile<BKC, BN, NT>(B, ldb, n0, kbeg + kt_stage * BK, st + A_BYTES, wave, lane);
+  };
+
+  // Register budget per lane: 4 waves = 1 wave/SIMD (512 VGPR+AGPR), 8 waves = 2 waves/SIMD (256).
+  constexpr int REG_BUDGET = NT == 256 ? 480 : 232;
+  constexpr int ACC_R = MI * NJ * 4, FRAG_R = (MI + NJ) * 4;
+  constexpr bool DBL = ACC_R + 2 * FRAG_R <= REG_BUDGET;
   // prologue: stages 0..S-2 in flight
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) {
-    if (s < nk) {
-      char* st = smem + s * STAGE;
-      stage_tile<AK, BM>(A, lda, m0, kbeg + s * BK, st, wave, lane);
-      stage_tile<BKC, BN>(B, ldb, n0, kbeg + s * BK, st + A_BYTES, wave, lane);
-    }
+    if (s < nk) issue_stage(s, s);
   }
 
   for (int kt = 0; kt < nk; ++kt) {
@@ -206,12 +238,12 @@ __global__ void __launch_bounds__(NT, 2)
     __builtin_amdgcn_s_barrier();  // every wave retired stage kt and finished computing kt-1
     if (kt + S - 1 < nk) {
       char* st = smem + ((kt + S - 1) % S) * STAGE;
-      stage_tile<AK, BM>(A, lda, m0, kbeg + (kt + S - 1) * BK, st, wave, lane);
-      stage_tile<BKC, BN>(B, ldb, n0, kbeg + (kt + S - 1) * BK, st + A_BYTES, wave, lane);
+      stage_tile<AK, BM, NT>(A, lda, m0, kbeg + (kt + S - 1) * BK, st, wave, lane);
+      stage_tile<BKC, BN, NT>(B, ldb, n0, kbeg + (kt + S - 1) * BK, st + A_BYTES, wave, lane);
     }
     const char* sa = smem + (kt % S) * STAGE;
     const char* sb = sa + A_BYTES;
-    if constexpr (MI * NJ <= 16) {
+    if constexpr (DBL) {
       // issue the fragment reads of BOTH k-steps up front: the k-step-1 reads overlap the k-step-0 MFMAs
       // (hipcc emits counted lgkmcnt waits per consumer)
       s16x8 af[2][MI], bfr[2][NJ];
@@ -221,6 +253,10 @@ __global__ void __launch_bounds__(NT, 2)
         for (int i = 0; i < MI; ++i) af[ks][i] = read_frag<AK>(sa, wm * WTM + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bfr[ks][j] = read_frag<BKC>(sb, wn * WTN + j * 16, ks, lane);
+        if (do_colsum) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) cs[j] += frag_sum(bfr[ks][j]);
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -244,6 +280,10 @@ __global__ void __launch_bounds__(NT, 2)
         for (int i = 0; i < MI; ++i) af[i] = read_frag<AK>(sa, wm * WTM + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<BKC>(sb, wn * WTN + j * 16, ks, lane);
+        if (do_colsum) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) cs[j] += frag_sum(bfr[j]);
+        }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < MI; ++i)
@@ -254,6 +294,16 @@ __global__ void __launch_bounds__(NT, 2)
                                                                 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
+    }
+  }
+
+  if (do_colsum) {  // lanes l, l^16, l^32, l^48 hold the same column over different k rows
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float v = cs[j];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lane < 16) colsum[n0 + wn * WTN + j * 16 + lane] = v;
     }
   }
 
@@ -323,16 +373,18 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   if (sk > 1) {
     auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, true>;
     FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL(k, grid, NT, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
-                       (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace);
+    hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
+                       (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
+                       (float*)nullptr);
     hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
                        (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
                        a.ldaux, a.M, a.N);
   } else {
     auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>;
     FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL(k, grid, NT, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
-                       (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1, (float*)nullptr);
+    hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
+                       (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1, (float*)nullptr,
+                       a.colsum);
   }
 }
 
@@ -355,71 +407,24 @@ void launch_epi(const GemmArgs& a, int sk, hipStream_t s) {
 }
 
 template <bool AK, bool BKC>
-void launch_tile(const GemmArgs& a, int bm, int bn, int sk, hipStream_t s) {
+void launch_tile(const GemmArgs& a, int bm, int bn, int waves, int sk, hipStream_t s) {
+#ifdef FAN_GEMM_4WAVE
+  // One wave per SIMD (2x2 waves, up to 512 VGPR+AGPR per lane). Measured 5-25% slower than the 8-wave
+  // variants on every MLP / BERT / square shape (bench/gemm_bench.py --sweep), so not built by default.
+  if (waves == 4) {
+    if (bm == 256 && bn == 256) launch_epi<256, 256, 2, 2, AK, BKC>(a, sk, s);
+    else if (bm == 256 && bn == 128) launch_epi<256, 128, 2, 2, AK, BKC>(a, sk, s);
+    else if (bm == 128 && bn == 256) launch_epi<128, 256, 2, 2, AK, BKC>(a, sk, s);
+    else launch_epi<128, 128, 2, 2, AK, BKC>(a, sk, s);
+    return;
+  }
+#endif
+  (void)waves;
   if (bm == 256 && bn == 256) launch_epi<256, 256, 2, 4, AK, BKC>(a, sk, s);
   else if (bm == 256 && bn == 128) launch_epi<256, 128, 4, 2, AK, BKC>(a, sk, s);
   else if (bm == 128 && bn == 256) launch_epi<128, 256, 2, 4, AK, BKC>(a, sk, s);
   else launch_epi<128, 128, 2, 4, AK, BKC>(a, sk, s);
 }
 
-}  // namespace
-
-GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn) {
-  GemmPlan p{0, 0, 1};
-  if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % BK) return p;
-  // Measured on MI355X (bench/gemm_bench.py --sweep, MLP shapes + 4k/8k squares): take the largest tile
-  // that still gives >= one workgroup per CU (256), preferring 128x256 over 256x128; split K only when
-  // even 128x128 tiles leave more than half the CUs idle (split-K costs an f32 slab round trip).
-  const int cand[4][2] = {{256, 256}, {128, 256}, {256, 128}, {128, 128}};
-  int best = -1;
-  for (int c = 0; c < 4 && best < 0; ++c) {
-    const int bm = cand[c][0], bn = cand[c][1];
-    if (M % bm || N % bn) continue;
-    if (tile_bm > 0 && (bm != tile_bm || bn != tile_bn)) continue;
-    if (tile_bm > 0 || (M / bm) * (N / bn) >= kNumCU) best = c;
-  }
-  if (best < 0) {  // small output: the tile with the most workgroups
-    for (int c = 3; c >= 0 && best < 0; --c) {
-      const int bm = cand[c][0], bn = cand[c][1];
-      if (M % bm || N % bn) continue;
-      if (tile_bm > 0 && (bm != tile_bm || bn != tile_bn)) continue;
-      best = c;
-    }
-  }
-  if (best < 0) return p;
-  const int tiles = (M / cand[best][0]) * (N / cand[best][1]);
-  int sk = 1;
-  if (split_k > 0) {
-    sk = split_k;
-    if (K % (BK * sk)) return p;
-  } else if (tiles * 2 <= kNumCU) {
-    while (tiles * sk < kNumCU && sk < 8 && K % (BK * sk * 2) == 0 && K / (sk * 2) >= 512) sk *= 2;
-  }
-  p.bm = cand[best][0];
-  p.bn = cand[best][1];
-  p.split_k = sk;
-  return p;
-}
-
-bool gemm_bf16_supported(const GemmArgs& a) {
-  const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn);
-  if (p.bm == 0) return false;
-  if (a.lda % 8 || a.ldb % 8 || a.ldc % 4 || (a.aux && a.ldaux % 4)) return false;
-  if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return false;
-  if (((uintptr_t)a.C) & (a.c_bf16 ? 7 : 15)) return false;
-  if (a.accumulate && a.c_bf16) return false;
-  if (p.split_k > 1 && a.workspace == nullptr) return false;
-  return true;
-}
-
-void launch_gemm_bf16(const GemmArgs& a, hipStream_t s) {
-  FAN_CHECK(gemm_bf16_supported(a), "gemm_bf16: unsupported shape/layout (need M,N % 128 == 0, K % 64 == 0)");
-  const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn);
-  if (a.a_kcontig && a.b_kcontig) launch_tile<true, true>(a, p.bm, p.bn, p.split_k, s);
-  else if (a.a_kcontig && !a.b_kcontig) launch_tile<true, false>(a, p.bm, p.bn, p.split_k, s);
-  else if (!a.a_kcontig && a.b_kcontig) launch_tile<false, true>(a, p.bm, p.bn, p.split_k, s);
-  else launch_tile<false, false>(a, p.bm, p.bn, p.split_k, s);
-  FAN_HIP_CHECK(hipGetLastError());
-}
-
+}  // namespace gemm_detail
 }  // namespace fan

@@ -1,0 +1,83 @@
+// bf16 GEMM planner + dispatch. The kernel template lives in gemm_bf16_kernel.h; each operand layout is
+// instantiated in its own translation unit (gemm_bf16_l*.hip) so the ~200 kernels build in parallel.
+#include "gemm/gemm_bf16_kernel.h"
+
+namespace fan {
+
+using gemm_detail::BK;
+using gemm_detail::kDefaultWaves;
+using gemm_detail::launch_tile;
+
+namespace gemm_detail {  // instantiated in gemm_bf16_l{00,01,10,11}.hip
+extern template void launch_tile<false, false>(const GemmArgs&, int, int, int, int, hipStream_t);
+extern template void launch_tile<false, true>(const GemmArgs&, int, int, int, int, hipStream_t);
+extern template void launch_tile<true, false>(const GemmArgs&, int, int, int, int, hipStream_t);
+extern template void launch_tile<true, true>(const GemmArgs&, int, int, int, int, hipStream_t);
+}  // namespace gemm_detail
+
+GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn, int tile_waves) {
+  GemmPlan p{0, 0, 1, 8};
+  if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % BK) return p;
+  // Measured on MI355X (bench/gemm_bench.py --sweep, MLP shapes + 4k/8k squares): take the largest tile
+  // that still gives >= one workgroup per CU (256), preferring 128x256 over 256x128; split K only when
+  // even 128x128 tiles leave more than half the CUs idle (split-K costs an f32 slab round trip).
+  const int cand[4][2] = {{256, 256}, {128, 256}, {256, 128}, {128, 128}};
+  int best = -1;
+  for (int c = 0; c < 4 && best < 0; ++c) {
+    const int bm = cand[c][0], bn = cand[c][1];
+    if (M % bm || N % bn) continue;
+    if (tile_bm > 0 && (bm != tile_bm || bn != tile_bn)) continue;
+    if (tile_bm > 0 || (M / bm) * (N / bn) >= kNumCU) best = c;
+  }
+  if (best < 0) {  // small output: the tile with the most workgroups
+    for (int c = 3; c >= 0 && best < 0; --c) {
+      const int bm = cand[c][0], bn = cand[c][1];
+      if (M % bm || N % bn) continue;
+      if (tile_bm > 0 && (bm != tile_bm || bn != tile_bn)) continue;
+      best = c;
+    }
+  }
+  if (best < 0) return p;
+  const int tiles = (M / cand[best][0]) * (N / cand[best][1]);
+  int sk = 1;
+  if (split_k > 0) {
+    sk = split_k;
+    if (K % (BK * sk)) return p;
+  } else if (tiles * 2 <= kNumCU) {
+    while (tiles * sk < kNumCU && sk < 8 && K % (BK * sk * 2) == 0 && K / (sk * 2) >= 512) sk *= 2;
+  }
+  p.bm = cand[best][0];
+  p.bn = cand[best][1];
+  p.split_k = sk;
+#ifdef FAN_GEMM_4WAVE
+  p.waves = tile_waves == 4 || tile_waves == 8 ? tile_waves : kDefaultWaves;
+#else
+  p.waves = kDefaultWaves;
+  (void)tile_waves;
+#endif
+  return p;
+}
+
+bool gemm_bf16_supported(const GemmArgs& a) {
+  const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn, a.tile_waves);
+  if (p.bm == 0) return false;
+  if (a.lda % 8 || a.ldb % 8 || a.ldc % 4 || (a.aux && a.ldaux % 4)) return false;
+  if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return false;
+  if (((uintptr_t)a.C) & (a.c_bf16 ? 7 : 15)) return false;
+  if (a.accumulate && a.c_bf16) return false;
+  if (p.split_k > 1 && a.workspace == nullptr) return false;
+  if (a.colsum && (p.split_k > 1 || a.b_kcontig)) return false;
+  return true;
+}
+
+void launch_gemm_bf16(const GemmArgs& a, hipStream_t s) {
+  FAN_CHECK(gemm_bf16_supported(a), "gemm_bf16: unsupported shape/layout (need M,N % 128 == 0, K % 64 == 0)");
+  const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn, a.tile_waves);
+  if (a.a_kcontig && a.b_kcontig) launch_tile<true, true>(a, p.bm, p.bn, p.waves, p.split_k, s);
+  else if (a.a_kcontig && !a.b_kcontig) launch_tile<true, false>(a, p.bm, p.bn, p.waves, p.split_k, s);
+  else if (!a.a_kcontig && a.b_kcontig) launch_tile<false, true>(a, p.bm, p.bn, p.waves, p.split_k, s);
+  else launch_tile<false, false>(a, p.bm, p.bn, p.waves, p.split_k, s);
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fan

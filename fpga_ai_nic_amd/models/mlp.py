@@ -141,8 +141,11 @@ class MLP:
 
     def backward_weight(self, i: int):
         l = self.layers[i]
-        G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
-        NN.col_sum(self.dz[i + 1], l.gb)
+        if l.gw.is_cuda and self.dtype == torch.bfloat16:  # bias gradient fused into the bwd-weight GEMM
+            G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw, bias_grad=l.gb)
+        else:
+            G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
+            NN.col_sum(self.dz[i + 1], l.gb)
 
     def backward_data(self, i: int):
         if i == 0:

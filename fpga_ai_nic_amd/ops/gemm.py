@@ -45,9 +45,10 @@ def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
 
 
 def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux=None, accumulate=False,
-         split_k: int | None = None, tile: tuple | None = None):
+         split_k: int | None = None, tile: tuple | None = None, colsum=None):
     """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
-    ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only)."""
+    ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only).
+    ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N])."""
     if C.is_cuda:
         Cx = _ext.require()
         M = A.shape[1] if a_t else A.shape[0]
@@ -55,16 +56,24 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
         N = B.shape[0] if b_t else B.shape[1]
         ws = None
         sk = 0 if split_k is None else int(split_k)
-        tbm, tbn = tile if tile is not None else (0, 0)
+        if colsum is not None:
+            if A.dtype != torch.bfloat16 or b_t:
+                from . import nn as _nn
+
+                gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile)
+                _nn.col_sum(B.t() if b_t else B, colsum)
+                return C
+            sk = 1
+        tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
         if A.dtype == torch.bfloat16:
-            bm, bn, sk = Cx.gemm_plan(M, N, K, sk, tbm, tbn)
+            bm, bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
             if bm == 0:
                 raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
             if sk > 1:
                 ws = _workspace(C.device, sk * M * N)
         else:
             sk = 1
-        Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, tbm, tbn)
+        Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, tbm, tbn, colsum, tw)
         return C
     # CPU reference path
     a = (A.t() if a_t else A).float()
@@ -79,6 +88,8 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     if accumulate:
         r = r + C.float()
     C.copy_(r.to(C.dtype))
+    if colsum is not None:
+        colsum.copy_(b.sum(0).to(colsum.dtype))
     return C
 
 
@@ -93,6 +104,6 @@ def linear_bwd_data(dz, w, out, relu_input=None):
     return gemm(dz, False, w, True, out, EPI_NONE)
 
 
-def linear_bwd_weight(x, dz, out, accumulate=False):
-    """dW = Xᵀ · dZ (f32 out)."""
-    return gemm(x, True, dz, False, out, EPI_NONE, accumulate=accumulate)
+def linear_bwd_weight(x, dz, out, accumulate=False, bias_grad=None):
+    """dW = Xᵀ · dZ (f32 out); with ``bias_grad`` also db = colsum(dZ), fused into the same kernel."""
+    return gemm(x, True, dz, False, out, EPI_NONE, accumulate=accumulate, colsum=bias_grad)

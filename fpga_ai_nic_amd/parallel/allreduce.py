@@ -184,7 +184,7 @@ class CompressedAllReduce:
 
     def __init__(self, transport: Transport, *, codec: str = "bfp_rne", algo: str = "mesh", rings: int = 1,
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
-                 timeout_s: float = 600.0, stream=None, stream_priority: int = -1):
+                 timeout_s: float = 600.0, stream=None, stream_priority: int = -1, force_comm: bool = False):
         if algo not in ("mesh", "ring"):
             raise ValueError(f"unknown algo {algo!r}")
         self.transport = transport
@@ -200,8 +200,10 @@ class CompressedAllReduce:
         self.cuda = self.device.type == "cuda"
         self.orders = ring_orders(self.world, rings) if algo == "ring" else [list(range(self.world))]
         self.rings = len(self.orders)
-        # world 1: nothing to overlap -> run inline on the caller's stream (no side stream, no event packets)
-        self.inline = self.world == 1
+        # world 1: nothing to overlap -> run inline on the caller's stream (no side stream, no event packets).
+        # force_comm keeps the multi-rank code path (side stream, collectives) even at world 1.
+        self.force_comm = force_comm
+        self.inline = self.world == 1 and not force_comm
         if self.cuda and not self.inline:
             self.stream = stream or torch.cuda.Stream(device=self.device, priority=stream_priority)
         else:
@@ -363,7 +365,7 @@ class CompressedAllReduce:
         sb = wire.shard_bytes(c, s)
         g = grad.view(-1)[: L.n_pad]
         S = self._buf(L, "mesh_S", sb)
-        if N == 1:
+        if N == 1 and not self.force_comm:
             wire.reduce(S, 1, 0, g[:s], S, None, s, c)
             return [lambda: finish(S, s, 1, 0, s)]
         if c == 2 and g.dtype == torch.float32:

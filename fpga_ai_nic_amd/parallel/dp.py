@@ -51,16 +51,16 @@ class RcclAllReduce(CompressedAllReduce):
 
 def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str = "rne", algo: str = "mesh",
                 rings: int = 1, max_slice_elems: int = 1 << 22, compat_owner_fp32: bool = False,
-                timeout_s: float = 600.0):
+                timeout_s: float = 600.0, force_comm: bool = False):
     """kind: 'bfp' (compressed engine), 'raw' (engine, uncompressed fp32 wire), 'rccl' (baseline),
     'local' (no communication: world 1)."""
     if kind == "local" or transport is None:
         return None
     if kind == "rccl":
-        return RcclAllReduce(transport, timeout_s=timeout_s)
+        return RcclAllReduce(transport, timeout_s=timeout_s, force_comm=force_comm)
     codec = {"bfp": f"bfp_{rounding}", "raw": "raw_f32", "raw_bf16": "raw_bf16"}[kind]
     return CompressedAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
-                               compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s)
+                               compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm)
 
 
 class DataParallelTrainer:

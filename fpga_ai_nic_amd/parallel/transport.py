@@ -66,22 +66,24 @@ class TorchDistTransport(Transport):
 
     name = "torch"
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force_collectives: bool = False):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        # world 1 normally short-circuits to local copies; force_collectives issues the real (1-rank) RCCL ops
+        self._local = self.world == 1 and not force_collectives
 
     def all_to_all(self, send, recv):
-        if self.world == 1:
+        if self._local:
             recv.copy_(send)
             return
         dist.all_to_all_single(_u8(recv), _u8(send), group=self.group)
 
     def all_gather(self, send, recv):
-        if self.world == 1:
+        if self._local:
             recv.copy_(send)
             return
         s, r = _u8(send), _u8(recv)
@@ -123,7 +125,8 @@ class NativeTransport(Transport):
 
     name = "native"
 
-    def __init__(self, rank: int | None = None, world: int | None = None, device: int | None = None, store=None):
+    def __init__(self, rank: int | None = None, world: int | None = None, device: int | None = None, store=None,
+                 force_collectives: bool = False):
         C = _ext.require()
         if rank is None:
             rank, world = dist.get_rank(), dist.get_world_size()
@@ -140,16 +143,17 @@ class NativeTransport(Transport):
                 store.set(key, C.nccl_unique_id())
             uid = store.get(key)
         self.rank, self.world = rank, world
+        self._local = world == 1 and not force_collectives
         self.comm = C.NativeComm(uid, rank, world, device)
 
     def all_to_all(self, send, recv):
-        if self.world == 1:
+        if self._local:
             recv.copy_(send)
         else:
             self.comm.all_to_all(_u8(send), _u8(recv))
 
     def all_gather(self, send, recv):
-        if self.world == 1:
+        if self._local:
             recv.copy_(send)
         else:
             self.comm.all_gather(_u8(send), _u8(recv))

@@ -18,8 +18,9 @@ def env_rank_world():
         os.environ.get("LOCAL_RANK", "0"))
 
 
-def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
-    """Initialise torch.distributed from the torchrun environment (no-op for world 1 without env).
+def init_distributed(backend: str | None = None, timeout_s: float = 600.0, force: bool = False):
+    """Initialise torch.distributed from the torchrun environment (no-op for world 1 without env, unless
+    ``force``: a 1-rank process group, used to exercise the multi-rank code path on one GPU).
 
     Returns (rank, world, local_rank, device)."""
     rank, world, local = env_rank_world()
@@ -29,7 +30,7 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0):
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         be = backend or ("nccl" if use_cuda else "gloo")

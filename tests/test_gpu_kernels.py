@@ -186,3 +186,16 @@ def test_col_sum(C):
     out = torch.zeros(640, device=DEV)
     NN.col_sum(x, out, 2.0)
     assert (out - x.float().sum(0) * 2).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 4096, 2048), (4096, 1024, 2048), (4096, 4096, 2048), (512, 384, 256)])
+def test_gemm_fused_bias_grad(C, M, N, K):
+    """bwd-weight GEMM with the bias gradient (column sums of dZ) fused: both outputs vs fp32 references."""
+    torch.manual_seed(5)
+    X = torch.randn(K, M, device=DEV).to(torch.bfloat16)   # activations [batch][in]
+    dZ = torch.randn(K, N, device=DEV).to(torch.bfloat16)  # upstream grad [batch][out]
+    dW = torch.empty(M, N, device=DEV)
+    db = torch.full((N,), float("nan"), device=DEV)
+    G.linear_bwd_weight(X, dZ, dW, bias_grad=db)
+    assert (dW - X.float().t() @ dZ.float()).abs().max().item() < 0.25
+    assert (db - dZ.float().sum(0)).abs().max().item() < 1e-2 * K ** 0.5
