@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--algo", default="mesh", choices=["mesh", "ring"])
     ap.add_argument("--rings", type=int, default=1)
     ap.add_argument("--transport", default="torch", choices=["torch", "native"])
+    ap.add_argument("--engine", default="python", choices=["python", "native"],
+                    help="request path: Python-issued engine or the C++ engine (csrc/comm/engine.cpp)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--force-dist", action="store_true",
@@ -61,7 +63,7 @@ def main():
         transport = ThreadFabric(1).transport(0)
     kind = "local" if a.compress == "local" else a.compress
     engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings,
-                         force_comm=a.force_dist)
+                         force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python")
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
     if world > 1:
@@ -121,6 +123,7 @@ def main():
                 "algo": a.algo,
                 "rings": engine.rings if engine is not None else 0,
                 "transport": a.transport if world > 1 else "none",
+                "engine": a.engine,
                 "fused_sgd": True,
             },
             "extra": {

@@ -1,5 +1,6 @@
 // Bindings for the native communicator (RCCL over xGMI).
 #include "bindings_common.h"
+#include "comm/engine.h"
 #include "comm/native_comm.h"
 
 namespace fan {
@@ -56,6 +57,94 @@ void register_engine(pybind11::module_& m) {
       .def("broadcast", [](NativeComm& c, at::Tensor& buf, int root) { c.broadcast(ptr_of(buf), bytes_of(buf), root, fan_stream()); })
       .def("async_error", &NativeComm::async_error)
       .def("abort", &NativeComm::abort);
+
+  namespace py = pybind11;
+  py::class_<AllReduceEngine>(m, "AllReduceEngine")
+      .def(py::init([](NativeComm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
+                       bool compat, double timeout_s, int priority, bool force_comm, int device) {
+             EngineConfig c;
+             c.codec = codec;
+             c.algo = algo;
+             c.rings = rings;
+             c.max_slice_elems = max_slice;
+             c.compat_owner_fp32 = compat;
+             c.timeout_s = timeout_s;
+             c.stream_priority = priority;
+             c.force_comm = force_comm;
+             return new AllReduceEngine(comm, rank, world, c, device);
+           }),
+           py::keep_alive<1, 2>(), py::arg("comm").none(true), py::arg("rank"), py::arg("world"), py::arg("codec"),
+           py::arg("algo"), py::arg("rings"), py::arg("max_slice_elems"), py::arg("compat_owner_fp32"),
+           py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"))
+      .def("layout",
+           [](AllReduceEngine& e, int64_t n) {
+             const EngineLayout L = e.layout(n);
+             return py::dict(py::arg("n") = L.n, py::arg("n_pad") = L.n_pad, py::arg("algo") = L.algo,
+                             py::arg("shard") = L.shard, py::arg("slice") = L.slice, py::arg("blocks") = L.blocks,
+                             py::arg("rings") = L.rings, py::arg("part") = L.part);
+           })
+      .def("wire_bytes", [](AllReduceEngine& e, int64_t n) { return e.wire_bytes(e.layout(n)); })
+      .def_property_readonly("orders", &AllReduceEngine::orders)
+      .def_property_readonly("inline", &AllReduceEngine::is_inline)
+      .def_property_readonly("stream", [](AllReduceEngine& e) { return (uintptr_t)e.stream(); })
+      .def("submit",
+           [](AllReduceEngine& e, const at::Tensor& grad, at::Tensor& master, c10::optional<at::Tensor> lp,
+              c10::optional<at::Tensor> mom, int64_t n_valid, double lr, double grad_scale, double wd,
+              double momentum, bool nesterov, bool defer, bool update, c10::optional<at::Tensor> out_sum) {
+             FAN_T_CUDA_CONTIG(grad);
+             TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
+                         "gradients must be f32 or bf16");
+             const EngineLayout L = e.layout(n_valid);
+             TORCH_CHECK(grad.numel() >= L.n_pad, "gradient buffer has ", grad.numel(), " elements; layout needs ",
+                         L.n_pad);
+             if (update) {
+               FAN_T_CUDA_CONTIG(master);
+               TORCH_CHECK(master.scalar_type() == at::kFloat && master.numel() >= n_valid, "master: f32[n_valid]");
+             }
+             bf16_t* lpp = nullptr;
+             float* momp = nullptr;
+             float* outp = nullptr;
+             if (lp && lp->defined()) {
+               FAN_T_CUDA_CONTIG(*lp);
+               TORCH_CHECK(lp->scalar_type() == at::kBFloat16 && lp->numel() >= n_valid, "lp: bf16[n_valid]");
+               lpp = reinterpret_cast<bf16_t*>(lp->data_ptr());
+             }
+             if (mom && mom->defined()) {
+               FAN_T_CUDA_CONTIG(*mom);
+               TORCH_CHECK(mom->scalar_type() == at::kFloat && mom->numel() >= n_valid, "mom: f32[n_valid]");
+               momp = mom->data_ptr<float>();
+             }
+             if (out_sum && out_sum->defined()) {
+               FAN_T_CUDA_CONTIG(*out_sum);
+               TORCH_CHECK(out_sum->scalar_type() == at::kFloat && out_sum->numel() >= L.n_pad,
+                           "out_sum: f32[n_pad]");
+               outp = out_sum->data_ptr<float>();
+             }
+             SgdParams p{(float)lr, (float)grad_scale, (float)wd, (float)momentum, nesterov ? 1 : 0};
+             return e.submit(grad.data_ptr(), grad.scalar_type() == at::kFloat ? kF32 : kBF16,
+                             update ? master.data_ptr<float>() : nullptr, lpp, momp, n_valid, p, fan_stream(), defer,
+                             update, outp);
+           },
+           py::arg("grad"), py::arg("master"), py::arg("lp") = py::none(), py::arg("mom") = py::none(),
+           py::arg("n_valid"), py::arg("lr"), py::arg("grad_scale") = 1.0, py::arg("weight_decay") = 0.0,
+           py::arg("momentum") = 0.0, py::arg("nesterov") = false, py::arg("defer") = false,
+           py::arg("update") = true, py::arg("out_sum") = py::none())
+      .def(
+          "commit",
+          [](AllReduceEngine& e, int slot, bool after_current) {
+            e.commit(slot, after_current ? fan_stream() : nullptr);
+          },
+          py::arg("slot"), py::arg("after_current") = true)
+      .def("wait_stream", [](AllReduceEngine& e, int slot) { e.wait_stream(slot, fan_stream()); })
+      .def("query", &AllReduceEngine::query)
+      .def("done_word", &AllReduceEngine::done_word)
+      .def("slot_seq", &AllReduceEngine::slot_seq)
+      .def("synchronize", &AllReduceEngine::synchronize, py::arg("slot"), py::arg("timeout_s") = -1.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("latency_ms", &AllReduceEngine::latency_ms, py::call_guard<py::gil_scoped_release>())
+      .def("set_timing", &AllReduceEngine::set_timing)
+      .def("diagnostics", &AllReduceEngine::diagnostics)
+      .def_property_readonly("requests", &AllReduceEngine::requests);
 }
 
 }  // namespace fan

@@ -1,0 +1,344 @@
+// Native compressed all-reduce engine. See engine.h.
+#include "comm/engine.h"
+
+#include <chrono>
+#include <functional>
+#include <sstream>
+#include <thread>
+
+namespace fan {
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static int64_t round_up(int64_t a, int64_t b) { return cdiv(a, b) * b; }
+static size_t esize(int dtype) { return dtype == kF32 ? 4 : 2; }
+
+AllReduceEngine::AllReduceEngine(NativeComm* comm, int rank, int world, EngineConfig cfg, int device)
+    : comm_(comm), rank_(rank), world_(world), device_(device), cfg_(cfg) {
+  FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+  FAN_CHECK(world == 1 || comm != nullptr, "world > 1 needs a communicator");
+  FAN_HIP_CHECK(hipSetDevice(device));
+  orders_ = cfg.algo == 1 ? ring_orders(world, cfg.rings) : std::vector<std::vector<int>>{{}};
+  if (cfg.algo != 1) {
+    orders_[0].resize(world);
+    for (int i = 0; i < world; ++i) orders_[0][i] = i;
+  }
+  inline_ = world == 1 && !cfg.force_comm;
+  FAN_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, cfg.stream_priority));
+  run_stream_ = stream_;
+  void* h = nullptr;
+  FAN_HIP_CHECK(hipHostMalloc(&h, kSlots * 64, hipHostMallocMapped));
+  std::memset(h, 0, kSlots * 64);
+  flags_host_ = reinterpret_cast<volatile uint32_t*>(h);
+  void* d = nullptr;
+  FAN_HIP_CHECK(hipHostGetDevicePointer(&d, h, 0));
+  flags_dev_ = reinterpret_cast<uint32_t*>(d);
+  for (auto& s : slots_) {
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.ready, hipEventDisableTiming));
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.update, hipEventDisableTiming));
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    FAN_HIP_CHECK(hipEventCreate(&s.t0));
+    FAN_HIP_CHECK(hipEventCreate(&s.t1));
+  }
+}
+
+AllReduceEngine::~AllReduceEngine() {
+  hipStreamSynchronize(stream_);
+  for (auto& s : slots_) {
+    hipEventDestroy(s.ready);
+    hipEventDestroy(s.update);
+    hipEventDestroy(s.done);
+    hipEventDestroy(s.t0);
+    hipEventDestroy(s.t1);
+  }
+  for (auto& kv : scratch_) hipFree(kv.second.first);
+  if (flags_host_) hipHostFree((void*)flags_host_);
+  hipStreamDestroy(stream_);
+}
+
+EngineLayout AllReduceEngine::layout(int64_t n) const {
+  EngineLayout L;
+  L.n = n;
+  L.algo = cfg_.algo;
+  const int N = world_;
+  if (cfg_.algo == 0) {
+    L.shard = round_up(std::max<int64_t>(cdiv(n, N), 1), 256);
+    L.n_pad = L.shard * N;
+    return L;
+  }
+  const int R = (int)orders_.size();
+  const int64_t chunk = cdiv(std::max<int64_t>(n, 1), R);
+  const RingGeometry g = ring_geometry(chunk, N, cfg_.max_slice_elems);
+  L.rings = R;
+  L.slice = g.slice_elems;
+  L.blocks = g.blocks;
+  L.part = g.n_pad;
+  L.n_pad = g.n_pad * R;
+  return L;
+}
+
+int64_t AllReduceEngine::wire_bytes(const EngineLayout& L) const {
+  const int N = world_;
+  if (N == 1) return 0;
+  if (L.algo == 0) return 2 * (N - 1) * (int64_t)wire_shard_bytes(cfg_.codec, L.shard);
+  return (int64_t)L.rings * L.blocks * 2 * (N - 1) * (int64_t)wire_shard_bytes(cfg_.codec, L.slice);
+}
+
+uint8_t* AllReduceEngine::scratch(const std::string& key, size_t bytes) {
+  auto it = scratch_.find(key);
+  if (it != scratch_.end() && it->second.second >= bytes) return it->second.first;
+  if (it != scratch_.end()) {
+    FAN_HIP_CHECK(hipDeviceSynchronize());  // rare (bucket grew): the old buffer may still be in flight
+    hipFree(it->second.first);
+  }
+  void* p = nullptr;
+  FAN_HIP_CHECK(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+  FAN_HIP_CHECK(hipMemsetAsync(p, 0, std::max<size_t>(bytes, 256), run_stream_));
+  scratch_[key] = {reinterpret_cast<uint8_t*>(p), bytes};
+  return reinterpret_cast<uint8_t*>(p);
+}
+
+// Epilogue over a gathered wire region: fused decode + SGD (and/or decoded sum output).
+static void epilogue(int codec, hipStream_t st, const uint8_t* G, int64_t shard, int n_shards, int64_t off,
+                     int64_t len, float* master, bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
+                     float* out_sum, int skip_shard = -1, int skip_period = 0) {
+  const int64_t nv = std::max<int64_t>(0, std::min<int64_t>(n_valid - off, len));
+  if (update && nv > 0)
+    launch_wire_sgd(codec, G, (size_t)shard, n_shards, skip_shard, skip_period, master + off, lp ? lp + off : nullptr,
+                    mom ? mom + off : nullptr, p, (size_t)nv, st);
+  if (out_sum) launch_wire_unpack(codec, kF32, G, out_sum + off, (size_t)shard, n_shards, st);
+}
+
+std::vector<std::function<void()>> AllReduceEngine::run_mesh(const EngineLayout& L, const void* grad, int gdt,
+                                                             float* master, bf16_t* lp, float* mom, int64_t n_valid,
+                                                             SgdParams p, bool update, float* out_sum) {
+  const int N = world_, r = rank_, c = cfg_.codec;
+  const int64_t s = L.shard;
+  const size_t sb = wire_shard_bytes(c, s);
+  const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
+  uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
+  hipStream_t st = run_stream_;
+  if ((N == 1 && !cfg_.force_comm) || comm_ == nullptr) {
+    launch_wire_reduce(c, gdt, S, sb, 1, 0, g, S, nullptr, (size_t)s, st);
+    return {[=] { epilogue(c, st, S, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
+  }
+  const uint8_t* P = g;
+  const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
+  if (!zero_copy) {
+    uint8_t* Pb = scratch("mesh_P" + std::to_string(sb * N), sb * N);
+    launch_wire_pack(c, gdt, g, Pb, (size_t)s, N, st);
+    P = Pb;
+  }
+  uint8_t* R = scratch("mesh_R" + std::to_string(sb * N), sb * N);
+  comm_->all_to_all(P, R, sb, st);
+  launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
+  uint8_t* G = scratch("mesh_G" + std::to_string(sb * N), sb * N);
+  comm_->all_gather(S, G, sb, st);
+  const int64_t n_pad = L.n_pad;
+  return {[=] { epilogue(c, st, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
+}
+
+std::vector<std::function<void()>> AllReduceEngine::run_ring(const EngineLayout& L, const void* grad, int gdt,
+                                                             float* master, bf16_t* lp, float* mom, int64_t n_valid,
+                                                             SgdParams p, bool update, float* out_sum) {
+  const int N = world_, c = cfg_.codec;
+  const int64_t S = L.slice;
+  const size_t sb = wire_shard_bytes(c, S);
+  const int64_t nsl = L.blocks * N;
+  const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
+  hipStream_t st = run_stream_;
+  const bool compat = cfg_.compat_owner_fp32 && N > 1 && update;
+  struct RingState {
+    int64_t off;
+    int down, up, pos;
+    std::vector<RingRound> plan;
+    uint8_t *G, *send, *recv[2];
+    const uint8_t* last_partial;
+    float* fp32;
+  };
+  std::vector<RingState> rings;
+  const std::string k = std::to_string(sb) + "_" + std::to_string(nsl);
+  for (size_t i = 0; i < orders_.size(); ++i) {
+    const auto& o = orders_[i];
+    int pos = 0;
+    for (int q = 0; q < N; ++q)
+      if (o[q] == rank_) pos = q;
+    RingState rs;
+    rs.off = (int64_t)i * L.part;
+    rs.pos = pos;
+    rs.down = o[(pos - 1 + N) % N];
+    rs.up = o[(pos + 1) % N];
+    rs.plan = ring_plan(N, pos, L.blocks);
+    rs.G = scratch("ring_G" + std::to_string(i) + "_" + k, sb * nsl);
+    rs.send = scratch("ring_send" + std::to_string(i) + "_" + k, sb);
+    rs.recv[0] = scratch("ring_recv0_" + std::to_string(i) + "_" + k, sb);
+    rs.recv[1] = scratch("ring_recv1_" + std::to_string(i) + "_" + k, sb);
+    rs.last_partial = nullptr;
+    rs.fp32 = compat ? reinterpret_cast<float*>(scratch("ring_fp32_" + std::to_string(i) + "_" + k, 4 * S * L.blocks))
+                     : nullptr;
+    rings.push_back(rs);
+  }
+  const size_t nrows = rings[0].plan.size();
+  std::vector<std::vector<size_t>> rounds;
+  for (size_t j = 0; j < nrows; ++j) {  // a SEND_LOCAL row joins the previous round (OUTPUT_SEND overlap)
+    if (!rounds.empty() && j > 0 && rings[0].plan[j].send_src == kSendLocal) rounds.back().push_back(j);
+    else rounds.push_back({j});
+  }
+  auto local = [&](const RingState& rs, int64_t x) { return g + (size_t)(rs.off + x * S) * esize(gdt); };
+  for (const auto& rnd : rounds) {
+    std::vector<P2POp> sends, recvs;
+    for (size_t j : rnd) {
+      for (auto& rs : rings) {
+        const RingRound& row = rs.plan[j];
+        uint8_t* out = nullptr;
+        if (row.send_src == kSendLocal) {
+          out = row.owned >= 0 ? rs.G + (size_t)row.send_slice * sb : rs.send;
+          launch_wire_pack(c, gdt, local(rs, row.send_slice), out, (size_t)S, 1, st);
+        } else if (row.send_src == kSendReduce) {
+          out = row.owned >= 0 ? rs.G + (size_t)row.send_slice * sb : rs.send;
+          float* f32 = nullptr;
+          if (compat && row.owned >= 0) f32 = rs.fp32 + (size_t)(row.owned / N) * S;
+          launch_wire_reduce(c, gdt, rs.last_partial, sb, 2, 1, local(rs, row.send_slice), out, f32, (size_t)S, st);
+        } else if (row.send_src == kSendForward) {
+          out = rs.G + (size_t)row.send_slice * sb;
+        }
+        if (out && N > 1) sends.push_back({out, sb, rs.down});
+        if (row.recv_slice >= 0) {
+          uint8_t* tgt;
+          if (row.recv_full) {
+            tgt = rs.G + (size_t)row.recv_slice * sb;
+          } else {
+            tgt = rs.recv[j % 2];
+            rs.last_partial = tgt;
+          }
+          recvs.push_back({tgt, sb, rs.up});
+        }
+      }
+    }
+    if (N > 1) comm_->sendrecv(sends, recvs, st);
+  }
+  std::vector<std::function<void()>> thunks;
+  for (auto& rs : rings) {
+    const int64_t off = rs.off, part = L.part, blocks = L.blocks;
+    uint8_t* G = rs.G;
+    if (compat) {
+      const int own = (rs.pos - 1 + N) % N;
+      float* f32 = rs.fp32;
+      thunks.push_back([=] {
+        epilogue(c, st, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum, own, N);
+        for (int64_t b = 0; b < blocks; ++b) {
+          const int64_t o2 = off + (b * N + own) * S;
+          const int64_t nv = std::max<int64_t>(0, std::min<int64_t>(n_valid - o2, S));
+          if (nv > 0)
+            launch_wire_sgd(kRawF32, f32 + b * S, (size_t)S, 1, -1, 0, master + o2, lp ? lp + o2 : nullptr,
+                            mom ? mom + o2 : nullptr, p, (size_t)nv, st);
+        }
+      });
+    } else {
+      thunks.push_back([=] { epilogue(c, st, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum); });
+    }
+  }
+  return thunks;
+}
+
+int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
+                            SgdParams sgd, hipStream_t producer, bool defer, bool update, float* out_sum) {
+  FAN_HIP_CHECK(hipSetDevice(device_));
+  const int slot = next_slot_;
+  next_slot_ = (slot + 1) % kSlots;
+  Slot& sl = slots_[slot];
+  FAN_CHECK(!sl.pending, "request slot still has an uncommitted epilogue (more than 8 requests in flight)");
+  const EngineLayout L = layout(n_valid);
+  sl.stream = run_stream_ = inline_ ? producer : stream_;
+  if (!inline_) {
+    FAN_HIP_CHECK(hipEventRecord(sl.ready, producer));
+    FAN_HIP_CHECK(hipStreamWaitEvent(stream_, sl.ready, 0));
+  }
+  sl.timed = timing_;
+  if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t0, sl.stream));
+  sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum)
+                             : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
+  FAN_HIP_CHECK(hipGetLastError());
+  sl.pending = true;
+  sl.seq = ++seq_;
+  sl.t_issue = now_s();
+  if (!defer) commit(slot, nullptr);
+  return slot;
+}
+
+void AllReduceEngine::commit(int slot, hipStream_t producer) {
+  Slot& sl = slots_.at(slot);
+  if (!sl.pending) return;
+  // inline requests already run on the producer's stream: stream order is the dependency
+  if (producer && producer != sl.stream) {
+    FAN_HIP_CHECK(hipEventRecord(sl.update, producer));
+    FAN_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.update, 0));
+  }
+  for (auto& t : sl.thunks) t();
+  sl.thunks.clear();
+  if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t1, sl.stream));
+  // Side-stream requests: completion word written by the GPU into host-mapped memory (the NIC's "write 1 to
+  // done_addr + done_id"). Inline requests sit on the critical compute stream, where the extra packet costs
+  // more than it buys: their completion is the done event.
+  if (!inline_) FAN_HIP_CHECK(hipStreamWriteValue32(sl.stream, flags_dev_ + slot * 16, sl.seq, 0));
+  FAN_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
+  sl.pending = false;
+}
+
+void AllReduceEngine::wait_stream(int slot, hipStream_t s) {
+  Slot& sl = slots_.at(slot);
+  if (sl.pending) commit(slot, nullptr);
+  if (s != sl.stream) FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
+}
+
+bool AllReduceEngine::query(int slot) {
+  const Slot& sl = slots_.at(slot);
+  if (sl.pending) return false;
+  if (inline_) return hipEventQuery(sl.done) == hipSuccess;
+  return flags_host_[slot * 16] == sl.seq;
+}
+
+std::string AllReduceEngine::diagnostics(int slot) const {
+  const Slot& sl = slots_.at(slot);
+  std::ostringstream os;
+  os << "rank=" << rank_ << " world=" << world_ << " algo=" << (cfg_.algo ? "ring" : "mesh") << " codec=" << cfg_.codec
+     << " slot=" << slot << " seq=" << sl.seq << " done_word=" << flags_host_[slot * 16]
+     << " elapsed=" << (now_s() - sl.t_issue) << "s";
+  if (comm_) os << " rccl_async_error='" << comm_->async_error() << "'";
+  return os.str();
+}
+
+void AllReduceEngine::synchronize(int slot, double timeout_s) {
+  Slot& sl = slots_.at(slot);
+  if (sl.pending) commit(slot, nullptr);
+  const double t0 = now_s();
+  const double tmo = timeout_s > 0 ? timeout_s : cfg_.timeout_s;
+  int spins = 0;
+  while (!query(slot)) {
+    if (++spins > 64) {
+      std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 5));
+      if (comm_ && (spins & 255) == 0) {
+        const std::string e = comm_->async_error();
+        if (!e.empty()) throw std::runtime_error("all-reduce failed: " + e + " [" + diagnostics(slot) + "]");
+      }
+      if (now_s() - t0 > tmo) {
+        const std::string d = diagnostics(slot);
+        if (comm_) comm_->abort();
+        throw std::runtime_error("all-reduce timed out after " + std::to_string(tmo) + "s [" + d + "]");
+      }
+    }
+  }
+}
+
+float AllReduceEngine::latency_ms(int slot) {
+  Slot& sl = slots_.at(slot);
+  if (!sl.timed) return -1.f;
+  synchronize(slot);
+  float ms = 0.f;
+  FAN_HIP_CHECK(hipEventElapsedTime(&ms, sl.t0, sl.t1));
+  return ms;
+}
+
+}  // namespace fan

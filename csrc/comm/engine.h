@@ -1,0 +1,115 @@
+// Native compressed all-reduce engine (C++): the MI355X counterpart of the reference NIC's request path.
+//
+// Reference behaviour being re-expressed:
+//   * all_reduce_setup(done, count, node_id)   -> AllReduceEngine(comm, rank, world, cfg)
+//   * all_reduce(buf, weight_out, flags, ...)  -> submit(): enqueue pack -> xGMI exchange -> reduce ->
+//                                                 exchange -> fused SGD epilogue on a high-priority comm stream
+//   * 8 done slots, round-robin 3-bit done_id  -> kSlots request slots; completion is a 32-bit sequence number
+//     (hw/all_reduce.sv:1228, 1368-1375)          written by the GPU (hipStreamWriteValue32) into host-mapped memory
+//   * wait(done_buf) busy spin (sw:157-180)     -> synchronize(slot, timeout): polls the done word with a bounded
+//                                                 timeout + RCCL async-error check (never spins forever)
+//   * get_all_reduce_latency (sw:100-106)       -> latency_ms(slot) from device timestamps
+// Algorithms: mesh (pack / all-to-all / owner reduce / re-encode / all-gather) and the reference ring schedule
+// (native planner, any N, R arc-disjoint rings) with one fused decode+add+encode kernel per hop.
+#pragma once
+#include <array>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "bfp/bfp_format.h"
+#include "comm/native_comm.h"
+#include "comm/planner.h"
+
+namespace fan {
+
+struct EngineConfig {
+  int codec = kBfpRne;
+  int algo = 0;  // 0 mesh, 1 ring
+  int rings = 1;
+  int64_t max_slice_elems = 1 << 22;
+  bool compat_owner_fp32 = false;
+  double timeout_s = 600.0;
+  int stream_priority = -1;
+  bool force_comm = false;  // world 1 still runs the collectives (exercises the multi-rank path)
+};
+
+struct EngineLayout {
+  int64_t n = 0, n_pad = 0;
+  int algo = 0;
+  int64_t shard = 0;        // mesh
+  int64_t slice = 0;        // ring
+  int64_t blocks = 0;       // ring
+  int rings = 1;
+  int64_t part = 0;         // ring: padded elements per ring part
+};
+
+class AllReduceEngine {
+ public:
+  static constexpr int kSlots = 8;
+
+  AllReduceEngine(NativeComm* comm, int rank, int world, EngineConfig cfg, int device);
+  ~AllReduceEngine();
+
+  EngineLayout layout(int64_t n) const;
+  const std::vector<std::vector<int>>& orders() const { return orders_; }
+  hipStream_t stream() const { return stream_; }
+  bool is_inline() const { return inline_; }
+
+  // Enqueue the communication phase of a request. grad: padded flat buffer (f32 or bf16) ready on `producer`.
+  // If `defer`, the weight update is enqueued later by commit(); otherwise immediately. Returns the slot.
+  int submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
+             SgdParams sgd, hipStream_t producer, bool defer, bool update = true, float* out_sum = nullptr);
+  // Enqueue the deferred SGD epilogue after everything currently enqueued on `producer`.
+  void commit(int slot, hipStream_t producer);
+  void wait_stream(int slot, hipStream_t s);            // GPU-side wait
+  bool query(int slot);                                  // host: request done?
+  uint32_t done_word(int slot) const { return flags_host_[slot * 16]; }  // last completed sequence number
+  uint32_t slot_seq(int slot) const { return slots_.at(slot).seq; }
+  void synchronize(int slot, double timeout_s = -1.0);   // host: bounded wait (throws with diagnostics)
+  float latency_ms(int slot);
+  void set_timing(bool on) { timing_ = on; }
+  std::string diagnostics(int slot) const;
+  uint64_t requests() const { return seq_; }
+  int64_t wire_bytes(const EngineLayout& L) const;
+
+ private:
+  struct Slot {
+    hipEvent_t ready = nullptr, update = nullptr, done = nullptr, t0 = nullptr, t1 = nullptr;
+    uint32_t seq = 0;
+    bool pending = false;   // epilogue not yet committed
+    bool timed = false;
+    hipStream_t stream = nullptr;  // stream the request runs on (comm stream, or the producer when inline)
+    std::vector<std::function<void()>> thunks;
+    double t_issue = 0.0;
+  };
+  uint8_t* scratch(const std::string& key, size_t bytes);
+  std::vector<std::function<void()>> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
+                                              bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
+                                              float* out_sum);
+  std::vector<std::function<void()>> run_ring(const EngineLayout& L, const void* grad, int gdt, float* master,
+                                              bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
+                                              float* out_sum);
+
+  NativeComm* comm_;
+  int rank_, world_, device_;
+  EngineConfig cfg_;
+  std::vector<std::vector<int>> orders_;
+  hipStream_t stream_ = nullptr;
+  // world 1 without forced collectives: nothing to overlap, so requests run inline on the producer's
+  // stream (no cross-stream event packets); run_stream_ is the stream of the request being issued.
+  bool inline_ = false;
+  hipStream_t run_stream_ = nullptr;
+  std::array<Slot, kSlots> slots_;
+  volatile uint32_t* flags_host_ = nullptr;  // host-mapped done words (one 64-B line per slot)
+  uint32_t* flags_dev_ = nullptr;
+  uint32_t seq_ = 0;
+  int next_slot_ = 0;
+  bool timing_ = false;
+  std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
+};
+
+}  // namespace fan

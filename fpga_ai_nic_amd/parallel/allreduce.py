@@ -134,6 +134,14 @@ class Handle:
         self.event = self.engine._run_thunks(thunks, update_after)
         return self
 
+    def commit_after_current(self):
+        """commit() ordered after everything enqueued so far on the current stream."""
+        ev = None
+        if self._pending is not None and self.engine.cuda and not self.engine.inline:
+            ev = self.engine._event()
+            ev.record()
+        return self.commit(update_after=ev)
+
     def done(self) -> bool:
         if self._pending is not None:
             return False

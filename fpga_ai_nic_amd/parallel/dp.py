@@ -51,14 +51,20 @@ class RcclAllReduce(CompressedAllReduce):
 
 def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str = "rne", algo: str = "mesh",
                 rings: int = 1, max_slice_elems: int = 1 << 22, compat_owner_fp32: bool = False,
-                timeout_s: float = 600.0, force_comm: bool = False):
+                timeout_s: float = 600.0, force_comm: bool = False, impl: str = "python"):
     """kind: 'bfp' (compressed engine), 'raw' (engine, uncompressed fp32 wire), 'rccl' (baseline),
-    'local' (no communication: world 1)."""
+    'local' (no communication: world 1). impl: 'python' (request path issued from Python over any
+    transport) or 'native' (C++ engine over its own RCCL communicator; GPU only)."""
     if kind == "local" or transport is None:
         return None
     if kind == "rccl":
         return RcclAllReduce(transport, timeout_s=timeout_s, force_comm=force_comm)
     codec = {"bfp": f"bfp_{rounding}", "raw": "raw_f32", "raw_bf16": "raw_bf16"}[kind]
+    if impl == "native":
+        from .native_engine import NativeAllReduce
+
+        return NativeAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
+                               compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm)
     return CompressedAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
                                compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm)
 
@@ -132,11 +138,7 @@ class DataParallelTrainer:
                                                   name=f"fc{i}")
                 m.backward_data(i)
                 if h is not None:
-                    ev = None
-                    if self.cuda and not self.engine.inline:
-                        ev = self.engine._event()
-                        ev.record()
-                    self.pending[i] = h.commit(update_after=ev)
+                    self.pending[i] = h.commit_after_current()
                     self.last_handle = self.pending[i]
                 else:
                     self._sgd_local(l)

@@ -1,0 +1,172 @@
+"""Python face of the native C++ all-reduce engine (csrc/comm/engine.{h,cpp}).
+
+Same request API as :class:`~fpga_ai_nic_amd.parallel.allreduce.CompressedAllReduce` (``layout``,
+``allreduce_sgd(defer=...)`` -> handle with ``commit_after_current / wait / synchronize / done /
+latency_ms``), but every request is issued by C++: slot bookkeeping, cross-stream events, the mesh / ring
+schedule over the engine's own RCCL communicator and the fused decode+SGD epilogue launch — no Python per
+kernel or per ring round. This is the counterpart of the reference's C++ host driver
+(sw/mlp_mpi_example_f32.cpp:65-180: all_reduce_setup / all_reduce / wait / get_all_reduce_latency):
+
+* completion: 8 request slots; the GPU writes the request's sequence number into host-mapped memory
+  (``hipStreamWriteValue32``) the way the NIC DMA-writes ``done_buf[done_id]`` (hw/all_reduce.sv:1368-1375);
+  ``synchronize`` polls it with a bounded timeout instead of the reference's unbounded spin (sw:163-168);
+* world 1 (no forced collectives): requests run inline on the caller's stream.
+
+GPU only (the engine launches HIP kernels); CPU paths use the Python engine.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from .. import _ext
+from ..ops import wire
+from .allreduce import NUM_SLOTS, BucketLayout, CommTimeoutError
+from .transport import NativeTransport, Transport
+
+_ALGOS = {"mesh": 0, "ring": 1}
+
+
+class NativeHandle:
+    def __init__(self, engine: "NativeAllReduce", slot: int, seq: int, name: str, pending: bool):
+        self.engine = engine
+        self.slot = slot
+        self.seq = seq
+        self.name = name
+        self.t_issue = time.time()
+        self._pending = pending
+
+    def commit(self, update_after=None):
+        """Enqueue the deferred epilogue; with ``update_after`` (any truthy value, e.g. an event recorded on
+        the current stream) it is ordered after everything enqueued so far on the current stream."""
+        if self._pending:
+            self.engine.C.commit(self.slot, update_after is not None)
+            self._pending = False
+        return self
+
+    def commit_after_current(self):
+        if self._pending:
+            self.engine.C.commit(self.slot, True)
+            self._pending = False
+        return self
+
+    def done(self) -> bool:
+        if self._pending:
+            return False
+        C = self.engine.C
+        if self.engine.inline:  # completion is the slot's done event (a reused slot is a later request)
+            return C.query(self.slot)
+        return ((C.done_word(self.slot) - self.seq) & 0xFFFFFFFF) < (1 << 31)
+
+    def wait(self, stream=None):
+        self.commit_after_current()
+        if stream is None:
+            self.engine.C.wait_stream(self.slot)
+        else:
+            with torch.cuda.stream(stream):
+                self.engine.C.wait_stream(self.slot)
+
+    def synchronize(self, timeout: float | None = None):
+        self.commit_after_current()
+        if self.done():
+            return
+        try:
+            self.engine.C.synchronize(self.slot, -1.0 if timeout is None else float(timeout))
+        except RuntimeError as e:
+            raise CommTimeoutError(f"all-reduce '{self.name}': {e}") from e
+
+    def latency_ms(self) -> float | None:
+        if self._pending or self.engine.C.slot_seq(self.slot) != self.seq:
+            return None
+        v = self.engine.C.latency_ms(self.slot)
+        return None if v < 0 else v
+
+
+class NativeAllReduce:
+    """Compressed all-reduce + fused SGD driven entirely from C++."""
+
+    def __init__(self, transport: Transport | None, *, codec: str = "bfp_rne", algo: str = "mesh", rings: int = 1,
+                 max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
+                 timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False):
+        if algo not in _ALGOS:
+            raise ValueError(f"unknown algo {algo!r}")
+        C = _ext.require()
+        self.transport = transport
+        self.rank = transport.rank if transport is not None else 0
+        self.world = transport.world if transport is not None else 1
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise RuntimeError("the native engine runs on GPU only")
+        comm = None
+        if self.world > 1 or force_comm:
+            if not isinstance(transport, NativeTransport):
+                transport = NativeTransport(self.rank, self.world, self.device.index, force_collectives=force_comm)
+                self.transport = transport
+            comm = transport.comm
+        self.codec, self.codec_id, self.algo = codec, wire.codec_id(codec), algo
+        self.timeout_s = timeout_s
+        self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
+                                   compat_owner_fp32, timeout_s, stream_priority, force_comm, self.device.index)
+        self.orders = [list(o) for o in self.C.orders]
+        self.rings = len(self.orders)
+        self.inline = bool(self.C.inline)
+        self.cuda = True
+        self._timing = False
+        self.stats = {"requests": 0, "wire_bytes": 0, "logical_bytes": 0}
+
+    @property
+    def timing(self):
+        return self._timing
+
+    @timing.setter
+    def timing(self, on):
+        self._timing = bool(on)
+        self.C.set_timing(self._timing)
+
+    @property
+    def stream(self):
+        return torch.cuda.ExternalStream(self.C.stream, device=self.device)
+
+    def layout(self, n: int) -> BucketLayout:
+        d = self.C.layout(int(n))
+        return BucketLayout(n=d["n"], n_pad=d["n_pad"], algo=self.algo, world=self.world, shard=d["shard"],
+                            slice_elems=d["slice"], blocks=d["blocks"], rings=d["rings"], part=d["part"])
+
+    def wire_bytes(self, L: BucketLayout) -> int:
+        return int(self.C.wire_bytes(L.n))
+
+    def allreduce_sgd(self, grad: torch.Tensor, master: torch.Tensor, lp: torch.Tensor | None = None,
+                      mom: torch.Tensor | None = None, *, n_valid: int | None = None, lr: float,
+                      grad_scale: float = 1.0, weight_decay: float = 0.0, momentum: float = 0.0,
+                      nesterov: bool = False, update_after=None, defer: bool = False,
+                      name: str = "bucket") -> NativeHandle:
+        n_valid = int(n_valid if n_valid is not None else master.numel())
+        slot = self.C.submit(grad.view(-1), master.view(-1), None if lp is None else lp.view(-1),
+                             None if mom is None else mom.view(-1), n_valid, lr, grad_scale, weight_decay, momentum,
+                             nesterov, True, True, None)
+        h = NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=True)
+        self._account(n_valid)
+        return h if defer else h.commit(update_after)
+
+    def allreduce(self, grad: torch.Tensor, out: torch.Tensor, *, n_valid: int | None = None,
+                  name: str = "bucket") -> NativeHandle:
+        """Sum-only all-reduce: decoded f32 result written to ``out`` (padded length)."""
+        n_valid = int(n_valid if n_valid is not None else grad.numel())
+        if out.dtype != torch.float32:
+            raise TypeError("native allreduce writes f32 sums")
+        slot = self.C.submit(grad.view(-1), out.view(-1), None, None, n_valid, 0.0, 1.0, 0.0, 0.0, False, False,
+                             False, out.view(-1))
+        self._account(n_valid)
+        return NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=False)
+
+    def _account(self, n):
+        self.stats["requests"] += 1
+        self.stats["wire_bytes"] += self.C.wire_bytes(n)
+        self.stats["logical_bytes"] += n * 4
+
+    def diagnostics(self, h: NativeHandle) -> str:
+        return self.C.diagnostics(h.slot)
+
+
+__all__ = ["NativeAllReduce", "NativeHandle", "NUM_SLOTS"]
