@@ -1,6 +1,7 @@
 // Bindings for the native communicator (RCCL over xGMI).
 #include "bindings_common.h"
 #include "comm/engine.h"
+#include "comm/loopback_comm.h"
 #include "comm/native_comm.h"
 
 namespace fan {
@@ -18,7 +19,19 @@ size_t bytes_of(const at::Tensor& t) { return (size_t)t.numel() * t.element_size
 void register_engine(pybind11::module_& m) {
   m.def("nccl_unique_id", []() { return pybind11::bytes(nccl_unique_id_bytes()); });
   m.def("nccl_version", &nccl_version);
-  pybind11::class_<NativeComm>(m, "NativeComm")
+  pybind11::class_<Comm>(m, "Comm")
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def("async_error", &Comm::async_error)
+      .def("abort", &Comm::abort);
+  pybind11::class_<LoopbackFabric, std::shared_ptr<LoopbackFabric>>(m, "LoopbackFabric")
+      .def(pybind11::init<int, double>(), pybind11::arg("world"), pybind11::arg("timeout_s") = 60.0)
+      .def_property_readonly("world", &LoopbackFabric::world)
+      .def("comm", [](std::shared_ptr<LoopbackFabric> f, int rank) { return new LoopbackComm(f, rank); });
+  pybind11::class_<LoopbackComm, Comm>(m, "LoopbackComm")
+      .def("drop_after", &LoopbackComm::drop_after)
+      .def_property_readonly("collectives", &LoopbackComm::collectives);
+  pybind11::class_<NativeComm, Comm>(m, "NativeComm")
       .def(pybind11::init([](pybind11::bytes uid, int rank, int world, int device) {
              return new NativeComm(std::string(uid), rank, world, device);
            }),
@@ -60,7 +73,7 @@ void register_engine(pybind11::module_& m) {
 
   namespace py = pybind11;
   py::class_<AllReduceEngine>(m, "AllReduceEngine")
-      .def(py::init([](NativeComm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
+      .def(py::init([](Comm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
                        bool compat, double timeout_s, int priority, bool force_comm, int device) {
              EngineConfig c;
              c.codec = codec;
@@ -128,13 +141,13 @@ void register_engine(pybind11::module_& m) {
            py::arg("grad"), py::arg("master"), py::arg("lp") = py::none(), py::arg("mom") = py::none(),
            py::arg("n_valid"), py::arg("lr"), py::arg("grad_scale") = 1.0, py::arg("weight_decay") = 0.0,
            py::arg("momentum") = 0.0, py::arg("nesterov") = false, py::arg("defer") = false,
-           py::arg("update") = true, py::arg("out_sum") = py::none())
+           py::arg("update") = true, py::arg("out_sum") = py::none(), py::call_guard<py::gil_scoped_release>())
       .def(
           "commit",
           [](AllReduceEngine& e, int slot, bool after_current) {
             e.commit(slot, after_current ? fan_stream() : nullptr);
           },
-          py::arg("slot"), py::arg("after_current") = true)
+          py::arg("slot"), py::arg("after_current") = true, py::call_guard<py::gil_scoped_release>())
       .def("wait_stream", [](AllReduceEngine& e, int slot) { e.wait_stream(slot, fan_stream()); })
       .def("query", &AllReduceEngine::query)
       .def("done_word", &AllReduceEngine::done_word)

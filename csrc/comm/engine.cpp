@@ -15,7 +15,7 @@ static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static int64_t round_up(int64_t a, int64_t b) { return cdiv(a, b) * b; }
 static size_t esize(int dtype) { return dtype == kF32 ? 4 : 2; }
 
-AllReduceEngine::AllReduceEngine(NativeComm* comm, int rank, int world, EngineConfig cfg, int device)
+AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig cfg, int device)
     : comm_(comm), rank_(rank), world_(world), device_(device), cfg_(cfg) {
   FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
   FAN_CHECK(world == 1 || comm != nullptr, "world > 1 needs a communicator");

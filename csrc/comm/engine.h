@@ -51,7 +51,7 @@ class AllReduceEngine {
  public:
   static constexpr int kSlots = 8;
 
-  AllReduceEngine(NativeComm* comm, int rank, int world, EngineConfig cfg, int device);
+  AllReduceEngine(Comm* comm, int rank, int world, EngineConfig cfg, int device);
   ~AllReduceEngine();
 
   EngineLayout layout(int64_t n) const;
@@ -94,7 +94,7 @@ class AllReduceEngine {
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                               float* out_sum);
 
-  NativeComm* comm_;
+  Comm* comm_;
   int rank_, world_, device_;
   EngineConfig cfg_;
   std::vector<std::vector<int>> orders_;

@@ -29,22 +29,38 @@ struct P2POp {
   int peer;
 };
 
-class NativeComm {
+// What the all-reduce engine needs from a communicator. Implemented by NativeComm (RCCL over xGMI) and by
+// LoopbackComm (virtual ranks on one GPU, csrc/comm/loopback_comm.h) so the engine's multi-rank schedules are
+// testable on a single device.
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  // One group with every send and recv of a round (ring round / multi-ring round). Several sends to the same
+  // peer in one group are matched to that peer's receives in issue order.
+  virtual void sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>& recvs, hipStream_t s) = 0;
+  virtual void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s) = 0;
+  virtual void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // Returns an empty string when healthy, else the async error text.
+  virtual std::string async_error() = 0;
+  virtual void abort() = 0;
+};
+
+class NativeComm : public Comm {
  public:
   NativeComm(const std::string& uid_bytes, int rank, int world, int device);
-  ~NativeComm();
-  int rank() const { return rank_; }
-  int world() const { return world_; }
-  // One RCCL group with every send and recv (ring round / multi-ring round).
-  void sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>& recvs, hipStream_t s);
-  void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s);
-  void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s);
+  ~NativeComm() override;
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  void sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>& recvs, hipStream_t s) override;
+  void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s) override;
+  void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override;
   void all_reduce(void* buf, size_t count, int dtype /*0 f32, 1 bf16*/, hipStream_t s);
   void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, hipStream_t s);
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s);
-  // Returns an empty string when healthy, else the RCCL async error text.
-  std::string async_error();
-  void abort();
+  std::string async_error() override;
+  void abort() override;
 
  private:
   ncclComm_t comm_ = nullptr;

@@ -29,6 +29,7 @@ untouched (re-encoding a decoded group is idempotent).
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -44,6 +45,17 @@ NUM_SLOTS = 8  # reference: 3-bit done_id
 
 class CommTimeoutError(RuntimeError):
     pass
+
+
+class ChecksumError(RuntimeError):
+    """A message failed verification (debug ``verify`` mode): corrupted payload or out-of-order request."""
+
+
+def _checksum(rows: torch.Tensor) -> torch.Tensor:
+    """Per-row Fletcher-style checksum of byte rows [k, nbytes] (nbytes % 4 == 0) -> int64 [k, 2]."""
+    w = rows.contiguous().view(torch.int32).to(torch.int64)
+    idx = torch.arange(1, w.shape[1] + 1, device=w.device, dtype=torch.int64)
+    return torch.stack([w.sum(1), (w * idx).sum(1)], 1)
 
 
 def _cdiv(a, b):
@@ -192,7 +204,8 @@ class CompressedAllReduce:
 
     def __init__(self, transport: Transport, *, codec: str = "bfp_rne", algo: str = "mesh", rings: int = 1,
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
-                 timeout_s: float = 600.0, stream=None, stream_priority: int = -1, force_comm: bool = False):
+                 timeout_s: float = 600.0, stream=None, stream_priority: int = -1, force_comm: bool = False,
+                 verify: bool | None = None):
         if algo not in ("mesh", "ring"):
             raise ValueError(f"unknown algo {algo!r}")
         self.transport = transport
@@ -222,6 +235,9 @@ class CompressedAllReduce:
         self._slot = 0
         self.fault = faults.FaultInjector.from_env()
         self.stats = {"requests": 0, "wire_bytes": 0, "logical_bytes": 0}
+        # debug mode: every message travels with a checksum + the request sequence number,
+        # verified on arrival (host-synchronous: for bisecting corruption / desync, not for speed)
+        self.verify = bool(int(os.environ.get("FAN_VERIFY", "0"))) if verify is None else verify
 
     # -------------------------------------------------------------------------------- layout
     def layout(self, n: int) -> BucketLayout:
@@ -356,6 +372,23 @@ class CompressedAllReduce:
             done.record(self.stream)
         return done
 
+    def _tag(self, rows: torch.Tensor) -> torch.Tensor:
+        """[k, 3] int64: checksum of each byte row + the request sequence number."""
+        seq = torch.full((rows.shape[0], 1), self.stats["requests"], dtype=torch.int64, device=rows.device)
+        return torch.cat([_checksum(rows), seq], 1)
+
+    def _verify_rows(self, rows, tags, peers, what):
+        got = _checksum(rows).cpu()
+        tags = tags.cpu()
+        for i, peer in enumerate(peers):
+            if int(tags[i, 2]) != self.stats["requests"]:
+                raise ChecksumError(f"rank {self.rank}: {what}: message from peer {peer} belongs to request "
+                                    f"#{int(tags[i, 2])}, expected #{self.stats['requests']} (out of order)")
+            if not torch.equal(got[i], tags[i, :2]):
+                raise ChecksumError(f"rank {self.rank}: {what}: message from peer {peer} is corrupted "
+                                    f"(checksum {got[i].tolist()} != {tags[i, :2].tolist()}, request "
+                                    f"#{self.stats['requests']})")
+
     def diagnostics(self, h: Handle) -> str:
         return (f"rank={self.rank} world={self.world} algo={self.algo} codec={self.codec} rings={self.rings} "
                 f"slot={h.slot} elapsed={time.time() - h.t_issue:.1f}s transport={self.transport.name} "
@@ -383,12 +416,21 @@ class CompressedAllReduce:
         else:
             P = self._buf(L, "mesh_P", sb * N)
             wire.pack(g, P, s, c)
+        cs = self._tag(P.view(N, sb)) if self.verify else None
         self.fault.maybe_corrupt("mesh_pack", P)
         R = self._buf(L, "mesh_R", sb * N)
         self.transport.all_to_all(P, R)
+        if cs is not None:
+            cs_r = torch.empty_like(cs)
+            self.transport.all_to_all(cs, cs_r)
+            self._verify_rows(R.view(N, sb), cs_r, list(range(N)), "mesh all_to_all")
         wire.reduce(R, N, r, g[r * s:(r + 1) * s], S, None, s, c)
         G = self._buf(L, "mesh_G", sb * N)
         self.transport.all_gather(S, G)
+        if self.verify:
+            cs_g = torch.empty(N, 3, dtype=torch.int64, device=G.device)
+            self.transport.all_gather(self._tag(S.view(1, sb)), cs_g)
+            self._verify_rows(G.view(N, sb), cs_g, list(range(N)), "mesh all_gather")
         return [lambda: finish(G, s, N, 0, L.n_pad)]
 
     def _ring(self, L, grad, finish, owner_fp32, allow_compat):
@@ -426,6 +468,7 @@ class CompressedAllReduce:
             o = ring["off"] + x * S
             return g[o:o + S]
 
+        checks = []
         for ri, rnd in enumerate(rounds):
             sends, recvs = [], []
             for j in rnd:
@@ -446,8 +489,11 @@ class CompressedAllReduce:
                     elif src == 2:  # FORWARD (already-encoded full slice)
                         out = Gs(send_slice)
                     if out is not None and N > 1:
+                        cs = self._tag(out.view(1, sb)) if self.verify else None
                         self.fault.maybe_corrupt("ring_send", out)
                         sends.append((out, ring["down"]))
+                        if cs is not None:
+                            sends.append((cs, ring["down"]))
                     if recv_slice >= 0:
                         if recv_full:
                             tgt = Gs(recv_slice)
@@ -455,8 +501,15 @@ class CompressedAllReduce:
                             tgt = ring["recv"][j % 2]
                             ring["last_partial"] = tgt
                         recvs.append((tgt, ring["up"]))
+                        if self.verify:
+                            cs_r = torch.empty(1, 3, dtype=torch.int64, device=tgt.device)
+                            recvs.append((cs_r, ring["up"]))
+                            checks.append((tgt, cs_r, ring["up"], f"ring round {ri} slice {recv_slice}"))
             if N > 1:
                 self.transport.sendrecv(sends, recvs)
+                for tgt, cs_r, peer, what in checks:
+                    self._verify_rows(tgt.view(1, sb), cs_r, [peer], what)
+                checks.clear()
         thunks = []
         for i, ring in enumerate(rings):
             off = ring["off"]

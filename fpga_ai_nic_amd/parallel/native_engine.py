@@ -88,18 +88,21 @@ class NativeAllReduce:
 
     def __init__(self, transport: Transport | None, *, codec: str = "bfp_rne", algo: str = "mesh", rings: int = 1,
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
-                 timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False):
+                 timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None):
+        """``comm``: an explicit ``_C.Comm`` (e.g. ``_C.LoopbackFabric(N).comm(r)`` for virtual ranks on one
+        GPU); otherwise the engine's own RCCL communicator is created from ``transport``."""
         if algo not in _ALGOS:
             raise ValueError(f"unknown algo {algo!r}")
         C = _ext.require()
         self.transport = transport
         self.rank = transport.rank if transport is not None else 0
         self.world = transport.world if transport is not None else 1
+        if comm is not None:
+            self.rank, self.world = comm.rank, comm.world
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if self.device.type != "cuda":
             raise RuntimeError("the native engine runs on GPU only")
-        comm = None
-        if self.world > 1 or force_comm:
+        if comm is None and (self.world > 1 or force_comm):
             if not isinstance(transport, NativeTransport):
                 transport = NativeTransport(self.rank, self.world, self.device.index, force_collectives=force_comm)
                 self.transport = transport
