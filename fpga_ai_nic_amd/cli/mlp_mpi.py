@@ -9,9 +9,12 @@ Positional signature kept from sw/mlp_mpi_example_f32.cpp:270-320::
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m fpga_ai_nic_amd.cli.mlp_mpi \
         20 5376 0 A 32 32 32 2048 2048 2048 2048 2048 2048 2048 2048 2048 2048 2048 --dtype f32
 
-(the reference run.sh workload: 10 FC layers of 2048, global MB 5376). ``type`` must be 'A' (FWD+BWD+UPD;
-'F'/'B' are validated but, as in the reference, only 'A' runs). ``fuse_type``: 0 none, 1 bias, 2 relu,
-3 bias+relu (the framework always fuses bias+ReLU into the GEMM epilogue; the flag is validated and reported).
+(the reference run.sh workload: 10 FC layers of 2048, global MB 5376). ``type``: 'A' FWD+BWD+UPD (the
+reference's live path), 'F' forward only, 'B' backward+all-reduce/UPD only (the reference's commented-out
+modes, sw:543-680, with their GFLOP formulas and PERFDUMP,FP / PERFDUMP,BP lines). ``fuse_type`` selects the
+layer epilogue fused into the GEMMs exactly as the reference maps it (sw:479-489): 0 none, 1 bias,
+2 ReLU (with mask), 3 bias+ReLU, 4/5 fall back to none. ``--model-fuse hidden`` instead applies bias+ReLU to
+the hidden layers only (the bench.py model).
 """
 from __future__ import annotations
 
@@ -39,6 +42,8 @@ def build_parser():
     ap.add_argument("bk", type=int, nargs="?", default=64)
     ap.add_argument("bc", type=int, nargs="?", default=64)
     ap.add_argument("C", type=int, nargs="*")
+    ap.add_argument("--model-fuse", default="ref", choices=["ref", "hidden"],
+                    help="ref: fuse_type semantics on every layer; hidden: bias+ReLU on hidden layers only")
     return add_named_flags(ap)
 
 
@@ -53,8 +58,6 @@ def run(argv=None, out=sys.stdout):
     a = build_parser().parse_args(argv)
     if a.type not in ("A", "F", "B"):
         raise SystemExit("type needs to be 'A' (ALL), 'F' (FWD) or 'B' (BWD)")
-    if a.type != "A":
-        raise SystemExit("only type 'A' (FWD+BWD+UPD) is implemented, as in the reference (sw:543-680)")
     if a.fuse_type not in (0, 1, 2, 3, 4, 5):
         raise SystemExit("fuse_type needs to be 0..5")
     sizes = a.C if a.C else [1024, 4096, 4096, 1024]
@@ -85,7 +88,12 @@ def run(argv=None, out=sys.stdout):
                          max_slice_elems=cfg.slice_elems, compat_owner_fp32=cfg.compat_owner_fp32,
                          timeout_s=cfg.timeout_s)
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
-    model = MLP(sizes, dtype=dtype, device=device, pad_fn=pad_fn, seed=cfg.seed, momentum=cfg.momentum > 0)
+    if a.model_fuse == "hidden":
+        bias, relu = True, "hidden"
+    else:  # reference fuse_type mapping (sw:479-489)
+        bias, relu = {1: (True, "none"), 2: (False, "all"), 3: (True, "all")}.get(a.fuse_type, (False, "none"))
+    model = MLP(sizes, dtype=dtype, device=device, pad_fn=pad_fn, seed=cfg.seed, momentum=cfg.momentum > 0,
+                bias=bias, relu=relu)
     if world > 1:  # reference C3/C4: broadcast weights + bias from rank 0
         for l in model.layers:
             transport.broadcast_(l.master, 0)
@@ -101,21 +109,33 @@ def run(argv=None, out=sys.stdout):
         print(" ".join(str(v) for v in (argv if argv is not None else sys.argv[1:])), file=out)
         print(metrics.setup_banner(sizes, cfg.global_mb, cfg.iters, threads, 2 if dtype == torch.bfloat16 else 4),
               file=out)
+    def one_iter():
+        if a.type == "A":
+            trainer.step(x, y)
+        elif a.type == "F":  # forward + loss forward (the fused softmax-xent kernel also emits dlogits)
+            trainer.forward_pass(x)
+            model.loss_backward(y, grad_scale=cfg.loss_scale / mb)
+        else:  # 'B': loss bwd + backward + all-reduce/UPD on the activations of one forward
+            trainer.backward_pass(y)
+
+    if a.type == "B":
+        trainer.forward_pass(x)
     for _ in range(cfg.warmup):
-        trainer.step(x, y)
+        one_iter()
     trainer.finish()
     trainer.times = {k: 0 if k == "steps" else 0.0 for k in trainer.times}
     D.barrier()
     t0 = time.perf_counter()
     for _ in range(cfg.iters):
-        loss_rows = trainer.step(x, y)
+        one_iter()
+    loss_rows = model.loss_rows
     trainer.finish()
     D.barrier()
     total = D.max_over_ranks(time.perf_counter() - t0)
     loss = float(loss_rows.float().mean().item())
     if rank == 0:
         print(metrics.result_report(sizes, cfg.global_mb, mb, cfg.iters, total, threads,
-                                    trainer.times if cfg.profile else None), file=out)
+                                    trainer.times if cfg.profile else None, kind=a.type), file=out)
         print(f"LOSS = {loss:.6g}", file=out)
         if engine is not None:
             print(f"ALLREDUCE: algo={engine.algo} codec={engine.codec} rings={engine.rings} "

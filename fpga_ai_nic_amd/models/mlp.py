@@ -63,9 +63,16 @@ class MLP:
     """Manual-backprop MLP whose hot ops are the framework's HIP kernels (on GPU)."""
 
     def __init__(self, sizes, *, dtype=torch.bfloat16, device="cpu", pad_fn=None, seed: int = 1,
-                 momentum: bool = False, init_scale: float | None = None):
+                 momentum: bool = False, init_scale: float | None = None, bias: bool = True,
+                 relu: str = "hidden"):
+        """``bias`` / ``relu`` select the layer epilogue. ``relu``: 'hidden' (every layer but the classifier,
+        the default model), 'all' or 'none'. The reference's fuse_type (sw:479-489) maps to
+        0 -> (bias=False, relu='none'), 1 -> (True, 'none'), 2 -> (False, 'all'), 3 -> (True, 'all')."""
         if len(sizes) < 2:
             raise ValueError("need at least one layer")
+        if relu not in ("hidden", "all", "none"):
+            raise ValueError(f"relu must be hidden|all|none, got {relu!r}")
+        self.bias, self.relu = bias, relu
         self.sizes = list(sizes)
         self.L = len(sizes) - 1
         self.dtype = dtype
@@ -80,13 +87,26 @@ class MLP:
             master = torch.zeros(n_pad, dtype=torch.float32)
             bound = init_scale if init_scale is not None else 1.0 / math.sqrt(cin)
             master[: cin * cout] = (torch.rand(cin * cout, generator=gen) * 2 - 1) * bound
-            master[cin * cout: n] = (torch.rand(cout, generator=gen) * 2 - 1) * bound
+            b0 = (torch.rand(cout, generator=gen) * 2 - 1) * bound
+            master[cin * cout: n] = b0 if bias else 0.0  # without bias the segment stays 0 (zero gradient)
             master = master.to(self.device)
             lp = master.to(torch.bfloat16) if dtype == torch.bfloat16 else None
             grad = torch.zeros(n_pad, dtype=torch.float32, device=self.device)
             mom = torch.zeros(n_pad, dtype=torch.float32, device=self.device) if momentum else None
             self.layers.append(LayerBucket(cin, cout, n, n_pad, master, grad, lp, mom))
         self._act_mb = None
+        self._zero_b: dict[int, torch.Tensor] = {}
+
+    def _relu_at(self, i: int) -> bool:
+        return self.relu == "all" or (self.relu == "hidden" and i + 1 < self.L)
+
+    def _bias_of(self, l: LayerBucket):
+        if self.bias:
+            return l.b
+        z = self._zero_b.get(l.cout)
+        if z is None:
+            z = self._zero_b[l.cout] = torch.zeros(l.cout, dtype=l.b.dtype, device=self.device)
+        return z
 
     # ------------------------------------------------------------------ parameters
     def num_params(self) -> int:
@@ -134,14 +154,18 @@ class MLP:
     def forward_layer(self, i: int):
         l = self.layers[i]
         out = self.act[i + 1] if i + 1 < self.L else self.logits
-        G.linear_fwd(self.act[i], l.w, l.b, out, relu=(i + 1 < self.L))
+        G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i))
 
     def loss_backward(self, labels, grad_scale: float):
         NN.softmax_xent(self.logits, labels, self.dz[self.L], self.loss_rows, grad_scale)
+        if self._relu_at(self.L - 1):  # ReLU on the classifier output (reference fuse_type 2/3)
+            self.dz[self.L].mul_(self.logits > 0)
 
     def backward_weight(self, i: int):
         l = self.layers[i]
-        if l.gw.is_cuda and self.dtype == torch.bfloat16:  # bias gradient fused into the bwd-weight GEMM
+        if not self.bias:
+            G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
+        elif l.gw.is_cuda and self.dtype == torch.bfloat16:  # bias gradient fused into the bwd-weight GEMM
             G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw, bias_grad=l.gb)
         else:
             G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
@@ -151,7 +175,7 @@ class MLP:
         if i == 0:
             return
         l = self.layers[i]
-        G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i], relu_input=self.act[i])
+        G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i], relu_input=self.act[i] if self._relu_at(i - 1) else None)
 
     def forward(self, x):
         """Inference forward (returns f32 logits)."""

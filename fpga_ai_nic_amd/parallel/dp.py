@@ -93,34 +93,50 @@ class DataParallelTrainer:
                  n_valid=l.n)
 
     def step(self, x: torch.Tensor, labels: torch.Tensor):
+        """One training iteration (reference type 'A': FWD + loss + BWD + all-reduce/UPD)."""
+        self.forward_pass(x)
+        self.backward_pass(labels)
+        self.times["steps"] += 1
+        self.step_count += 1
+        return self.m.loss_rows
+
+    def forward_pass(self, x: torch.Tensor):
+        """Forward of every layer (reference type 'F' times this plus the loss forward)."""
         m = self.m
-        mb = x.shape[0]
-        m.alloc_activations(mb)
+        m.alloc_activations(x.shape[0])
         m.act[0] = x
-        prof = self.profile
         t0 = time.perf_counter()
         with tracing.range("fwd"):
-            # Weights of every layer must be updated before its forward. All requests of a step run in issue
-            # order (L-1 .. 0) on the engine's single comm stream, so on GPU ONE wait on the last-issued handle
-            # covers them all (each cross-stream wait costs a barrier packet on the compute queue).
-            if self.last_handle is not None:
-                if self.cuda:
-                    self.last_handle.wait()
-                else:
-                    for h in self.pending:
-                        if h is not None:
-                            h.synchronize()
-                self.pending = [None] * m.L
-                self.last_handle = None
+            self._wait_updates()
             for i in range(m.L):
                 m.forward_layer(i)
-        if prof:
+        if self.profile:
             self._sync()
-            t1 = time.perf_counter()
-            self.times["fwd"] += t1 - t0
-            t0 = t1
+            self.times["fwd"] += time.perf_counter() - t0
+
+    def _wait_updates(self):
+        """Weights must be updated before they are read again. All requests of a step run in issue order
+        (L-1 .. 0) on the engine's single comm stream, so on GPU ONE wait on the last-issued handle covers
+        them all (each cross-stream wait costs a barrier packet on the compute queue)."""
+        if self.last_handle is None:
+            return
+        if self.cuda:
+            self.last_handle.wait()
+        else:
+            for h in self.pending:
+                if h is not None:
+                    h.synchronize()
+        self.pending = [None] * self.m.L
+        self.last_handle = None
+
+    def backward_pass(self, labels: torch.Tensor):
+        """Loss fwd+bwd, then per layer L-1..0: dW -> async all-reduce+SGD -> dX (reference type 'B')."""
+        m = self.m
+        prof = self.profile
+        self._wait_updates()  # no-op after forward_pass; needed when backward passes run back to back
+        t0 = time.perf_counter()
         with tracing.range("loss"):
-            m.loss_backward(labels, grad_scale=self.loss_scale / mb)
+            m.loss_backward(labels, grad_scale=self.loss_scale / m.act[0].shape[0])
         if prof:
             self._sync()
             t1 = time.perf_counter()
@@ -151,9 +167,6 @@ class DataParallelTrainer:
         if prof:
             self._sync()
             self.times["bwd"] += time.perf_counter() - t0
-        self.times["steps"] += 1
-        self.step_count += 1
-        return m.loss_rows
 
     def _sync(self):
         if self.cuda:

@@ -13,13 +13,15 @@ import time
 from .. import __version__
 
 
-def mlp_gflop(sizes, global_mb: int) -> float:
-    """The reference formula (sw:794-798): 6*MB*C_i*C_{i+1} for layers >= 1, 4*MB*C0*C1 for layer 0."""
+def mlp_gflop(sizes, global_mb: int, kind: str = "A") -> float:
+    """The reference formulas. 'A' (sw:794-798): 6*MB*C_i*C_{i+1} for layers >= 1, 4*MB*C0*C1 for layer 0;
+    'F' (sw:574-577): 2*MB*C_i*C_{i+1}; 'B' (sw:654-658): 4*MB*C_i*C_{i+1} for layers >= 1, 2*MB*C0*C1."""
+    hi, lo = {"A": (6.0, 4.0), "F": (2.0, 2.0), "B": (4.0, 2.0)}[kind]
     g = 0.0
     L = len(sizes) - 1
     for i in range(L - 1, 0, -1):
-        g += 6.0 * global_mb * sizes[i] * sizes[i + 1] / 1e9
-    g += 4.0 * global_mb * sizes[0] * sizes[1] / 1e9
+        g += hi * global_mb * sizes[i] * sizes[i + 1] / 1e9
+    g += lo * global_mb * sizes[0] * sizes[1] / 1e9
     return g
 
 
@@ -51,13 +53,13 @@ def setup_banner(sizes, global_mb: int, iters: int, threads: int, bytes_per_el: 
 
 
 def result_report(sizes, global_mb: int, mb_local: int, iters: int, total_s: float, threads: int,
-                  times: dict | None = None) -> str:
-    gflop = mlp_gflop(sizes, global_mb)
+                  times: dict | None = None, kind: str = "A") -> str:
+    gflop = mlp_gflop(sizes, global_mb, kind)
     t = total_s / max(iters, 1)
     gflops = gflop / t if t > 0 else 0.0
     L = len(sizes) - 1
     lines = [f"GFLOP  = {gflop:.5g}", f"fp time = {t:.5g}", f"GFLOPS  = {gflops:.5g}",
-             "PERFDUMP,BP,fan-" + __version__ + f",{threads},{mb_local}," + "".join(f"{c}," for c in sizes[:L])
+             f"PERFDUMP,{'FP' if kind == 'F' else 'BP'},fan-" + __version__ + f",{threads},{mb_local}," + "".join(f"{c}," for c in sizes[:L])
              + f"{t:f},{gflops:f}",
              f"SAMPLES/S = {global_mb / t if t > 0 else 0.0:.5g}"]
     if times and times.get("steps"):
