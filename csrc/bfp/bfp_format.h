@@ -178,6 +178,9 @@ void launch_wire_pack(int codec, int in_dtype, const void* in, void* out, size_t
                       hipStream_t stream);
 void launch_wire_unpack(int codec, int out_dtype, const void* in, void* out, size_t n_s, int n_shards,
                         hipStream_t stream);
+// Pack flat elements [begin, end) (multiples of 16) into the shard layout (shards of n_s elements).
+void launch_wire_pack_range(int codec, int in_dtype, const void* in, void* out, size_t n_s, size_t begin,
+                            size_t end, hipStream_t stream);
 // out = sum over slots (slot self_pos replaced by the dense local operand when given).
 void launch_wire_reduce(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots,
                         int self_pos, const void* local, void* out_wire, float* out_f32, size_t n_s,

@@ -36,6 +36,23 @@ __global__ void __launch_bounds__(kBlock) wire_pack_kernel(const TIN* __restrict
   }
 }
 
+// Pack flat elements [begin, end) (multiples of 16) of a bucket into its shard layout (shards of n_s elements):
+// the part of a bucket the producing GEMM did not encode itself (bias gradient + padding).
+template <typename TIN, int C>
+__global__ void __launch_bounds__(kBlock) wire_pack_range_kernel(const TIN* __restrict__ in, uint8_t* __restrict__ out,
+                                                                size_t n_s, size_t begin, size_t end) {
+  const size_t tasks = (end - begin) >> 3;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t sb = wire_shard_bytes(C, n_s);
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+    const size_t f = begin + (t << 3);
+    const size_t sh = f / n_s;
+    float v[8];
+    DenseLane<TIN>::load8(in, f, v);
+    WireLane<C>::store8(out + sh * sb, n_s, f - sh * n_s, v);
+  }
+}
+
 template <typename TOUT, int C>
 __global__ void __launch_bounds__(kBlock) wire_unpack_kernel(const uint8_t* __restrict__ in, TOUT* __restrict__ out,
                                                             size_t n_s, int n_shards) {
@@ -153,6 +170,23 @@ void launch_wire_pack(int codec, int in_dtype, const void* in, void* out, size_t
     else
       hipLaunchKernelGGL((wire_pack_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const bf16_t*)in,
                          (uint8_t*)out, n_s, n_shards);
+  });
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+void launch_wire_pack_range(int codec, int in_dtype, const void* in, void* out, size_t n_s, size_t begin,
+                            size_t end, hipStream_t stream) {
+  check_ns(n_s);
+  FAN_CHECK(begin % 16 == 0 && end % 16 == 0 && begin <= end, "pack_range: bounds must be multiples of 16");
+  if (end == begin) return;
+  const int grid = stream_grid((end - begin) / 8, kBlock);
+  FAN_CODEC_SWITCH(codec, {
+    if (in_dtype == kF32)
+      hipLaunchKernelGGL((wire_pack_range_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in,
+                         (uint8_t*)out, n_s, begin, end);
+    else
+      hipLaunchKernelGGL((wire_pack_range_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const bf16_t*)in,
+                         (uint8_t*)out, n_s, begin, end);
   });
   FAN_HIP_CHECK(hipGetLastError());
 }

@@ -37,6 +37,21 @@ void wire_pack(const at::Tensor& x, at::Tensor& out, int64_t shard_elems, int64_
                         fan_stream());
 }
 
+void wire_pack_range(const at::Tensor& x, at::Tensor& out, int64_t shard_elems, int64_t begin, int64_t end,
+                     int64_t codec) {
+  FAN_T_CUDA_CONTIG(x);
+  FAN_T_CUDA_CONTIG(out);
+  TORCH_CHECK(out.scalar_type() == at::kByte, "packed buffer must be uint8");
+  TORCH_CHECK(shard_elems > 0 && shard_elems % 256 == 0, "shard_elems must be a positive multiple of 256");
+  TORCH_CHECK(0 <= begin && begin <= end && end <= x.numel() && begin % 16 == 0 && end % 16 == 0, "bad range");
+  if (end == begin) return;
+  const int64_t shards = (end - 1) / shard_elems + 1;
+  TORCH_CHECK((int64_t)out.numel() >= (int64_t)fan::wire_shard_bytes((int)codec, shard_elems) * shards,
+              "packed buffer too small");
+  fan::launch_wire_pack_range((int)codec, dtype_code(x), x.data_ptr(), out.data_ptr(), (size_t)shard_elems,
+                              (size_t)begin, (size_t)end, fan_stream());
+}
+
 void wire_unpack(const at::Tensor& packed, at::Tensor& out, int64_t shard_elems, int64_t codec) {
   FAN_T_CUDA_CONTIG(packed);
   FAN_T_CUDA_CONTIG(out);
@@ -114,6 +129,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wire_shard_bytes", [](int64_t codec, int64_t n_s) { return (int64_t)fan::wire_shard_bytes((int)codec, n_s); });
   m.def("wire_pack", &wire_pack, "encode dense f32/bf16 into the wire format (per shard)");
   m.def("wire_unpack", &wire_unpack, "decode wire format into dense f32/bf16");
+  m.def("wire_pack_range", &wire_pack_range, "encode flat elements [begin, end) into the shard layout");
   m.def("wire_reduce", &wire_reduce, "sum wire slots (+ dense local) -> wire and/or f32", pybind11::arg("slots"),
         pybind11::arg("n_slots"), pybind11::arg("self_pos"), pybind11::arg("local"), pybind11::arg("out_wire"),
         pybind11::arg("out_f32"), pybind11::arg("shard_elems"), pybind11::arg("codec"));

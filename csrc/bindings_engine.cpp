@@ -103,7 +103,8 @@ void register_engine(pybind11::module_& m) {
       .def("submit",
            [](AllReduceEngine& e, const at::Tensor& grad, at::Tensor& master, c10::optional<at::Tensor> lp,
               c10::optional<at::Tensor> mom, int64_t n_valid, double lr, double grad_scale, double wd,
-              double momentum, bool nesterov, bool defer, bool update, c10::optional<at::Tensor> out_sum) {
+              double momentum, bool nesterov, bool defer, bool update, c10::optional<at::Tensor> out_sum,
+              c10::optional<at::Tensor> prepacked, int64_t prepacked_elems) {
              FAN_T_CUDA_CONTIG(grad);
              TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
                          "gradients must be f32 or bf16");
@@ -133,15 +134,31 @@ void register_engine(pybind11::module_& m) {
                            "out_sum: f32[n_pad]");
                outp = out_sum->data_ptr<float>();
              }
+             const uint8_t* pre = nullptr;
+             if (prepacked && prepacked->defined()) {
+               FAN_T_CUDA_CONTIG(*prepacked);
+               const auto shp = e.prepack_shape(n_valid);
+               TORCH_CHECK(shp[0] > 0, "this engine configuration cannot take prepacked input");
+               TORCH_CHECK(prepacked->scalar_type() == at::kByte &&
+                               prepacked->numel() >= shp[1] * (int64_t)wire_shard_bytes(e.codec(), shp[0]),
+                           "prepacked wire buffer too small");
+               pre = prepacked->data_ptr<uint8_t>();
+             }
              SgdParams p{(float)lr, (float)grad_scale, (float)wd, (float)momentum, nesterov ? 1 : 0};
              return e.submit(grad.data_ptr(), grad.scalar_type() == at::kFloat ? kF32 : kBF16,
                              update ? master.data_ptr<float>() : nullptr, lpp, momp, n_valid, p, fan_stream(), defer,
-                             update, outp);
+                             update, outp, pre, prepacked_elems);
            },
            py::arg("grad"), py::arg("master"), py::arg("lp") = py::none(), py::arg("mom") = py::none(),
            py::arg("n_valid"), py::arg("lr"), py::arg("grad_scale") = 1.0, py::arg("weight_decay") = 0.0,
            py::arg("momentum") = 0.0, py::arg("nesterov") = false, py::arg("defer") = false,
-           py::arg("update") = true, py::arg("out_sum") = py::none(), py::call_guard<py::gil_scoped_release>())
+           py::arg("update") = true, py::arg("out_sum") = py::none(), py::arg("prepacked") = py::none(),
+           py::arg("prepacked_elems") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("prepack_shape", [](AllReduceEngine& e, int64_t n) {
+        const auto s = e.prepack_shape(n);
+        return py::make_tuple(s[0], s[1], s[2]);
+      })
+      .def_property_readonly("codec", &AllReduceEngine::codec)
       .def(
           "commit",
           [](AllReduceEngine& e, int slot, bool after_current) {

@@ -28,7 +28,8 @@ int64_t ld_of(const at::Tensor& t) {
 void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tensor& C, int64_t epilogue,
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux, bool accumulate,
           int64_t split_k, const c10::optional<at::Tensor>& workspace, int64_t tile_bm, int64_t tile_bn,
-          const c10::optional<at::Tensor>& colsum, int64_t tile_waves) {
+          const c10::optional<at::Tensor>& colsum, int64_t tile_waves, const c10::optional<at::Tensor>& wire,
+          int64_t wire_shard, int64_t wire_own, int64_t wire_codec) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "A and B dtype mismatch");
   GemmArgs g{};
@@ -69,6 +70,18 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     g.ldaux = ld_of(*aux);
   }
   if (workspace) g.workspace = workspace->data_ptr();
+  if (epilogue == kEpiWire) {
+    TORCH_CHECK(wire && wire->is_cuda() && wire->is_contiguous() && wire->scalar_type() == at::kByte,
+                "wire epilogue needs a contiguous uint8 GPU wire buffer");
+    TORCH_CHECK(wire_shard > 0 && wire_shard % 256 == 0, "wire_shard must be a positive multiple of 256");
+    const int64_t last = (int64_t)(g.M - 1) * g.ldc + g.N - 1;
+    const int64_t need = (last / wire_shard + 1) * (int64_t)wire_shard_bytes((int)wire_codec, (size_t)wire_shard);
+    TORCH_CHECK(wire->numel() >= need, "wire buffer too small: ", wire->numel(), " < ", need);
+    g.wire = wire->data_ptr<uint8_t>();
+    g.wire_shard = wire_shard;
+    g.wire_own = (int)wire_own;
+    g.wire_codec = (int)wire_codec;
+  }
   if (A.scalar_type() == at::kBFloat16) {
     TORCH_CHECK(bias ? bias->scalar_type() == at::kBFloat16 : true, "bias must be bf16");
     TORCH_CHECK(gemm_bf16_supported(g), "gemm_bf16: unsupported shape M=", g.M, " N=", g.N, " K=", g.K,
@@ -128,7 +141,9 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("b_t"), pybind11::arg("C"), pybind11::arg("epilogue") = 0, pybind11::arg("bias") = pybind11::none(),
         pybind11::arg("aux") = pybind11::none(), pybind11::arg("accumulate") = false, pybind11::arg("split_k") = 1,
         pybind11::arg("workspace") = pybind11::none(), pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0,
-        pybind11::arg("colsum") = pybind11::none(), pybind11::arg("tile_waves") = 0);
+        pybind11::arg("colsum") = pybind11::none(), pybind11::arg("tile_waves") = 0,
+        pybind11::arg("wire") = pybind11::none(), pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1,
+        pybind11::arg("wire_codec") = 1);
   m.def("gemm_supported", &gemm_supported);
   m.def("gemm_plan", &gemm_plan, "bf16 GEMM tile/split-K plan (bm, bn, split_k, waves); bm == 0: unsupported",
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0,
@@ -137,6 +152,7 @@ void register_gemm(pybind11::module_& m) {
   m.attr("EPI_BIAS") = (int)kEpiBias;
   m.attr("EPI_BIAS_RELU") = (int)kEpiBiasRelu;
   m.attr("EPI_RELU_MASK") = (int)kEpiReluMask;
+  m.attr("EPI_WIRE") = (int)kEpiWire;
 }
 
 void register_nn(pybind11::module_& m) {

@@ -111,22 +111,39 @@ static void epilogue(int codec, hipStream_t st, const uint8_t* G, int64_t shard,
   if (out_sum) launch_wire_unpack(codec, kF32, G, out_sum + off, (size_t)shard, n_shards, st);
 }
 
+std::array<int64_t, 3> AllReduceEngine::prepack_shape(int64_t n) const {
+  if (cfg_.algo != 0 || (cfg_.codec != kBfpTrunc && cfg_.codec != kBfpRne)) return {0, 0, -1};
+  const EngineLayout L = layout(n);
+  const bool local = (world_ == 1 && !cfg_.force_comm) || comm_ == nullptr;
+  return {L.shard, world_, local ? -1 : rank_};
+}
+
 std::vector<std::function<void()>> AllReduceEngine::run_mesh(const EngineLayout& L, const void* grad, int gdt,
                                                              float* master, bf16_t* lp, float* mom, int64_t n_valid,
-                                                             SgdParams p, bool update, float* out_sum) {
+                                                             SgdParams p, bool update, float* out_sum,
+                                                             const uint8_t* prepacked, int64_t prepacked_elems) {
   const int N = world_, r = rank_, c = cfg_.codec;
   const int64_t s = L.shard;
   const size_t sb = wire_shard_bytes(c, s);
   const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
-  uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
   hipStream_t st = run_stream_;
+  if (prepacked) {  // encode what the producer did not (bias gradient + padding)
+    launch_wire_pack_range(c, gdt, grad, const_cast<uint8_t*>(prepacked), (size_t)s, (size_t)prepacked_elems,
+                           (size_t)L.n_pad, st);
+  }
   if ((N == 1 && !cfg_.force_comm) || comm_ == nullptr) {
+    if (prepacked) {  // the producer's encoding IS the (single-rank) result: no reduce pass
+      const uint8_t* W = prepacked;
+      return {[=] { epilogue(c, st, W, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
+    }
+    uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
     launch_wire_reduce(c, gdt, S, sb, 1, 0, g, S, nullptr, (size_t)s, st);
     return {[=] { epilogue(c, st, S, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
   }
-  const uint8_t* P = g;
+  uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
+  const uint8_t* P = prepacked ? prepacked : g;
   const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
-  if (!zero_copy) {
+  if (!zero_copy && !prepacked) {
     uint8_t* Pb = scratch("mesh_P" + std::to_string(sb * N), sb * N);
     launch_wire_pack(c, gdt, g, Pb, (size_t)s, N, st);
     P = Pb;
@@ -244,7 +261,8 @@ std::vector<std::function<void()>> AllReduceEngine::run_ring(const EngineLayout&
 }
 
 int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
-                            SgdParams sgd, hipStream_t producer, bool defer, bool update, float* out_sum) {
+                            SgdParams sgd, hipStream_t producer, bool defer, bool update, float* out_sum,
+                            const uint8_t* prepacked, int64_t prepacked_elems) {
   FAN_HIP_CHECK(hipSetDevice(device_));
   const int slot = next_slot_;
   next_slot_ = (slot + 1) % kSlots;
@@ -258,7 +276,12 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   }
   sl.timed = timing_;
   if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t0, sl.stream));
-  sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum)
+  if (prepacked) {
+    FAN_CHECK(prepack_shape(n_valid)[0] > 0, "prepacked input needs the mesh algorithm and a BFP codec");
+    FAN_CHECK(prepacked_elems % 16 == 0 && prepacked_elems <= L.n_pad, "bad prepacked_elems");
+  }
+  sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum,
+                                        prepacked, prepacked_elems)
                              : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
   FAN_HIP_CHECK(hipGetLastError());
   sl.pending = true;

@@ -58,11 +58,19 @@ class AllReduceEngine {
   const std::vector<std::vector<int>>& orders() const { return orders_; }
   hipStream_t stream() const { return stream_; }
   bool is_inline() const { return inline_; }
+  int codec() const { return cfg_.codec; }
 
   // Enqueue the communication phase of a request. grad: padded flat buffer (f32 or bf16) ready on `producer`.
   // If `defer`, the weight update is enqueued later by commit(); otherwise immediately. Returns the slot.
+  // prepacked (mesh, BFP codecs): the producer already encoded flat elements [0, prepacked_elems) of the bucket
+  // into `prepacked` (mesh shard layout, prepack_shape()); the engine packs the rest (bias + padding) and skips
+  // the pack pass (and, at world 1, the reduce pass). The owner shard must also be present in f32 in `grad`.
   int submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
-             SgdParams sgd, hipStream_t producer, bool defer, bool update = true, float* out_sum = nullptr);
+             SgdParams sgd, hipStream_t producer, bool defer, bool update = true, float* out_sum = nullptr,
+             const uint8_t* prepacked = nullptr, int64_t prepacked_elems = 0);
+  // (shard elements, shards, owner shard whose f32 values the reduce needs or -1) for a prepacked bucket,
+  // or shard elements 0 when this configuration cannot take prepacked input.
+  std::array<int64_t, 3> prepack_shape(int64_t n) const;
   // Enqueue the deferred SGD epilogue after everything currently enqueued on `producer`.
   void commit(int slot, hipStream_t producer);
   void wait_stream(int slot, hipStream_t s);            // GPU-side wait
@@ -89,7 +97,7 @@ class AllReduceEngine {
   uint8_t* scratch(const std::string& key, size_t bytes);
   std::vector<std::function<void()>> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
-                                              float* out_sum);
+                                              float* out_sum, const uint8_t* prepacked, int64_t prepacked_elems);
   std::vector<std::function<void()>> run_ring(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                               float* out_sum);

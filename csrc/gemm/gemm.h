@@ -15,6 +15,7 @@ enum GemmEpilogue : int {
   kEpiBias = 1,       // + bias[n]
   kEpiBiasRelu = 2,   // relu(x + bias[n])
   kEpiReluMask = 3,   // x * (aux[m][n] > 0)   (ReLU backward fused into the bwd-data GEMM)
+  kEpiWire = 4,       // BFP-encode the f32 result straight into all-reduce wire shards (see GemmArgs::wire)
 };
 
 struct GemmArgs {
@@ -36,6 +37,14 @@ struct GemmArgs {
   int tile_waves = 0;  // 0: default; 4 or 8 waves per workgroup
   float* colsum = nullptr;  // optional: colsum[n] = sum_k B(k, n) (bias gradient fused into bwd-weight;
                             // B MN-contiguous, no split-K); written, not accumulated
+  // kEpiWire: element (m, n) of C sits at flat index f = m*ldc + n of a bucket split into shards of
+  // wire_shard elements; it is encoded (groups of 16 along n) into the wire layout of shard f / wire_shard
+  // (bfp_format.h). Elements of shard wire_own (>= 0) are also written to C in f32 (the owner's
+  // un-quantised local contribution for the mesh reduce). f32 output, no split-K, no accumulate.
+  uint8_t* wire = nullptr;
+  int64_t wire_shard = 0;
+  int wire_own = -1;
+  int wire_codec = 1;  // kBfpTrunc or kBfpRne
 };
 
 struct GemmPlan {

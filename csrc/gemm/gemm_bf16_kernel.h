@@ -21,6 +21,7 @@
 //   * split-K: K is split over workgroups, f32 partial slabs + an ordered (deterministic) reduce kernel
 //     that applies the same epilogue.
 #pragma once
+#include "bfp/bfp_format.h"
 #include "gemm/gemm.h"
 #include "gemm/glds.h"
 
@@ -160,13 +161,46 @@ __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc
   Out<TC>::store4(p, v);
 }
 
+// kEpiWire target (GemmArgs::wire*): passed by value as one kernel argument.
+struct WireOut {
+  uint8_t* p;
+  int64_t shard;  // elements per shard (multiple of 256)
+  int own;        // shard also written to C in f32 (-1: none)
+  int codec;      // kBfpTrunc / kBfpRne
+};
+
+// Encode 4 consecutive columns held by this lane; the 16-column group is the 4 lanes (lane & ~3) .. +3
+// (the LDS-staged epilogue hands each lane 4 columns of one row, 16-B aligned).
+__device__ __forceinline__ void wire_epi4(const float v[4], float* __restrict__ C, int64_t ldc, const WireOut& wo,
+                                          int row, int col, int lane) {
+  const int64_t f = (int64_t)row * ldc + col;
+  const int64_t sh = f / wo.shard;
+  const int64_t pos = f - sh * wo.shard;
+  uint32_t mx = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) mx = max(mx, __float_as_uint(v[u]) & 0x7FFFFFFFu);
+  mx = max(mx, (uint32_t)__shfl_xor((int)mx, 1));
+  mx = max(mx, (uint32_t)__shfl_xor((int)mx, 2));
+  const uint32_t E = mx >> 23;
+  uint32_t w = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int32_t q = wo.codec == kBfpTrunc ? bfp_encode_trunc(__float_as_uint(v[u]), E) : bfp_encode_rne(v[u], E);
+    w |= ((uint32_t)q & 0xFFu) << (8 * u);
+  }
+  uint8_t* base = wo.p + sh * (wo.shard + wo.shard / 16);
+  *reinterpret_cast<uint32_t*>(base + pos) = w;
+  if ((lane & 3) == 0) base[wo.shard + pos / 16] = (uint8_t)E;
+  if (sh == wo.own) *reinterpret_cast<float4*>(C + f) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 // 8 waves (2 per SIMD) or 4 waves (1 per SIMD, up to 512 VGPR+AGPR per lane: large per-wave tiles).
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
 __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
     gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                      TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                      int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
-                     float* __restrict__ colsum) {
+                     float* __restrict__ colsum, WireOut wo) {
   constexpr int NT = WM * WN * 64;
   constexpr int A_BYTES = OpTile<BM, NT>::BYTES, B_BYTES = OpTile<BN, NT>::BYTES;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -332,6 +366,8 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
       if (SPLIT) {
         float* slab = ws + (int64_t)ksplit * M * N;
         *reinterpret_cast<float4*>(slab + (int64_t)row * N + col) = q;
+      } else if constexpr (EPI == kEpiWire) {
+        wire_epi4(v, reinterpret_cast<float*>(C), ldc, wo, row, col, lane);
       } else {
         epi4<EPI, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
       }
@@ -375,7 +411,7 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
                        (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
-                       (float*)nullptr);
+                       (float*)nullptr, WireOut{nullptr, 0, -1, 0});
     hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
                        (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
                        a.ldaux, a.M, a.N);
@@ -384,7 +420,7 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
                        (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1, (float*)nullptr,
-                       a.colsum);
+                       a.colsum, WireOut{a.wire, a.wire_shard, a.wire_own, a.wire_codec});
   }
 }
 
@@ -401,6 +437,14 @@ void launch_epi(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_EPI_CASE(kEpiBias)
     FAN_EPI_CASE(kEpiBiasRelu)
     FAN_EPI_CASE(kEpiReluMask)
+    case kEpiWire:  // only the bwd-weight layout (A and B MN-contiguous) produces wire-ready gradients
+      if constexpr (!AK && !BKC) {
+        FAN_CHECK(sk == 1 && !a.c_bf16 && !a.accumulate, "wire epilogue: f32, no split-K, no accumulate");
+        launch_typed<BM, BN, WM, WN, AK, BKC, kEpiWire, float, false>(a, sk, s);
+        break;
+      }
+      FAN_CHECK(false, "wire epilogue needs A and B MN-contiguous (bwd-weight layout)");
+      break;
     default: FAN_CHECK(false, "bad epilogue");
   }
 #undef FAN_EPI_CASE

@@ -67,6 +67,11 @@ bool gemm_bf16_supported(const GemmArgs& a) {
   if (a.accumulate && a.c_bf16) return false;
   if (p.split_k > 1 && a.workspace == nullptr) return false;
   if (a.colsum && (p.split_k > 1 || a.b_kcontig)) return false;
+  if (a.epilogue == kEpiWire) {
+    if (p.split_k > 1 || a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire) return false;
+    if (a.wire_shard <= 0 || a.wire_shard % 256 || a.ldc % 16) return false;
+    if (a.wire_codec != kBfpTrunc && a.wire_codec != kBfpRne) return false;
+  }
   return true;
 }
 

@@ -17,7 +17,7 @@ import torch
 
 from .. import _ext
 
-EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK, EPI_WIRE = 0, 1, 2, 3, 4
 
 _ws: dict = {}
 
@@ -45,10 +45,22 @@ def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
 
 
 def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux=None, accumulate=False,
-         split_k: int | None = None, tile: tuple | None = None, colsum=None):
+         split_k: int | None = None, tile: tuple | None = None, colsum=None, wire=None):
     """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
     ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only).
-    ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N])."""
+    ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N]).
+    ``wire=(buf_u8, shard_elems, own_shard, codec_id)``: BFP-encode the f32 result straight into all-reduce
+    wire shards (flat index m*ldc + n; shard ``own_shard`` is also written to C) — bf16 bwd-weight only."""
+    if wire is not None:
+        if not C.is_cuda or A.dtype != torch.bfloat16 or not a_t or b_t:
+            raise ValueError("wire epilogue: bf16 GPU bwd-weight layout only")
+        Cx = _ext.require()
+        M, K, N = A.shape[1], A.shape[0], B.shape[1]
+        tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
+        buf, shard, own, codec = wire
+        Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, 1, None, tbm, tbn, colsum, tw, buf, int(shard),
+                int(own), int(codec))
+        return C
     if C.is_cuda:
         Cx = _ext.require()
         M = A.shape[1] if a_t else A.shape[0]
@@ -104,6 +116,9 @@ def linear_bwd_data(dz, w, out, relu_input=None):
     return gemm(dz, False, w, True, out, EPI_NONE)
 
 
-def linear_bwd_weight(x, dz, out, accumulate=False, bias_grad=None):
-    """dW = Xᵀ · dZ (f32 out); with ``bias_grad`` also db = colsum(dZ), fused into the same kernel."""
+def linear_bwd_weight(x, dz, out, accumulate=False, bias_grad=None, wire=None):
+    """dW = Xᵀ · dZ (f32 out); with ``bias_grad`` also db = colsum(dZ), fused into the same kernel; with
+    ``wire`` dW is written BFP-encoded into the all-reduce wire buffer instead (see :func:`gemm`)."""
+    if wire is not None:
+        return gemm(x, True, dz, False, out, EPI_WIRE, colsum=bias_grad, wire=wire)
     return gemm(x, True, dz, False, out, EPI_NONE, accumulate=accumulate, colsum=bias_grad)

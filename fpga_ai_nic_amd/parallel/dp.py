@@ -72,7 +72,7 @@ def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str
 class DataParallelTrainer:
     def __init__(self, model: MLP, engine: CompressedAllReduce | None, *, lr: float = 0.1,
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
-                 loss_scale: float = 1.0, average: bool = True, profile: bool = False):
+                 loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True):
         self.m = model
         self.engine = engine
         self.world = engine.world if engine is not None else 1
@@ -86,6 +86,9 @@ class DataParallelTrainer:
         self.profile = profile
         self.times = {"fwd": 0.0, "loss": 0.0, "bwd": 0.0, "bwd_first": 0.0, "steps": 0}
         self.step_count = 0
+        # fuse the BFP encode into the bwd-weight GEMM when the engine accepts prepacked wire input
+        self.prepack = (prepack and engine is not None and getattr(engine, "prepack", False) and self.cuda
+                        and model.dtype == torch.bfloat16)
 
     def _sgd_local(self, l):
         wire.sgd(wire.as_bytes(l.grad), l.n_pad, 1, l.master, codec="raw_f32", lp=l.lp, mom=l.mom, lr=self.lr,
@@ -145,13 +148,15 @@ class DataParallelTrainer:
         for i in reversed(range(m.L)):
             l = m.layers[i]
             with tracing.range(f"bwd{i}"):
-                m.backward_weight(i)
+                tgt = self.engine.prepack_target(l.grad, l.n) if self.prepack else None
+                m.backward_weight(i, wire=tgt)
                 h = None
                 if self.engine is not None:
+                    kw = {"prepacked": (tgt[0], l.cin * l.cout)} if tgt is not None else {}
                     h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
                                                   grad_scale=self.grad_scale, weight_decay=self.wd,
                                                   momentum=self.momentum, nesterov=self.nesterov, defer=True,
-                                                  name=f"fc{i}")
+                                                  name=f"fc{i}", **kw)
                 m.backward_data(i)
                 if h is not None:
                     self.pending[i] = h.commit_after_current()

@@ -115,6 +115,9 @@ class NativeAllReduce:
         self.rings = len(self.orders)
         self.inline = bool(self.C.inline)
         self.cuda = True
+        # producers (the bwd-weight GEMM) may write BFP wire shards directly: see prepack_target()
+        self.prepack = self.C.prepack_shape(1 << 20)[0] > 0
+        self._prepack_bufs: dict = {}
         self._timing = False
         self.stats = {"requests": 0, "wire_bytes": 0, "logical_bytes": 0}
 
@@ -139,15 +142,32 @@ class NativeAllReduce:
     def wire_bytes(self, L: BucketLayout) -> int:
         return int(self.C.wire_bytes(L.n))
 
+    def prepack_target(self, grad: torch.Tensor, n: int):
+        """Wire target for a producer that encodes the gradient itself (GEMM ``kEpiWire`` epilogue):
+        ``(wire_u8, shard_elems, own_shard, codec_id)`` — one persistent buffer per gradient bucket — or None
+        when this configuration (ring / raw codec) cannot take prepacked input."""
+        shard, shards, own = self.C.prepack_shape(int(n))
+        if shard == 0:
+            return None
+        need = shards * wire.shard_bytes(self.codec_id, shard)
+        key = grad.data_ptr()
+        buf = self._prepack_bufs.get(key)
+        if buf is None or buf.numel() < need:
+            buf = self._prepack_bufs[key] = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return buf, shard, own, self.codec_id
+
     def allreduce_sgd(self, grad: torch.Tensor, master: torch.Tensor, lp: torch.Tensor | None = None,
                       mom: torch.Tensor | None = None, *, n_valid: int | None = None, lr: float,
                       grad_scale: float = 1.0, weight_decay: float = 0.0, momentum: float = 0.0,
                       nesterov: bool = False, update_after=None, defer: bool = False,
-                      name: str = "bucket") -> NativeHandle:
+                      name: str = "bucket", prepacked=None) -> NativeHandle:
+        """``prepacked=(wire_u8, elems)``: flat elements [0, elems) were already encoded into ``wire_u8``
+        (from :meth:`prepack_target`); the engine encodes the rest and skips its pack pass."""
         n_valid = int(n_valid if n_valid is not None else master.numel())
+        pre, pre_n = (None, 0) if prepacked is None else prepacked
         slot = self.C.submit(grad.view(-1), master.view(-1), None if lp is None else lp.view(-1),
                              None if mom is None else mom.view(-1), n_valid, lr, grad_scale, weight_decay, momentum,
-                             nesterov, True, True, None)
+                             nesterov, True, True, None, pre, int(pre_n))
         h = NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=True)
         self._account(n_valid)
         return h if defer else h.commit(update_after)
