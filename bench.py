@@ -42,10 +42,12 @@ def main():
     ap.add_argument("--algo", default="mesh", choices=["mesh", "ring"])
     ap.add_argument("--rings", type=int, default=1)
     ap.add_argument("--transport", default="torch", choices=["torch", "native"])
-    ap.add_argument("--engine", default="python", choices=["python", "native"],
+    ap.add_argument("--engine", default="native", choices=["python", "native"],
                     help="request path: Python-issued engine or the C++ engine (csrc/comm/engine.cpp)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one training step in a HIP graph and replay it (world 1, inline engine)")
     ap.add_argument("--force-dist", action="store_true",
                     help="world 1 through the full multi-rank path (1-rank RCCL group, side-stream engine)")
     a = ap.parse_args()
@@ -79,12 +81,29 @@ def main():
     for _ in range(a.warmup):
         trainer.step(x, y)
     trainer.finish()
+    step = lambda: trainer.step(x, y)  # noqa: E731
+    graphed = False
+    if a.graph and device.type == "cuda" and world == 1 and (engine is None or getattr(engine, "inline", False)):
+        # the whole step (fwd, loss, bwd GEMMs, BFP encode, fused SGD) is a fixed kernel sequence on one
+        # stream at world 1: capture it once, replay per step (removes the host launch path entirely)
+        try:
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                trainer.step(x, y)
+                trainer.finish_async()
+            torch.cuda.synchronize()
+            step = gr.replay
+            graphed = True
+        except RuntimeError as e:  # capture unsupported for this configuration: stay eager
+            print(f"[bench] HIP graph capture failed ({e}); running eagerly", file=sys.stderr)
+            torch.cuda.synchronize()
     D.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss_rows = trainer.step(x, y)
+        step()
+    loss_rows = model.loss_rows
     t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
     trainer.finish()
     if device.type == "cuda":
@@ -123,7 +142,8 @@ def main():
                 "algo": a.algo,
                 "rings": engine.rings if engine is not None else 0,
                 "transport": a.transport if world > 1 else "none",
-                "engine": a.engine,
+                "engine": a.engine if device.type == "cuda" else "python",
+                "hip_graph": graphed,
                 "fused_sgd": True,
             },
             "extra": {

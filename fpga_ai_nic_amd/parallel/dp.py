@@ -177,6 +177,11 @@ class DataParallelTrainer:
         if self.cuda:
             torch.cuda.synchronize()
 
+    def finish_async(self):
+        """GPU-side: order the current stream after every outstanding update (no host wait; usable while
+        capturing a HIP graph)."""
+        self._wait_updates()
+
     def finish(self, timeout: float | None = None):
         """Wait (host) for every outstanding all-reduce/update."""
         for i, h in enumerate(self.pending):

@@ -107,9 +107,10 @@ def _engine_case(N, prepack, force=False, n=20000, codec="bfp_rne"):
         fabric = C.LoopbackFabric(N, 60.0)
         engines = [NativeAllReduce(None, codec=codec, comm=fabric.comm(r)) for r in range(N)]
     else:
-        engines = [NativeAllReduce(ThreadFabric(1).transport(0), codec=codec, force_comm=force)]
         if force:
             engines = [NativeAllReduce(_native_transport(), codec=codec, force_comm=True)]
+        else:
+            engines = [NativeAllReduce(ThreadFabric(1).transport(0), codec=codec)]
     L = engines[0].layout(n)
     w_elems = (n // 2) // 16 * 16  # pretend the producer encoded the first half
 
