@@ -74,7 +74,8 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     TORCH_CHECK(wire && wire->is_cuda() && wire->is_contiguous() && wire->scalar_type() == at::kByte,
                 "wire epilogue needs a contiguous uint8 GPU wire buffer");
     TORCH_CHECK(wire_shard > 0 && wire_shard % 256 == 0, "wire_shard must be a positive multiple of 256");
-    const int64_t last = (int64_t)(g.M - 1) * g.ldc + g.N - 1;
+    // with colsum the encoded bias segment follows C: flat M*ldc .. M*ldc + N - 1
+    const int64_t last = g.colsum ? (int64_t)g.M * g.ldc + g.N - 1 : (int64_t)(g.M - 1) * g.ldc + g.N - 1;
     const int64_t need = (last / wire_shard + 1) * (int64_t)wire_shard_bytes((int)wire_codec, (size_t)wire_shard);
     TORCH_CHECK(wire->numel() >= need, "wire buffer too small: ", wire->numel(), " < ", need);
     g.wire = wire->data_ptr<uint8_t>();

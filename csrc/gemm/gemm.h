@@ -41,6 +41,8 @@ struct GemmArgs {
   // wire_shard elements; it is encoded (groups of 16 along n) into the wire layout of shard f / wire_shard
   // (bfp_format.h). Elements of shard wire_own (>= 0) are also written to C in f32 (the owner's
   // un-quantised local contribution for the mesh reduce). f32 output, no split-K, no accumulate.
+  // With colsum, the column sums are also encoded as the bucket segment that follows C (flat M*ldc + n: the
+  // bias gradient of the [W | b] bucket). The bucket must have fewer than 2^31 elements.
   uint8_t* wire = nullptr;
   int64_t wire_shard = 0;
   int wire_own = -1;

@@ -167,31 +167,48 @@ struct WireOut {
   int64_t shard;  // elements per shard (multiple of 256)
   int own;        // shard also written to C in f32 (-1: none)
   int codec;      // kBfpTrunc / kBfpRne
+  float inv_shard;  // 1 / shard (shard index without a 64-bit integer division)
+  int bias_off;     // > 0: flat offset of the bias segment, encoded from the fused column sum
 };
 
-// Encode 4 consecutive columns held by this lane; the 16-column group is the 4 lanes (lane & ~3) .. +3
-// (the LDS-staged epilogue hands each lane 4 columns of one row, 16-B aligned).
-__device__ __forceinline__ void wire_epi4(const float v[4], float* __restrict__ C, int64_t ldc, const WireOut& wo,
-                                          int row, int col, int lane) {
-  const int64_t f = (int64_t)row * ldc + col;
-  const int64_t sh = f / wo.shard;
-  const int64_t pos = f - sh * wo.shard;
+// flat index -> (shard, position); f < 2^31, shard >= 256: the float estimate is off by at most one
+__device__ __forceinline__ int wire_shard_of(uint32_t f, const WireOut& wo) {
+  int sh = (int)((float)f * wo.inv_shard);
+  const uint32_t sz = (uint32_t)wo.shard;
+  if ((uint32_t)sh * sz > f) --sh;
+  else if ((uint32_t)(sh + 1) * sz <= f) ++sh;
+  return sh;
+}
+
+__device__ __forceinline__ uint8_t* wire_shard_base(int sh, const WireOut& wo) {
+  return wo.p + (int64_t)sh * (wo.shard + wo.shard / 16);
+}
+
+__device__ __forceinline__ int32_t wire_encode(float x, uint32_t E, int codec) {
+  return codec == kBfpTrunc ? bfp_encode_trunc(__float_as_uint(x), E) : bfp_encode_rne(x, E);
+}
+
+// Encode one whole 16-column group held by this lane: 16-B mantissa store + 1 exponent byte.
+__device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
+                                           int row, int col) {
+  const uint32_t f = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
+  const int sh = wire_shard_of(f, wo);
+  const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
   uint32_t mx = 0;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) mx = max(mx, __float_as_uint(v[u]) & 0x7FFFFFFFu);
-  mx = max(mx, (uint32_t)__shfl_xor((int)mx, 1));
-  mx = max(mx, (uint32_t)__shfl_xor((int)mx, 2));
+  for (int u = 0; u < 16; ++u) mx = max(mx, __float_as_uint(v[u]) & 0x7FFFFFFFu);
   const uint32_t E = mx >> 23;
-  uint32_t w = 0;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int32_t q = wo.codec == kBfpTrunc ? bfp_encode_trunc(__float_as_uint(v[u]), E) : bfp_encode_rne(v[u], E);
-    w |= ((uint32_t)q & 0xFFu) << (8 * u);
+  for (int u = 0; u < 16; ++u) w[u >> 2] |= ((uint32_t)wire_encode(v[u], E, wo.codec) & 0xFFu) << (8 * (u & 3));
+  uint8_t* base = wire_shard_base(sh, wo);
+  *reinterpret_cast<uint4*>(base + pos) = make_uint4(w[0], w[1], w[2], w[3]);
+  base[wo.shard + pos / 16] = (uint8_t)E;
+  if (sh == wo.own) {
+#pragma unroll
+    for (int u = 0; u < 16; u += 4)
+      *reinterpret_cast<float4*>(C + f + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
   }
-  uint8_t* base = wo.p + sh * (wo.shard + wo.shard / 16);
-  *reinterpret_cast<uint32_t*>(base + pos) = w;
-  if ((lane & 3) == 0) base[wo.shard + pos / 16] = (uint8_t)E;
-  if (sh == wo.own) *reinterpret_cast<float4*>(C + f) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // 8 waves (2 per SIMD) or 4 waves (1 per SIMD, up to 512 VGPR+AGPR per lane: large per-wave tiles).
@@ -337,7 +354,22 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
       float v = cs[j];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
-      if (lane < 16) colsum[n0 + wn * WTN + j * 16 + lane] = v;
+      const int col = n0 + wn * WTN + j * 16 + (lane & 15);
+      if (lane < 16) colsum[col] = v;
+      if constexpr (EPI == kEpiWire) {
+        if (wo.bias_off > 0) {  // the bias segment's 16-column group is lanes 0..15: encode it here too
+          uint32_t mx = __float_as_uint(v) & 0x7FFFFFFFu;
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+          const uint32_t E = mx >> 23;
+          const uint32_t f = (uint32_t)wo.bias_off + (uint32_t)col;
+          const int sh = wire_shard_of(f, wo);
+          const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
+          uint8_t* base = wire_shard_base(sh, wo);
+          if (lane < 16) base[pos] = (uint8_t)(wire_encode(v, E, wo.codec) & 0xFF);
+          if (lane == 0) base[wo.shard + pos / 16] = (uint8_t)E;
+        }
+      }
     }
   }
 
@@ -355,6 +387,28 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
 #pragma unroll
       for (int r = 0; r < 4; ++r) stg[(row_l + r) * EW + j * 16 + col_l] = acc[i][j][r];
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own LDS writes landed (wave-private region)
+    if constexpr (EPI == kEpiWire && !SPLIT) {
+      // one lane per 16-column group: no cross-lane exponent exchange, 16-B mantissa stores
+      constexpr int G16 = WTN / 16;                    // groups per staged row
+      constexpr int RPG = 64 / G16;                    // rows per pass (lanes beyond 16 rows idle)
+      constexpr int PASSES = RPG >= 16 ? 1 : 16 / RPG;
+#pragma unroll
+      for (int pass = 0; pass < PASSES; ++pass) {
+        const int rr = pass * RPG + lane / G16;
+        if (RPG <= 16 || rr < 16) {
+          const int cc = (lane % G16) * 16;
+          float v[16];
+#pragma unroll
+          for (int u = 0; u < 16; u += 4) {
+            const float4 q = *reinterpret_cast<const float4*>(stg + rr * EW + cc + u);
+            v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
+          }
+          wire_epi16(v, reinterpret_cast<float*>(C), ldc, wo, m0 + wm * WTM + i * 16 + rr, n0 + wn * WTN + cc);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      continue;
+    }
 #pragma unroll
     for (int pass = 0; pass < 16 / RPI; ++pass) {
       const int rr = pass * RPI + lane / C4;
@@ -366,8 +420,6 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
       if (SPLIT) {
         float* slab = ws + (int64_t)ksplit * M * N;
         *reinterpret_cast<float4*>(slab + (int64_t)row * N + col) = q;
-      } else if constexpr (EPI == kEpiWire) {
-        wire_epi4(v, reinterpret_cast<float*>(C), ldc, wo, row, col, lane);
       } else {
         epi4<EPI, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
       }
@@ -411,7 +463,7 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
                        (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
-                       (float*)nullptr, WireOut{nullptr, 0, -1, 0});
+                       (float*)nullptr, WireOut{nullptr, 0, -1, 0, 0.f, 0});
     hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
                        (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
                        a.ldaux, a.M, a.N);
@@ -420,7 +472,10 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
                        (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1, (float*)nullptr,
-                       a.colsum, WireOut{a.wire, a.wire_shard, a.wire_own, a.wire_codec});
+                       a.colsum,
+                       WireOut{a.wire, a.wire_shard, a.wire_own, a.wire_codec,
+                               a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
+                               a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0});
   }
 }
 

@@ -148,11 +148,14 @@ class DataParallelTrainer:
         for i in reversed(range(m.L)):
             l = m.layers[i]
             with tracing.range(f"bwd{i}"):
-                tgt = self.engine.prepack_target(l.grad, l.n) if self.prepack else None
+                # the bwd-weight GEMM encodes dW (and the fused bias gradient) straight into the wire buffer;
+                # the zero tail (padding, or the bias segment of a bias-free model) is encoded once
+                tgt = (self.engine.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout)
+                       if self.prepack else None)
                 m.backward_weight(i, wire=tgt)
                 h = None
                 if self.engine is not None:
-                    kw = {"prepacked": (tgt[0], l.cin * l.cout)} if tgt is not None else {}
+                    kw = {"prepacked": (tgt[0], l.n_pad)} if tgt is not None else {}
                     h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
                                                   grad_scale=self.grad_scale, weight_decay=self.wd,
                                                   momentum=self.momentum, nesterov=self.nesterov, defer=True,

@@ -142,18 +142,28 @@ class NativeAllReduce:
     def wire_bytes(self, L: BucketLayout) -> int:
         return int(self.C.wire_bytes(L.n))
 
-    def prepack_target(self, grad: torch.Tensor, n: int):
+    def prepack_target(self, grad: torch.Tensor, n: int, static_from: int | None = None):
         """Wire target for a producer that encodes the gradient itself (GEMM ``kEpiWire`` epilogue):
         ``(wire_u8, shard_elems, own_shard, codec_id)`` — one persistent buffer per gradient bucket — or None
-        when this configuration (ring / raw codec) cannot take prepacked input."""
+        when this configuration (ring / raw codec) cannot take prepacked input.
+
+        ``static_from``: flat elements [static_from, padded end) are always zero (padding, or a bias segment
+        the model does not have); they are encoded once here, so the producer's encoding plus this tail is
+        the whole bucket (pass ``prepacked=(buf, layout(n).n_pad)``)."""
         shard, shards, own = self.C.prepack_shape(int(n))
-        if shard == 0:
+        if shard == 0 or n % 16:
             return None
         need = shards * wire.shard_bytes(self.codec_id, shard)
-        key = grad.data_ptr()
+        static_from = n if static_from is None else int(static_from)
+        key = (grad.data_ptr(), static_from)
         buf = self._prepack_bufs.get(key)
         if buf is None or buf.numel() < need:
-            buf = self._prepack_bufs[key] = torch.empty(need, dtype=torch.uint8, device=self.device)
+            buf = torch.empty(need, dtype=torch.uint8, device=self.device)
+            total = shard * shards
+            if static_from < total:
+                _ext.require().wire_pack_range(torch.zeros(total, device=self.device), buf, shard, static_from,
+                                               total, self.codec_id)
+            self._prepack_bufs[key] = buf
         return buf, shard, own, self.codec_id
 
     def allreduce_sgd(self, grad: torch.Tensor, master: torch.Tensor, lp: torch.Tensor | None = None,

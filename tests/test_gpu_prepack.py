@@ -187,3 +187,34 @@ def test_trainer_fused_encode_matches_unfused():
         res.append((losses, [l.master.cpu() for l in m.layers]))
     assert res[0][0] == res[1][0]
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+@pytest.mark.parametrize("codec", ["bfp_rne", "bfp_trunc"])
+@pytest.mark.parametrize("nsh", [1, 3])
+def test_gemm_wire_epilogue_encodes_fused_bias(codec, nsh):
+    cin, cout, mb = 1024, 1024, 256
+    torch.manual_seed(nsh)
+    x = (torch.randn(mb, cin, device="cuda") * 0.5).to(torch.bfloat16)
+    dz = (torch.randn(mb, cout, device="cuda") * 0.1).to(torch.bfloat16)
+    n = cin * cout + cout
+    shard = ((n + nsh - 1) // nsh + 255) // 256 * 256
+    grad = torch.zeros(shard * nsh, device="cuda")
+    buf = torch.zeros(nsh * wire.shard_bytes(codec, shard), dtype=torch.uint8, device="cuda")
+    G.linear_bwd_weight(x, dz, grad[: cin * cout].view(cin, cout), bias_grad=grad[cin * cout:n],
+                        wire=(buf, shard, nsh - 1, wire.codec_id(codec)))
+    torch.cuda.synchronize()
+    flat = np.zeros(shard * nsh, np.float32)
+    ref = torch.empty(cin, cout, device="cuda")
+    G.gemm(x, True, dz, False, ref, G.EPI_NONE, split_k=1)
+    flat[: cin * cout] = ref.cpu().numpy().reshape(-1)
+    flat[cin * cout:n] = grad[cin * cout:n].cpu().numpy()  # the fused column sums (f32, always written)
+    exp = O.pack(flat, shard, codec)
+    got = buf.cpu().numpy()
+    sb = wire.shard_bytes(codec, shard)
+    for s in range(nsh):
+        lo, hi = s * shard, min((s + 1) * shard, n)
+        if hi <= lo:
+            continue
+        assert np.array_equal(got[s * sb:s * sb + hi - lo], exp[s * sb:s * sb + hi - lo]), f"shard {s} mantissas"
+        e0 = s * sb + shard
+        assert np.array_equal(got[e0:e0 + (hi - lo) // 16], exp[e0:e0 + (hi - lo) // 16]), f"shard {s} exponents"
