@@ -17,19 +17,23 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fpga_ai_nic_amd.ops import gemm as G  # noqa: E402
 
-# (name, M, N, K, a_t, b_t, epilogue) for MLP 1024-4096-4096-1024 at MB=2048
-MLP_SHAPES = [
-    ("fwd0", 2048, 4096, 1024, False, False, G.EPI_BIAS_RELU),
-    ("fwd1", 2048, 4096, 4096, False, False, G.EPI_BIAS_RELU),
-    ("fwd2", 2048, 1024, 4096, False, False, G.EPI_BIAS),
-    ("bwdw2", 4096, 1024, 2048, True, False, G.EPI_NONE),
-    ("bwdw1", 4096, 4096, 2048, True, False, G.EPI_NONE),
-    ("bwdw0", 1024, 4096, 2048, True, False, G.EPI_NONE),
-    ("bwdd2", 2048, 4096, 1024, False, True, G.EPI_RELU_MASK),
-    ("bwdd1", 2048, 4096, 4096, False, True, G.EPI_RELU_MASK),
-    ("sq4k", 4096, 4096, 4096, False, True, G.EPI_NONE),
-    ("sq8k", 8192, 8192, 8192, False, True, G.EPI_NONE),
-]
+def mlp_shapes(mb: int):
+    """(name, M, N, K, a_t, b_t, epilogue) of one MLP 1024-4096-4096-1024 step at minibatch ``mb``."""
+    return [
+        ("fwd0", mb, 4096, 1024, False, False, G.EPI_BIAS_RELU),
+        ("fwd1", mb, 4096, 4096, False, False, G.EPI_BIAS_RELU),
+        ("fwd2", mb, 1024, 4096, False, False, G.EPI_BIAS),
+        ("bwdw2", 4096, 1024, mb, True, False, G.EPI_NONE),
+        ("bwdw1", 4096, 4096, mb, True, False, G.EPI_NONE),
+        ("bwdw0", 1024, 4096, mb, True, False, G.EPI_NONE),
+        ("bwdd2", mb, 4096, 1024, False, True, G.EPI_RELU_MASK),
+        ("bwdd1", mb, 4096, 4096, False, True, G.EPI_RELU_MASK),
+        ("sq4k", 4096, 4096, 4096, False, True, G.EPI_NONE),
+        ("sq8k", 8192, 8192, 8192, False, True, G.EPI_NONE),
+    ]
+
+
+MLP_SHAPES = mlp_shapes(2048)
 
 
 def time_fn(fn, iters):
@@ -49,10 +53,11 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--shapes", default="")
     ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
+    ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
-    for name, M, N, K, a_t, b_t, epi in MLP_SHAPES:
+    for name, M, N, K, a_t, b_t, epi in mlp_shapes(a.mb):
         if a.shapes and name not in a.shapes.split(","):
             continue
         if a.dtype == "f32" and K > 4096:
