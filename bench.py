@@ -25,7 +25,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from fpga_ai_nic_amd.models.mlp import MLP  # noqa: E402
 from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine  # noqa: E402
-from fpga_ai_nic_amd.parallel.transport import NativeTransport, ThreadFabric, TorchDistTransport  # noqa: E402
+from fpga_ai_nic_amd.parallel.transport import (NativeTransport, ThreadFabric, TorchDistTransport,  # noqa: E402
+                                                make_p2p_comm)
 from fpga_ai_nic_amd.utils import dist as D  # noqa: E402
 
 SIZES = [1024, 4096, 4096, 1024]
@@ -44,7 +45,9 @@ def main():
     ap.add_argument("--rounding", default="rne", choices=["rne", "trunc"])
     ap.add_argument("--algo", default="mesh", choices=["mesh", "ring"])
     ap.add_argument("--rings", type=int, default=1)
-    ap.add_argument("--transport", default="torch", choices=["torch", "native"])
+    ap.add_argument("--transport", default="torch", choices=["torch", "native", "p2p"],
+                    help="torch/native: RCCL collectives; p2p: direct HIP-IPC peer writes + stream flags "
+                         "(C++ engine only)")
     ap.add_argument("--engine", default="native", choices=["python", "native"],
                     help="request path: Python-issued engine or the C++ engine (csrc/comm/engine.cpp)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
@@ -61,14 +64,17 @@ def main():
     if device.type != "cuda":
         print("[bench] no GPU visible: running the CPU path (functional only)", file=sys.stderr)
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    comm = None
     if world > 1 or a.force_dist:
         transport = NativeTransport(force_collectives=a.force_dist) if a.transport == "native" else \
             TorchDistTransport(force_collectives=a.force_dist)
+        if a.transport == "p2p" and device.type == "cuda" and a.engine == "native":
+            comm = make_p2p_comm()
     else:
         transport = ThreadFabric(1).transport(0)
     kind = "local" if a.compress == "local" else a.compress
     engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings,
-                         force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python")
+                         force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python", comm=comm)
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
     if world > 1:

@@ -3,6 +3,7 @@
 #include "comm/engine.h"
 #include "comm/loopback_comm.h"
 #include "comm/native_comm.h"
+#include "comm/p2p_comm.h"
 
 namespace fan {
 
@@ -31,6 +32,36 @@ void register_engine(pybind11::module_& m) {
   pybind11::class_<LoopbackComm, Comm>(m, "LoopbackComm")
       .def("drop_after", &LoopbackComm::drop_after)
       .def_property_readonly("collectives", &LoopbackComm::collectives);
+  pybind11::class_<P2PComm, Comm>(m, "P2PComm")
+      .def(pybind11::init<int, int, int, size_t>(), pybind11::arg("rank"), pybind11::arg("world"),
+           pybind11::arg("device"), pybind11::arg("slot_bytes") = (size_t)128 << 20)
+      .def("handles", [](P2PComm& c) { return pybind11::bytes(c.handles()); })
+      .def("connect",
+           [](P2PComm& c, const std::vector<pybind11::bytes>& all) {
+             std::vector<std::string> v;
+             for (auto& b : all) v.push_back(std::string(b));
+             c.connect(v);
+           })
+      .def_static("connect_local", &P2PComm::connect_local)
+      .def_property_readonly("slot_bytes", &P2PComm::slot_bytes)
+      .def_property_readonly("sequence", &P2PComm::sequence)
+      .def("all_to_all",
+           [](P2PComm& c, const at::Tensor& send, at::Tensor& recv) {
+             TORCH_CHECK(bytes_of(send) == bytes_of(recv) && bytes_of(send) % c.world() == 0, "all_to_all sizes");
+             c.all_to_all(ptr_of(send), ptr_of(recv), bytes_of(send) / c.world(), fan_stream());
+           })
+      .def("all_gather",
+           [](P2PComm& c, const at::Tensor& send, at::Tensor& recv) {
+             TORCH_CHECK(bytes_of(recv) == bytes_of(send) * c.world(), "all_gather sizes");
+             c.all_gather(ptr_of(send), ptr_of(recv), bytes_of(send), fan_stream());
+           })
+      .def("sendrecv", [](P2PComm& c, const std::vector<std::pair<at::Tensor, int>>& sends,
+                          const std::vector<std::pair<at::Tensor, int>>& recvs) {
+        std::vector<P2POp> s, r;
+        for (auto& p : sends) s.push_back({ptr_of(p.first), bytes_of(p.first), p.second});
+        for (auto& p : recvs) r.push_back({ptr_of(p.first), bytes_of(p.first), p.second});
+        c.sendrecv(s, r, fan_stream());
+      });
   pybind11::class_<NativeComm, Comm>(m, "NativeComm")
       .def(pybind11::init([](pybind11::bytes uid, int rank, int world, int device) {
              return new NativeComm(std::string(uid), rank, world, device);

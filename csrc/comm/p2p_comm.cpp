@@ -1,0 +1,159 @@
+// Direct peer-to-peer transport. See p2p_comm.h.
+#include "comm/p2p_comm.h"
+
+#include <cstring>
+
+namespace fan {
+
+namespace {
+
+struct Handles {
+  hipIpcMemHandle_t arena;
+  hipIpcMemHandle_t flags;
+};
+
+}  // namespace
+
+P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
+    : rank_(rank), world_(world), device_(device), slot_((slot_bytes + 255) / 256 * 256) {
+  FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+  FAN_CHECK(slot_ > 0, "slot_bytes must be > 0");
+  FAN_HIP_CHECK(hipSetDevice(device));
+  FAN_HIP_CHECK(hipMalloc(&arena_, (size_t)world * 2 * slot_));
+  // flags are polled by the command processor (hipStreamWaitValue64) and written by peers' command
+  // processors (hipStreamWriteValue64); plain device memory supports both and HIP IPC export (probed on
+  // MI355X: tools/probes/stream_wait_probe.cpp)
+  void* f = nullptr;
+  FAN_HIP_CHECK(hipMalloc(&f, (size_t)2 * world * sizeof(uint64_t)));
+  flags_ = reinterpret_cast<uint64_t*>(f);
+  FAN_HIP_CHECK(hipMemset(flags_, 0, (size_t)2 * world * sizeof(uint64_t)));
+  FAN_HIP_CHECK(hipDeviceSynchronize());
+  peer_arena_.assign(world, nullptr);
+  peer_flags_.assign(world, nullptr);
+  opened_.assign(world, false);
+  peer_arena_[rank] = arena_;
+  peer_flags_[rank] = flags_;
+  last_sent_[0].assign(world, 0);
+  last_sent_[1].assign(world, 0);
+}
+
+P2PComm::~P2PComm() {
+  hipSetDevice(device_);
+  hipDeviceSynchronize();
+  for (int p = 0; p < world_; ++p) {
+    if (!opened_[p]) continue;
+    hipIpcCloseMemHandle(peer_arena_[p]);
+    hipIpcCloseMemHandle(peer_flags_[p]);
+  }
+  hipFree(flags_);
+  hipFree(arena_);
+}
+
+std::string P2PComm::handles() const {
+  Handles h;
+  FAN_HIP_CHECK(hipIpcGetMemHandle(&h.arena, arena_));
+  FAN_HIP_CHECK(hipIpcGetMemHandle(&h.flags, flags_));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void P2PComm::connect(const std::vector<std::string>& all) {
+  FAN_CHECK((int)all.size() == world_, "connect: need one handle blob per rank");
+  FAN_HIP_CHECK(hipSetDevice(device_));
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    FAN_CHECK(all[p].size() == sizeof(Handles), "connect: bad handle blob");
+    Handles h;
+    std::memcpy(&h, all[p].data(), sizeof(h));
+    void* a = nullptr;
+    void* f = nullptr;
+    FAN_HIP_CHECK(hipIpcOpenMemHandle(&a, h.arena, hipIpcMemLazyEnablePeerAccess));
+    FAN_HIP_CHECK(hipIpcOpenMemHandle(&f, h.flags, hipIpcMemLazyEnablePeerAccess));
+    peer_arena_[p] = reinterpret_cast<uint8_t*>(a);
+    peer_flags_[p] = reinterpret_cast<uint64_t*>(f);
+    opened_[p] = true;
+  }
+}
+
+void P2PComm::connect_local(const std::vector<P2PComm*>& ranks) {
+  for (P2PComm* c : ranks) {
+    FAN_CHECK((int)ranks.size() == c->world_, "connect_local: need every rank");
+    for (P2PComm* d : ranks) {
+      c->peer_arena_[d->rank_] = d->arena_;
+      c->peer_flags_[d->rank_] = d->flags_;
+    }
+  }
+}
+
+void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>& recvs, hipStream_t s) {
+  FAN_CHECK(!aborted_, "p2p transport aborted");
+  const uint64_t q = ++seq_;
+  const int par = (int)(q & 1);
+  // sends: per destination, in issue order, packed back to back into this rank's slot of the peer's arena
+  for (int p = 0; p < world_; ++p) {
+    size_t off = 0;
+    bool any = false;
+    for (const P2POp& op : sends) {
+      if (op.peer != p || op.bytes == 0) continue;
+      FAN_CHECK(p != rank_, "p2p: self-send");
+      FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
+      if (!any) {
+        // WAR: the receiver must have drained the message we last put into this parity slot
+        const uint64_t prev = last_sent_[par][p];
+        if (prev) FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + world_ + p, prev, hipStreamWaitValueGte));
+        any = true;
+      }
+      FAN_CHECK(off + op.bytes <= slot_, "p2p: message larger than the arena slot (raise slot_bytes)");
+      FAN_HIP_CHECK(hipMemcpyAsync(slot_ptr(peer_arena_[p], rank_, q) + off, op.ptr, op.bytes,
+                                   hipMemcpyDeviceToDevice, s));
+      off += op.bytes;
+    }
+    if (any) {
+      FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, q, 0));  // "ready from rank_" at p
+      last_sent_[par][p] = q;
+    }
+  }
+  // receives: wait for each source's ready flag, copy out, acknowledge (frees the slot for the sender)
+  for (int src = 0; src < world_; ++src) {
+    size_t off = 0;
+    bool any = false;
+    for (const P2POp& op : recvs) {
+      if (op.peer != src || op.bytes == 0) continue;
+      FAN_CHECK(src != rank_, "p2p: self-receive");
+      if (!any) {
+        FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + src, q, hipStreamWaitValueGte));
+        any = true;
+      }
+      FAN_CHECK(off + op.bytes <= slot_, "p2p: message larger than the arena slot (raise slot_bytes)");
+      FAN_HIP_CHECK(hipMemcpyAsync(op.ptr, slot_ptr(arena_, src, q) + off, op.bytes, hipMemcpyDeviceToDevice, s));
+      off += op.bytes;
+    }
+    if (any) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[src] + world_ + rank_, q, 0));
+  }
+}
+
+void P2PComm::all_to_all(const void* send, void* recv, size_t bpp, hipStream_t s) {
+  std::vector<P2POp> sends, recvs;
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    sends.push_back({const_cast<uint8_t*>(static_cast<const uint8_t*>(send)) + p * bpp, bpp, p});
+    recvs.push_back({static_cast<uint8_t*>(recv) + p * bpp, bpp, p});
+  }
+  if (bpp)
+    FAN_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(recv) + rank_ * bpp,
+                                 static_cast<const uint8_t*>(send) + rank_ * bpp, bpp, hipMemcpyDeviceToDevice, s));
+  sendrecv(sends, recvs, s);
+}
+
+void P2PComm::all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) {
+  std::vector<P2POp> sends, recvs;
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    sends.push_back({const_cast<void*>(send), bytes, p});
+    recvs.push_back({static_cast<uint8_t*>(recv) + p * bytes, bytes, p});
+  }
+  if (bytes)
+    FAN_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t*>(recv) + rank_ * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
+  sendrecv(sends, recvs, s);
+}
+
+}  // namespace fan

@@ -1,0 +1,58 @@
+// Direct peer-to-peer transport over xGMI (SURVEY.md §5.8 transport (b), §7.1 transport_p2p).
+//
+// No RCCL in the data path: every rank exposes a receive ARENA and a FLAG block in its HBM through HIP IPC;
+// peers write message payloads straight into the arena over xGMI (stream-ordered device copies into the
+// IPC-mapped peer pointer) and then publish a 64-bit sequence number into the receiver's flag block with
+// hipStreamWriteValue64. The receiver's stream waits on that flag with hipStreamWaitValue64 — a
+// command-processor wait, so no CU spins and nothing can deadlock on occupancy — copies the payload out
+// and acknowledges into the sender's flag block, which frees that arena slot for reuse.
+//
+// Arena: world x 2 slots of slot_bytes (double-buffered by sequence parity per sender), so a sender only
+// stalls when it is two messages ahead of a receiver. Flags: ready[world] + ack[world] (uint64 each).
+// Reference analogue: the NIC's Ethernet link + credit flow control (hw/all_reduce.sv:468-483) and the
+// done-flag writes (hw/all_reduce.sv:1368-1375); here sequence numbers play the role of both.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "comm/native_comm.h"
+
+namespace fan {
+
+class P2PComm : public Comm {
+ public:
+  P2PComm(int rank, int world, int device, size_t slot_bytes);
+  ~P2PComm() override;
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  size_t slot_bytes() const { return slot_; }
+
+  // IPC bootstrap: this rank's (arena, flags) handles as bytes; connect() with every rank's bytes (in rank
+  // order) opens the peers' mappings. connect_local() wires ranks living in one process (no IPC).
+  std::string handles() const;
+  void connect(const std::vector<std::string>& all_handles);
+  static void connect_local(const std::vector<P2PComm*>& ranks);
+
+  void sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>& recvs, hipStream_t s) override;
+  void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s) override;
+  void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override;
+  std::string async_error() override { return aborted_ ? "p2p transport aborted" : ""; }
+  void abort() override { aborted_ = true; }
+  uint64_t sequence() const { return seq_; }
+
+ private:
+  uint8_t* slot_ptr(uint8_t* arena, int src, uint64_t seq) const { return arena + ((size_t)src * 2 + (seq & 1)) * slot_; }
+  int rank_, world_, device_;
+  size_t slot_;
+  uint8_t* arena_ = nullptr;   // local receive arena
+  uint64_t* flags_ = nullptr;  // local flags: [0, world) ready-from-src, [world, 2 world) ack-from-dst
+  std::vector<uint8_t*> peer_arena_;
+  std::vector<uint64_t*> peer_flags_;
+  std::vector<bool> opened_;   // peer mapping opened through IPC (to be closed)
+  std::vector<uint64_t> last_sent_[2];  // per parity: sequence of the last message sent to each peer
+  uint64_t seq_ = 0;
+  bool aborted_ = false;
+};
+
+}  // namespace fan

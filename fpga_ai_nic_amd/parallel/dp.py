@@ -51,10 +51,11 @@ class RcclAllReduce(CompressedAllReduce):
 
 def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str = "rne", algo: str = "mesh",
                 rings: int = 1, max_slice_elems: int = 1 << 22, compat_owner_fp32: bool = False,
-                timeout_s: float = 600.0, force_comm: bool = False, impl: str = "python"):
+                timeout_s: float = 600.0, force_comm: bool = False, impl: str = "python", comm=None):
     """kind: 'bfp' (compressed engine), 'raw' (engine, uncompressed fp32 wire), 'rccl' (baseline),
     'local' (no communication: world 1). impl: 'python' (request path issued from Python over any
-    transport) or 'native' (C++ engine over its own RCCL communicator; GPU only)."""
+    transport) or 'native' (C++ engine over its own RCCL communicator, or over ``comm``, e.g. the direct P2P
+    communicator of :func:`~fpga_ai_nic_amd.parallel.transport.make_p2p_comm`; GPU only)."""
     if kind == "local" or transport is None:
         return None
     if kind == "rccl":
@@ -64,7 +65,8 @@ def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str
         from .native_engine import NativeAllReduce
 
         return NativeAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
-                               compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm)
+                               compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm,
+                               comm=comm)
     return CompressedAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
                                compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm)
 

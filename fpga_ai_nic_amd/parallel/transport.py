@@ -182,6 +182,24 @@ class NativeTransport(Transport):
         self.comm.abort()
 
 
+def make_p2p_comm(rank: int | None = None, world: int | None = None, device: int | None = None,
+                  slot_bytes: int = 128 << 20):
+    """Direct peer-to-peer communicator (csrc/comm/p2p_comm.cpp): HIP-IPC receive arenas written over xGMI +
+    stream-ordered sequence flags, no RCCL in the data path. IPC handles are exchanged through the default
+    torch.distributed process group (any backend). Returns a ``_C.P2PComm`` usable as ``comm=`` of
+    :class:`~fpga_ai_nic_amd.parallel.native_engine.NativeAllReduce`."""
+    C = _ext.require()
+    if rank is None:
+        rank, world = dist.get_rank(), dist.get_world_size()
+    device = torch.cuda.current_device() if device is None else device
+    comm = C.P2PComm(rank, world, device, slot_bytes)
+    blobs = [None] * world
+    dist.all_gather_object(blobs, comm.handles())
+    comm.connect(blobs)
+    dist.barrier()
+    return comm
+
+
 class ThreadFabric:
     """Shared state of N virtual ranks running as threads in one process."""
 
