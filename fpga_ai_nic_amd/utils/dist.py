@@ -33,7 +33,9 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0, force
     if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        be = backend or ("nccl" if use_cuda else "gloo")
+        # FAN_CTRL_BACKEND=gloo: control plane (bootstrap, broadcast, barrier) over gloo even on GPU — for
+        # several ranks sharing one GPU with the P2P transport, where RCCL refuses duplicate devices
+        be = backend or os.environ.get("FAN_CTRL_BACKEND") or ("nccl" if use_cuda else "gloo")
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = device

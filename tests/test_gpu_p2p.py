@@ -104,3 +104,60 @@ def test_p2p_two_processes_one_gpu():
         assert "error" not in ok, ok
         assert all(ok.values()), (rank, ok)
     assert res[0][1] == res[1][1], "ranks issued different numbers of collectives"
+
+
+def _trainer_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fpga_ai_nic_amd.models.mlp import MLP
+        from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine
+        from fpga_ai_nic_amd.parallel.transport import TorchDistTransport, make_p2p_comm
+
+        torch.cuda.set_device(0)
+        t = TorchDistTransport()
+        eng = make_engine(t, "bfp", impl="native", comm=make_p2p_comm(rank, world, 0))
+        m = MLP([256, 512, 256, 128], dtype=torch.bfloat16, device="cuda", seed=5 + rank, momentum=True,
+                pad_fn=lambda n: eng.layout(n).n_pad)
+        for l in m.layers:  # replicas start from rank 0's weights (reference C3/C4)
+            t.broadcast_(l.master, 0)
+        m.sync_lp()
+        tr = DataParallelTrainer(m, eng, lr=0.05, momentum=0.9)
+        assert tr.prepack, "fused GEMM encode expected on the native mesh engine"
+        g = torch.Generator().manual_seed(100 + rank)
+        x = (torch.rand(256, 256, generator=g) * 2 - 1).to("cuda", torch.bfloat16)
+        y = torch.randint(0, 128, (256,), generator=g, dtype=torch.int32).cuda()
+        losses = [tr.step(x, y).float().mean().item() for _ in range(6)]
+        tr.finish()
+        w = torch.cat([l.master.cpu() for l in m.layers]).numpy()
+        q.put((rank, {"losses": losses, "w": w}, 0))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, {"error": repr(e)}, -1))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_p2p_data_parallel_trainer_two_ranks():
+    """DataParallelTrainer + C++ engine (fused GEMM encode, mesh) over the P2P transport with 2 ranks: replicas
+    stay bit-identical and the loss goes down."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_trainer_worker, args=(WORLD, _free_port(), q), nprocs=WORLD, join=False,
+                            start_method="spawn")
+    res = {}
+    try:
+        for _ in range(WORLD):
+            rank, out, _ = q.get(timeout=240)
+            res[rank] = out
+    except _queue.Empty:
+        for p in pc.processes:
+            p.kill()
+        pytest.fail("p2p trainer workers did not report within 240 s")
+    while not pc.join(60):
+        pass
+    for r in range(WORLD):
+        assert "error" not in res[r], res[r]
+    assert np.array_equal(res[0]["w"], res[1]["w"]), "replicas diverged"
+    for r in range(WORLD):
+        assert np.all(np.isfinite(res[r]["losses"])) and res[r]["losses"][-1] < res[r]["losses"][0]
