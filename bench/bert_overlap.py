@@ -36,13 +36,21 @@ def main():
     ap.add_argument("--rings", type=int, default=1)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--engine", default="native", choices=["python", "native"])
     a = ap.parse_args()
     rank, world, _, dev = D.init_distributed()
     transport = TorchDistTransport() if world > 1 else ThreadFabric(1).transport(0)
-    eng = make_engine(transport, a.compress, algo=a.algo, rings=a.rings)
-    if world == 1:  # force the side-stream path so the overlap is real even on one GPU
-        eng.inline = False
-        eng.stream = torch.cuda.Stream(priority=-1)
+    if a.engine == "native" and a.compress != "rccl":
+        from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce
+
+        codec = {"bfp": "bfp_rne", "raw": "raw_f32"}[a.compress]
+        # world 1: keep the side stream (no inline) so the overlap is real even on one GPU
+        eng = NativeAllReduce(transport, codec=codec, algo=a.algo, rings=a.rings, side_stream=(world == 1))
+    else:
+        eng = make_engine(transport, a.compress, algo=a.algo, rings=a.rings)
+        if world == 1:  # force the side-stream path so the overlap is real even on one GPU
+            eng.inline = False
+            eng.stream = torch.cuda.Stream(priority=-1)
     buckets = bert.gradient_buckets(a.layers)
     bufs = []
     for b in buckets:
@@ -93,6 +101,7 @@ def main():
     if rank == 0:
         print(json.dumps({
             "bench": "bert_base_bwd_overlap", "n_gpus": world, "tokens_per_gpu": T, "compress": a.compress,
+            "engine": a.engine,
             "algo": a.algo, "params": bert.num_params(a.layers), "t_compute_ms": round(tc, 3),
             "t_comm_ms": round(tm, 3), "t_overlap_ms": round(to, 3), "overlap_efficiency": round(eff, 3),
             "bwd_gemm_tflops": round(flops / (tc / 1e3) / 1e12, 1),

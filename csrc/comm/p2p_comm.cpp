@@ -88,7 +88,11 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
   FAN_CHECK(!aborted_, "p2p transport aborted");
   const uint64_t q = ++seq_;
   const int par = (int)(q & 1);
-  // sends: per destination, in issue order, packed back to back into this rank's slot of the peer's arena
+  // sends: per destination, in issue order, packed back to back into this rank's slot of the peer's arena.
+  // WAR first (the receiver drained what we last put into this parity slot), then ONE copy launch for all
+  // destinations (every link busy at once), then one ready flag per destination.
+  std::vector<P2PCopy> out;
+  std::vector<int> dests;
   for (int p = 0; p < world_; ++p) {
     size_t off = 0;
     bool any = false;
@@ -97,22 +101,24 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       FAN_CHECK(p != rank_, "p2p: self-send");
       FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
       if (!any) {
-        // WAR: the receiver must have drained the message we last put into this parity slot
         const uint64_t prev = last_sent_[par][p];
         if (prev) FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + world_ + p, prev, hipStreamWaitValueGte));
         any = true;
+        dests.push_back(p);
       }
       FAN_CHECK(off + op.bytes <= slot_, "p2p: message larger than the arena slot (raise slot_bytes)");
-      FAN_HIP_CHECK(hipMemcpyAsync(slot_ptr(peer_arena_[p], rank_, q) + off, op.ptr, op.bytes,
-                                   hipMemcpyDeviceToDevice, s));
-      off += op.bytes;
-    }
-    if (any) {
-      FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, q, 0));  // "ready from rank_" at p
-      last_sent_[par][p] = q;
+      out.push_back({op.ptr, slot_ptr(peer_arena_[p], rank_, q) + off, op.bytes});
+      off += (op.bytes + 15) / 16 * 16;
     }
   }
-  // receives: wait for each source's ready flag, copy out, acknowledge (frees the slot for the sender)
+  copy(out, s);
+  for (int p : dests) {
+    FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, q, 0));  // "ready from rank_" at p
+    last_sent_[par][p] = q;
+  }
+  // receives: wait for every source's ready flag, one copy-out launch, then acknowledge (frees the slots)
+  std::vector<P2PCopy> in;
+  std::vector<int> srcs;
   for (int src = 0; src < world_; ++src) {
     size_t off = 0;
     bool any = false;
@@ -122,13 +128,27 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       if (!any) {
         FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + src, q, hipStreamWaitValueGte));
         any = true;
+        srcs.push_back(src);
       }
       FAN_CHECK(off + op.bytes <= slot_, "p2p: message larger than the arena slot (raise slot_bytes)");
-      FAN_HIP_CHECK(hipMemcpyAsync(op.ptr, slot_ptr(arena_, src, q) + off, op.bytes, hipMemcpyDeviceToDevice, s));
-      off += op.bytes;
+      in.push_back({slot_ptr(arena_, src, q) + off, op.ptr, op.bytes});
+      off += (op.bytes + 15) / 16 * 16;
     }
-    if (any) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[src] + world_ + rank_, q, 0));
   }
+  copy(in, s);
+  for (int src : srcs) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[src] + world_ + rank_, q, 0));
+}
+
+void P2PComm::copy(const std::vector<P2PCopy>& segs, hipStream_t s) {
+  bool aligned = true;
+  for (const P2PCopy& c : segs)
+    aligned = aligned && c.bytes % 16 == 0 && ((uintptr_t)c.src & 15) == 0 && ((uintptr_t)c.dst & 15) == 0;
+  if (aligned) {
+    launch_multi_copy(segs, s);
+    return;
+  }
+  for (const P2PCopy& c : segs)
+    if (c.bytes) FAN_HIP_CHECK(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, s));
 }
 
 void P2PComm::all_to_all(const void* send, void* recv, size_t bpp, hipStream_t s) {

@@ -20,6 +20,14 @@
 
 namespace fan {
 
+struct P2PCopy {
+  const void* src;
+  void* dst;
+  size_t bytes;
+};
+// All segments in one (or few) kernel launches; segments 16-B aligned, sizes multiples of 16 B.
+void launch_multi_copy(const std::vector<P2PCopy>& segs, hipStream_t stream);
+
 class P2PComm : public Comm {
  public:
   P2PComm(int rank, int world, int device, size_t slot_bytes);
@@ -42,6 +50,7 @@ class P2PComm : public Comm {
   uint64_t sequence() const { return seq_; }
 
  private:
+  void copy(const std::vector<P2PCopy>& segs, hipStream_t s);
   uint8_t* slot_ptr(uint8_t* arena, int src, uint64_t seq) const { return arena + ((size_t)src * 2 + (seq & 1)) * slot_; }
   int rank_, world_, device_;
   size_t slot_;

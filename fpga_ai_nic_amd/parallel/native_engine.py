@@ -88,9 +88,11 @@ class NativeAllReduce:
 
     def __init__(self, transport: Transport | None, *, codec: str = "bfp_rne", algo: str = "mesh", rings: int = 1,
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
-                 timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None):
+                 timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None,
+                 side_stream: bool = False):
         """``comm``: an explicit ``_C.Comm`` (e.g. ``_C.LoopbackFabric(N).comm(r)`` for virtual ranks on one
-        GPU); otherwise the engine's own RCCL communicator is created from ``transport``."""
+        GPU); otherwise the engine's own RCCL communicator is created from ``transport``. ``side_stream``
+        (world 1): run requests on the engine's comm stream instead of inline (overlap measurements)."""
         if algo not in _ALGOS:
             raise ValueError(f"unknown algo {algo!r}")
         C = _ext.require()
@@ -110,7 +112,8 @@ class NativeAllReduce:
         self.codec, self.codec_id, self.algo = codec, wire.codec_id(codec), algo
         self.timeout_s = timeout_s
         self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
-                                   compat_owner_fp32, timeout_s, stream_priority, force_comm, self.device.index)
+                                   compat_owner_fp32, timeout_s, stream_priority, force_comm or side_stream,
+                                   self.device.index)
         self.orders = [list(o) for o in self.C.orders]
         self.rings = len(self.orders)
         self.inline = bool(self.C.inline)
