@@ -28,7 +28,7 @@ import torch
 from ..config import add_named_flags, config_from_args
 from ..models.mlp import MLP
 from ..parallel.dp import DataParallelTrainer, make_engine
-from ..parallel.transport import NativeTransport, TorchDistTransport
+from ..parallel.transport import NativeTransport, P2PTransport, TorchDistTransport
 from ..utils import checkpoint, dist as D, metrics
 
 
@@ -78,15 +78,20 @@ def run(argv=None, out=sys.stdout):
     transport = None
     if world > 1 or cfg.compress not in ("local",):
         if world > 1:
-            transport = NativeTransport() if cfg.transport == "native" else TorchDistTransport()
+            if cfg.transport == "p2p" and device.type == "cuda":
+                transport = P2PTransport()
+            else:
+                transport = NativeTransport() if cfg.transport == "native" else TorchDistTransport()
         else:
             from ..parallel.transport import ThreadFabric
 
             transport = ThreadFabric(1).transport(0)
     kind = cfg.compress if transport is not None else "local"
+    impl = cfg.engine if device.type == "cuda" else "python"
     engine = make_engine(transport, kind, rounding=cfg.rounding, algo=cfg.algo, rings=cfg.rings,
                          max_slice_elems=cfg.slice_elems, compat_owner_fp32=cfg.compat_owner_fp32,
-                         timeout_s=cfg.timeout_s)
+                         timeout_s=cfg.timeout_s, impl=impl,
+                         comm=transport.comm if isinstance(transport, P2PTransport) and impl == "native" else None)
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     if a.model_fuse == "hidden":
         bias, relu = True, "hidden"

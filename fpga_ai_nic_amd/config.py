@@ -32,7 +32,8 @@ class TrainConfig:
     algo: str = "mesh"             # mesh | ring
     rings: int = 1
     slice_elems: int = 1 << 22
-    transport: str = "torch"       # torch | native
+    transport: str = "torch"       # torch | native | p2p
+    engine: str = "python"         # python | native
     compat_owner_fp32: bool = False
     lr: float = 0.1
     momentum: float = 0.0
@@ -59,7 +60,9 @@ def add_named_flags(ap: argparse.ArgumentParser):
     ap.add_argument("--algo", default=d.algo, choices=["mesh", "ring"])
     ap.add_argument("--rings", type=int, default=d.rings)
     ap.add_argument("--slice-elems", type=int, default=d.slice_elems)
-    ap.add_argument("--transport", default=d.transport, choices=["torch", "native"])
+    ap.add_argument("--transport", default=d.transport, choices=["torch", "native", "p2p"])
+    ap.add_argument("--engine", default=d.engine, choices=["python", "native"],
+                    help="request path: Python-issued engine (any transport) or the C++ engine (GPU)")
     ap.add_argument("--compat-owner-fp32", action="store_true")
     ap.add_argument("--lr", type=float, default=d.lr)
     ap.add_argument("--momentum", type=float, default=d.momentum)

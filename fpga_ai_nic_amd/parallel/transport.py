@@ -8,6 +8,8 @@ All transports expose the same byte-level interface used by the all-reduce engin
   One process per GPU; ops are enqueued on the caller's current stream (host never blocks).
 * :class:`NativeTransport`   — the engine's own RCCL communicator (``_C.NativeComm``), bootstrapped
   through the torch.distributed store; no ProcessGroup in the data path.
+* :class:`P2PTransport`      — direct peer writes into HIP-IPC receive arenas over xGMI with
+  stream-ordered sequence flags (``_C.P2PComm``, csrc/comm/p2p_comm.cpp): no RCCL in the data path.
 * :class:`ThreadFabric` / :class:`ThreadTransport` — N virtual ranks as N threads of one process
   (CPU or one GPU). This is the framework's answer to the reference's 3-NIC RTL ring testbench
   (readme.pdf p.3 §3.2): the full engine runs against a simulated fabric without N GPUs.
@@ -313,9 +315,48 @@ class ThreadTransport(Transport):
         self._done()
 
 
+class P2PTransport(Transport):
+    """Byte-level transport over the direct P2P communicator (gradient plane); the uncompressed baseline's
+    all-reduce / broadcast / barrier go through torch.distributed (control plane)."""
+
+    name = "p2p"
+
+    def __init__(self, slot_bytes: int = 128 << 20):
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.comm = make_p2p_comm(self.rank, self.world, torch.cuda.current_device(), slot_bytes)
+        self._ctrl = TorchDistTransport()
+
+    def all_to_all(self, send, recv):
+        self.comm.all_to_all(_u8(send), _u8(recv))
+
+    def all_gather(self, send, recv):
+        self.comm.all_gather(_u8(send), _u8(recv))
+
+    def sendrecv(self, sends, recvs):
+        if sends or recvs:
+            self.comm.sendrecv([(_u8(t), p) for t, p in sends], [(_u8(t), p) for t, p in recvs])
+
+    def all_reduce_(self, t):
+        self._ctrl.all_reduce_(t)
+
+    def broadcast_(self, t, root=0):
+        self._ctrl.broadcast_(t, root)
+
+    def barrier(self):
+        self._ctrl.barrier()
+
+    def async_error(self):
+        return self.comm.async_error()
+
+    def abort(self):
+        self.comm.abort()
+
+
 def make_transport(kind: str = "torch", **kw) -> Transport:
     if kind == "torch":
         return TorchDistTransport(kw.get("group"))
     if kind == "native":
         return NativeTransport(**kw)
+    if kind == "p2p":
+        return P2PTransport(**kw)
     raise ValueError(f"unknown transport {kind!r}")
