@@ -199,3 +199,45 @@ def test_gemm_fused_bias_grad(C, M, N, K):
     G.linear_bwd_weight(X, dZ, dW, bias_grad=db)
     assert (dW - X.float().t() @ dZ.float()).abs().max().item() < 0.25
     assert (db - dZ.float().sum(0)).abs().max().item() < 1e-2 * K ** 0.5
+
+
+@pytest.mark.parametrize("K", [64, 128, 192, 1024, 4096])
+def test_gemm_256_tile_all_layouts_and_k(C, K):
+    """The 256x256 ping-pong schedule (forced tile) on all four operand layouts, K-tile counts 1, 2, 3 and
+    long loops, with and without split-K: vs an fp64 reference."""
+    torch.manual_seed(K)
+    M, N = 512, 768
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    Bkn = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    ref = _ref_mm(A.float(), Bkn.float())
+    tol = 2e-2 * (K ** 0.5)
+    for a_t in (False, True):
+        for b_t in (False, True):
+            Ain = A.t().contiguous() if a_t else A
+            Bin = Bkn.t().contiguous() if b_t else Bkn
+            for sk in (1, 2) if K % 128 == 0 else (1,):
+                Cout = torch.full((M, N), float("nan"), device=DEV)
+                G.gemm(Ain, a_t, Bin, b_t, Cout, split_k=sk, tile=(256, 256))
+                err = (Cout.double() - ref).abs().max().item()
+                assert err < tol, f"a_t={a_t} b_t={b_t} split_k={sk}: max err {err}"
+
+
+def test_gemm_256_tile_epilogues(C):
+    torch.manual_seed(9)
+    M, N, K = 512, 512, 768
+    X = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    W = (torch.randn(K, N, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV).to(torch.bfloat16)
+    Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm(X, False, W, False, Y, G.EPI_BIAS_RELU, bias=b, split_k=1, tile=(256, 256))
+    assert (Y.float() - torch.relu(X.float() @ W.float() + b.float())).abs().max().item() < 5e-2
+    dZ = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    act = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    dX = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    G.gemm(dZ, False, W, True, dX, G.EPI_RELU_MASK, aux=act, split_k=1, tile=(256, 256))
+    assert (dX.float() - (dZ.float() @ W.float().t()) * (act.float() > 0)).abs().max().item() < 5e-2
+    dW = torch.empty(K, N, device=DEV)
+    db = torch.zeros(N, device=DEV)
+    G.gemm(act, True, dZ, False, dW, G.EPI_NONE, split_k=1, tile=(256, 256), colsum=db)
+    assert (dW - act.float().t() @ dZ.float()).abs().max().item() < 0.25
+    assert (db - dZ.float().sum(0)).abs().max().item() < 1e-2 * M ** 0.5
