@@ -138,3 +138,17 @@ def test_native_trainer_matches_python_trainer():
         res.append((losses, [l.master.cpu() for l in m.layers]))
     assert res[0][0] == res[1][0]
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+def test_mlp_mpi_cli_native_engine_gpu():
+    """The reference entry point on GPU with the C++ engine (world 1): report lines + finite loss."""
+    import io
+
+    from fpga_ai_nic_amd.cli import mlp_mpi
+
+    out = io.StringIO()
+    res = mlp_mpi.run(["3", "512", "3", "A", "32", "32", "32", "512", "1024", "256", "--dtype", "bf16",
+                       "--engine", "native", "--warmup", "1"], out=out)
+    text = out.getvalue()
+    assert "PERFDUMP,BP," in text and "SAMPLES/S" in text
+    assert np.isfinite(res["loss"])
