@@ -36,6 +36,16 @@ def mlp_shapes(mb: int):
 MLP_SHAPES = mlp_shapes(2048)
 
 
+def bert_shapes(tokens: int):
+    """BERT-base encoder-layer backward GEMMs (BASELINE config 5) at ``tokens`` rows per GPU."""
+    import sys as _s
+    import os as _o
+    _s.path.insert(0, _o.path.dirname(_o.path.dirname(_o.path.abspath(__file__))))
+    from fpga_ai_nic_amd.models import bert
+
+    return [(name, M, N, K, a_t, b_t, G.EPI_NONE) for name, M, N, K, a_t, b_t in bert.layer_backward_gemms(tokens)]
+
+
 def time_fn(fn, iters):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -54,10 +64,12 @@ def main():
     ap.add_argument("--shapes", default="")
     ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
     ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
+    ap.add_argument("--set", default="mlp", choices=["mlp", "bert"])
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
-    for name, M, N, K, a_t, b_t, epi in mlp_shapes(a.mb):
+    shapes = mlp_shapes(a.mb) if a.set == "mlp" else bert_shapes(a.mb)
+    for name, M, N, K, a_t, b_t, epi in shapes:
         if a.shapes and name not in a.shapes.split(","):
             continue
         if a.dtype == "f32" and K > 4096:
