@@ -42,6 +42,11 @@ def build_parser():
     ap.add_argument("bk", type=int, nargs="?", default=64)
     ap.add_argument("bc", type=int, nargs="?", default=64)
     ap.add_argument("C", type=int, nargs="*")
+    ap.add_argument("--dump-norms", action="store_true",
+                    help="after training print the L1 norm of every layer's weight gradient (the reference's "
+                         "disabled libxsmm_matdiff block, sw:818-826)")
+    ap.add_argument("--verify-fwd", action="store_true",
+                    help="check one forward of the trained model against an fp32 PyTorch reference (matdiff)")
     ap.add_argument("--model-fuse", default="ref", choices=["ref", "hidden"],
                     help="ref: fuse_type semantics on every layer; hidden: bias+ReLU on hidden layers only")
     return add_named_flags(ap)
@@ -110,10 +115,11 @@ def run(argv=None, out=sys.stdout):
                                   loss_scale=cfg.loss_scale, profile=cfg.profile)
     x, y = make_data(mb, sizes[0], sizes[-1], rank, cfg.seed, device, dtype)
     threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    check = abs(float(os.environ.get("CHECK", "1") or 1))  # reference: env CHECK (sw:227-228)
     if rank == 0:
         print(" ".join(str(v) for v in (argv if argv is not None else sys.argv[1:])), file=out)
-        print(metrics.setup_banner(sizes, cfg.global_mb, cfg.iters, threads, 2 if dtype == torch.bfloat16 else 4),
-              file=out)
+        print(metrics.setup_banner(sizes, cfg.global_mb, cfg.iters, threads, 2 if dtype == torch.bfloat16 else 4,
+                                   show_threads=check == 0), file=out)
     def one_iter():
         if a.type == "A":
             trainer.step(x, y)
@@ -146,6 +152,19 @@ def run(argv=None, out=sys.stdout):
             print(f"ALLREDUCE: algo={engine.algo} codec={engine.codec} rings={engine.rings} "
                   f"wire_bytes/step={engine.stats['wire_bytes'] / max(1, engine.stats['requests']) * model.L:.4g}",
                   file=out)
+    if a.dump_norms and rank == world - 1:  # the reference prints from the last rank
+        for i, l in enumerate(model.layers):
+            print(f"L1 of layer's {i} dweights after training : {float(l.gw.double().abs().sum()):.25g}", file=out)
+    if a.verify_fwd and rank == 0:
+        xs = x[: min(64, x.shape[0])]
+        got = model.forward(xs).float().cpu()
+        h = xs.float()
+        for i, l in enumerate(model.layers):
+            h = h @ l.w.float() + (l.b.float() if model.bias else 0)
+            if model._relu_at(i):
+                h = torch.relu(h)
+        nd = metrics.matdiff(h.cpu().numpy(), got.numpy())
+        print("VERIFY fwd vs fp32 reference: " + " ".join(f"{k}={v:.6g}" for k, v in nd.items()), file=out)
     sink = metrics.JsonlSink(cfg.metrics_jsonl if rank == 0 else None)
     sink.write(kind="mlp_mpi", sizes=sizes, global_mb=cfg.global_mb, world=world, iters=cfg.iters,
                s_per_iter=total / max(cfg.iters, 1), samples_per_s=cfg.global_mb * cfg.iters / total, loss=loss,

@@ -25,11 +25,14 @@ def mlp_gflop(sizes, global_mb: int, kind: str = "A") -> float:
     return g
 
 
-def setup_banner(sizes, global_mb: int, iters: int, threads: int, bytes_per_el: int = 4) -> str:
+def setup_banner(sizes, global_mb: int, iters: int, threads: int, bytes_per_el: int = 4,
+                 show_threads: bool = True) -> str:
+    """The reference's "Setting Up (Common)" block (sw:353-377). As there, the thread count is printed only
+    when ``CHECK`` is 0 (``show_threads``)."""
     L = len(sizes) - 1
     lines = ["##########################################", "#          Setting Up (Common)           #",
              "##########################################", f"PARAMS: N:{global_mb}", f"PARAMS: Layers: {L}",
-             f"PARAMS: ITERS:{iters}  Threads:{threads}"]
+             f"PARAMS: ITERS:{iters}  Threads:{threads}" if show_threads else f"PARAMS: ITERS:{iters}"]
     mib = 1024.0 * 1024.0
     act = fil = 0.0
     for i in range(L):
@@ -69,6 +72,22 @@ def result_report(sizes, global_mb: int, mb_local: int, iters: int, total_s: flo
         lines.append(f"Bwdupd compute FIRST time overlaped = {times['bwd_first'] / n:.5g}")
         lines.append(f"Bwdupd compute time overlaped = {(times['bwd'] - times['bwd_first']) / n:.5g}")
     return "\n".join(lines)
+
+
+def matdiff(ref, tst) -> dict:
+    """Norms of a test matrix against a reference (the libxsmm_matdiff report the reference links, sw:818-826):
+    l1/l2/linf of the difference, their values relative to the reference, and the two L1 norms."""
+    import numpy as np
+
+    r = np.asarray(ref, dtype=np.float64).reshape(-1)
+    t = np.asarray(tst, dtype=np.float64).reshape(-1)
+    d = t - r
+    l1_ref, l1_tst = float(np.abs(r).sum()), float(np.abs(t).sum())
+    l2_abs, linf_abs = float(np.sqrt((d * d).sum())), float(np.abs(d).max()) if d.size else 0.0
+    nr2 = float(np.sqrt((r * r).sum()))
+    return {"l1_ref": l1_ref, "l1_tst": l1_tst, "l1_abs": float(np.abs(d).sum()),
+            "l2_abs": l2_abs, "l2_rel": l2_abs / nr2 if nr2 else 0.0,
+            "linf_abs": linf_abs, "linf_rel": linf_abs / float(np.abs(r).max()) if r.size and np.abs(r).max() else 0.0}
 
 
 def allreduce_bw(logical_bytes: float, seconds: float, world: int):

@@ -70,3 +70,27 @@ def test_fuse_variants_forward_and_grad(bias, relu):
             assert torch.allclose(l.gb, bs[i].grad, atol=1e-5)
         else:
             assert torch.count_nonzero(l.gb) == 0
+
+
+def test_check_env_and_norm_dumps(monkeypatch):
+    monkeypatch.setenv("CHECK", "0")  # reference quirk: thread count printed only when CHECK is 0
+    out = io.StringIO()
+    mlp_mpi.run(["2", "16", "3", "A"] + ARGS + ["--dump-norms", "--verify-fwd"], out=out)
+    text = out.getvalue()
+    assert "Threads:" in text
+    assert text.count("L1 of layer's") == 2
+    line = [l for l in text.splitlines() if l.startswith("VERIFY fwd")][0]
+    linf = float(line.split("linf_abs=")[1].split()[0])
+    assert linf < 1e-4
+    monkeypatch.setenv("CHECK", "1")
+    out = io.StringIO()
+    mlp_mpi.run(["1", "16", "3", "A"] + ARGS, out=out)
+    assert "Threads:" not in out.getvalue()
+
+
+def test_matdiff():
+    import numpy as np
+
+    r = np.array([1.0, -2.0, 3.0])
+    d = metrics.matdiff(r, r + np.array([0.0, 0.5, 0.0]))
+    assert d["l1_ref"] == 6.0 and d["linf_abs"] == 0.5 and abs(d["l2_rel"] - 0.5 / np.sqrt(14)) < 1e-12
