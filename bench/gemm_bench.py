@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
     ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
     ap.add_argument("--set", default="mlp", choices=["mlp", "bert"])
+    ap.add_argument("--ab", action="store_true", help="also time the one-role main loop (ping-pong off)")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
@@ -106,7 +107,7 @@ def main():
             res = {}
             for tile in ((256, 256), (256, 128), (128, 256), (128, 128)):
                 for waves in (8, 4):
-                    for sk in (1, 2):
+                    for sk in (1, 2, 4):
                         if M % tile[0] or N % tile[1] or K % (64 * sk):
                             continue
                         t3 = tile + (waves,)
@@ -123,8 +124,13 @@ def main():
                               "auto_plan": G._ext.require().gemm_plan(M, N, K)}), flush=True)
         mine(); ref(); torch.cuda.synchronize()
         err = (C.float() - (ref().float() * ((aux > 0) if epi == G.EPI_RELU_MASK else 1))).abs().max().item()
-        tm, tr, tmm = [], [], []
+        tm, tr, tmm, tone = [], [], [], []
+        Cx = G._ext.require()
         for _ in range(a.rounds):
+            if a.ab:  # same plan with the one-role main loop (256x256 tiles only differ)
+                Cx.gemm_set_pingpong(False)
+                tone.append(time_fn(mine, a.iters))
+                Cx.gemm_set_pingpong(True)
             tm.append(time_fn(mine, a.iters))
             tr.append(time_fn(ref, a.iters))
             tmm.append(time_fn(ref_mm_only, a.iters))
@@ -136,7 +142,8 @@ def main():
                           "mine_us": round(m, 2), "mine_tflops": round(flop / m / 1e6, 1),
                           "torch_fused_us": round(r, 2), "torch_matmul_only_us": round(rm, 2),
                           "torch_matmul_tflops": round(flop / rm / 1e6, 1), "speedup_vs_torch_fused": round(r / m, 3),
-                          "max_abs_err": err}), flush=True)
+                          "max_abs_err": err,
+                          **({"oneloop_us": round(statistics.median(tone), 2)} if tone else {})}), flush=True)
 
 
 if __name__ == "__main__":

@@ -85,6 +85,13 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
   }
   if (A.scalar_type() == at::kBFloat16) {
     TORCH_CHECK(bias ? bias->scalar_type() == at::kBFloat16 : true, "bias must be bf16");
+    const GemmPlan p = gemm_bf16_plan(g.M, g.N, g.K, g.split_k, g.tile_bm, g.tile_bn, g.tile_waves);
+    if (p.split_k > 1) {
+      const int64_t need = (int64_t)p.split_k * ((int64_t)g.M * g.N + (g.colsum ? g.N : 0));
+      TORCH_CHECK(workspace && workspace->scalar_type() == at::kFloat && workspace->is_contiguous() &&
+                      workspace->numel() >= need,
+                  "gemm: split-K ", p.split_k, " needs an f32 workspace of ", need, " elements");
+    }
     TORCH_CHECK(gemm_bf16_supported(g), "gemm_bf16: unsupported shape M=", g.M, " N=", g.N, " K=", g.K,
                 " split_k=", g.split_k);
     launch_gemm_bf16(g, fan_stream());
@@ -146,6 +153,8 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("wire") = pybind11::none(), pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1,
         pybind11::arg("wire_codec") = 1);
   m.def("gemm_supported", &gemm_supported);
+  m.def("gemm_set_pingpong", [](bool on) { gemm_pingpong_flag().store(on); },
+        "256x256 GEMM tiles: ping-pong main loop (default) or the one-role loop");
   m.def("gemm_plan", &gemm_plan, "bf16 GEMM tile/split-K plan (bm, bn, split_k, waves); bm == 0: unsupported",
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0,
         pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0, pybind11::arg("tile_waves") = 0);

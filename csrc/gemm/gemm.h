@@ -6,6 +6,8 @@
 // so forward (X·W, W=[in][out]), backward-data (dZ·Wᵀ) and backward-weight (Xᵀ·dZ) of the
 // MLP all run without a transpose pass (reference: libxsmm fc fwd/bwd, sw/mlp_mpi_example_f32.cpp:708, 741, 770).
 #pragma once
+#include <atomic>
+
 #include "common/hip_common.h"
 
 namespace fan {
@@ -31,7 +33,7 @@ struct GemmArgs {
   bool c_bf16;       // output dtype (bf16 or f32)
   bool accumulate;   // C += result (f32 output only)
   int split_k;       // 0: auto; >=1: K split over workgroups (fp32 partial slabs + ordered reduce)
-  void* workspace;   // split-K slabs: split_k * M * N floats
+  void* workspace;   // split-K slabs: split_k * M * N floats (+ split_k * N with colsum: bias-gradient partials)
   int tile_bm = 0;   // 0: automatic tile choice; else force BM x BN (128/256)
   int tile_bn = 0;
   int tile_waves = 0;  // 0: default; 4 or 8 waves per workgroup
@@ -59,6 +61,9 @@ GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm = 0, int t
 // Returns false if the shape is not supported by the MFMA path (caller must then error out).
 bool gemm_bf16_supported(const GemmArgs& a);
 void launch_gemm_bf16(const GemmArgs& a, hipStream_t stream);
+
+// 256x256 tiles: staggered 4-phase main loop (true; env FAN_GEMM_PP=1 starts with true) or the one-role loop.
+std::atomic<bool>& gemm_pingpong_flag();
 
 bool gemm_f32_supported(const GemmArgs& a);
 void launch_gemm_f32(const GemmArgs& a, hipStream_t stream);

@@ -48,28 +48,34 @@ struct OpTile {
   static constexpr int PER_HALF = (64 * 256) / IB;  // MN-contig: instructions per 128-column half
 };
 
-// Stage one operand tile (outer extent OUTER from o0, k extent 64 from k0) with NT threads.
+// Issue glds instruction i (of OpTile::GLDS) of one operand tile (outer extent OUTER from o0, k extent 64 from
+// k0) with NT threads: this wave's 1 KiB piece of it.
+template <bool KCONTIG, int OUTER, int NT>
+__device__ __forceinline__ void stage_one(const bf16_t* __restrict__ g, int64_t ld, int o0, int k0, char* lds,
+                                          int wave, int lane, int i) {
+  using T = OpTile<OUTER, NT>;
+  const int t = wave * 64 + lane;
+  const bf16_t* src;
+  if (KCONTIG) {
+    const int row = i * (T::IB / 128) + (t >> 3);  // rows of 128 B
+    const int c = (t & 7) ^ ((row >> 1) & 7);
+    src = g + (int64_t)(o0 + row) * ld + k0 + c * 8;
+  } else {
+    const int half = i / T::PER_HALF;                               // 128-column half
+    const int krow = (i % T::PER_HALF) * (T::IB / 256) + (t >> 4);  // k-rows of 256 B
+    const int cs = t & 15;
+    const int blk = (cs >> 1) ^ mn_swz(krow);
+    src = g + (int64_t)(k0 + krow) * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8;
+  }
+  glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + i * T::IB + wave * 1024)));
+}
+
+// Stage one whole operand tile.
 template <bool KCONTIG, int OUTER, int NT>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int64_t ld, int o0, int k0, char* lds,
                                            int wave, int lane) {
-  using T = OpTile<OUTER, NT>;
-  const int t = wave * 64 + lane;
 #pragma unroll
-  for (int i = 0; i < T::GLDS; ++i) {
-    const bf16_t* src;
-    if (KCONTIG) {
-      const int row = i * (T::IB / 128) + (t >> 3);  // rows of 128 B
-      const int c = (t & 7) ^ ((row >> 1) & 7);
-      src = g + (int64_t)(o0 + row) * ld + k0 + c * 8;
-    } else {
-      const int half = i / T::PER_HALF;                               // 128-column half
-      const int krow = (i % T::PER_HALF) * (T::IB / 256) + (t >> 4);  // k-rows of 256 B
-      const int cs = t & 15;
-      const int blk = (cs >> 1) ^ mn_swz(krow);
-      src = g + (int64_t)(k0 + krow) * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8;
-    }
-    glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + i * T::IB + wave * 1024)));
-  }
+  for (int i = 0; i < OpTile<OUTER, NT>::GLDS; ++i) stage_one<KCONTIG, OUTER, NT>(g, ld, o0, k0, lds, wave, lane, i);
 }
 
 template <bool KCONTIG>
@@ -188,10 +194,9 @@ __device__ __forceinline__ int32_t wire_encode(float x, uint32_t E, int codec) {
   return codec == kBfpTrunc ? bfp_encode_trunc(__float_as_uint(x), E) : bfp_encode_rne(x, E);
 }
 
-// Encode one whole 16-column group held by this lane: 16-B mantissa store + 1 exponent byte.
-__device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
-                                           int row, int col) {
-  const uint32_t f = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
+// Encode the 16-value group at flat bucket index f (f % 16 == 0) held by this lane: 16-B mantissa store +
+// 1 exponent byte. Returns the shard it landed in.
+__device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const WireOut& wo) {
   const int sh = wire_shard_of(f, wo);
   const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
   uint32_t mx = 0;
@@ -204,10 +209,108 @@ __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict_
   uint8_t* base = wire_shard_base(sh, wo);
   *reinterpret_cast<uint4*>(base + pos) = make_uint4(w[0], w[1], w[2], w[3]);
   base[wo.shard + pos / 16] = (uint8_t)E;
-  if (sh == wo.own) {
+  return sh;
+}
+
+// Encode one whole 16-column group of C(row, col..col+15); the owner shard is also written to C in f32.
+__device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
+                                           int row, int col) {
+  const uint32_t f = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
+  if (wire_store16(v, f, wo) == wo.own) {
 #pragma unroll
     for (int u = 0; u < 16; u += 4)
       *reinterpret_cast<float4*>(C + f + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
+  }
+}
+
+// Fused bias gradient tail: lanes l, l^16, l^32, l^48 hold the same column over different k rows. Writes
+// out[col0 + j*16 + lane] (the column sums, or this K-split's partial sums); with kEpiWire and no split-K also
+// encodes the bias segment of the [W | b] bucket (its 16-column group is lanes 0..15).
+template <int NJ, int WTN, int EPI, bool SPLIT>
+__device__ __forceinline__ void colsum_finish(float (&cs)[NJ], int lane, int col0, float* __restrict__ out,
+                                              const WireOut& wo) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    float v = cs[j];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    const int col = col0 + j * 16 + (lane & 15);
+    if (lane < 16) out[col] = v;
+    if constexpr (EPI == kEpiWire && !SPLIT) {
+      if (wo.bias_off > 0) {
+        uint32_t mx = __float_as_uint(v) & 0x7FFFFFFFu;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        const uint32_t E = mx >> 23;
+        const uint32_t f = (uint32_t)wo.bias_off + (uint32_t)col;
+        const int sh = wire_shard_of(f, wo);
+        const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
+        uint8_t* base = wire_shard_base(sh, wo);
+        if (lane < 16) base[pos] = (uint8_t)(wire_encode(v, E, wo.codec) & 0xFF);
+        if (lane == 0) base[wo.shard + pos / 16] = (uint8_t)E;
+      }
+    }
+  }
+}
+
+// Epilogue of one wave's (MI*16) x WTN accumulator tile at C(row0, col0), staged through a wave-private LDS
+// region one 16-row block at a time and written as coalesced row segments (f32 16 B / bf16 8 B per lane), with
+// the fused epilogue; SPLIT writes the f32 partial slab of K-split ksplit; kEpiWire encodes whole 16-column
+// groups (one lane per group: 16-B mantissa store + exponent byte). Caller: all LDS operand reads retired.
+template <int MI, int NJ, int WTN, int EPI, typename TC, bool ACCUM, bool SPLIT>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* smem, int wave, int lane, int row0,
+                                           int col0, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
+                                           const TC* __restrict__ aux, int64_t ldaux, int M, int N, int ksplit,
+                                           float* __restrict__ ws, const WireOut& wo) {
+  constexpr int EW = WTN + 4;  // staged row stride in floats (16-B aligned, breaks bank aliasing)
+  float* stg = reinterpret_cast<float*>(smem) + wave * (16 * EW);
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  constexpr int C4 = WTN / 4;   // float4 chunks per staged row
+  constexpr int RPI = 64 / C4;  // rows covered per pass by the wave
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[(row_l + r) * EW + j * 16 + col_l] = acc[i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own LDS writes landed (wave-private region)
+    if constexpr (EPI == kEpiWire && !SPLIT) {
+      constexpr int G16 = WTN / 16;  // groups per staged row
+      constexpr int RPG = 64 / G16;  // rows per pass (lanes beyond 16 rows idle)
+      constexpr int PASSES = RPG >= 16 ? 1 : 16 / RPG;
+#pragma unroll
+      for (int pass = 0; pass < PASSES; ++pass) {
+        const int rr = pass * RPG + lane / G16;
+        if (RPG <= 16 || rr < 16) {
+          const int cc = (lane % G16) * 16;
+          float v[16];
+#pragma unroll
+          for (int u = 0; u < 16; u += 4) {
+            const float4 q = *reinterpret_cast<const float4*>(stg + rr * EW + cc + u);
+            v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
+          }
+          wire_epi16(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr, col0 + cc);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      continue;
+    }
+#pragma unroll
+    for (int pass = 0; pass < 16 / RPI; ++pass) {
+      const int rr = pass * RPI + lane / C4;
+      const int cc = (lane % C4) * 4;
+      const float4 q = *reinterpret_cast<const float4*>(stg + rr * EW + cc);
+      float v[4] = {q.x, q.y, q.z, q.w};
+      const int row = row0 + i * 16 + rr;
+      const int col = col0 + cc;
+      if (SPLIT) {
+        float* slab = ws + (int64_t)ksplit * M * N;
+        *reinterpret_cast<float4*>(slab + (int64_t)row * N + col) = q;
+      } else {
+        epi4<EPI, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
   }
 }
 
@@ -252,7 +355,7 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
   // fused bias gradient: the waves of the first row-block sum the (MN-contiguous) B fragments they read
-  const bool do_colsum = !BKC && colsum != nullptr && m0 == 0 && wm == 0;
+  const bool do_colsum = !BKC && colsum != nullptr && m0 == 0 && wm == 0;  // (SPLIT: partial sums)
   float cs[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
@@ -348,84 +451,201 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
     }
   }
 
-  if (do_colsum) {  // lanes l, l^16, l^32, l^48 hold the same column over different k rows
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      float v = cs[j];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      const int col = n0 + wn * WTN + j * 16 + (lane & 15);
-      if (lane < 16) colsum[col] = v;
-      if constexpr (EPI == kEpiWire) {
-        if (wo.bias_off > 0) {  // the bias segment's 16-column group is lanes 0..15: encode it here too
-          uint32_t mx = __float_as_uint(v) & 0x7FFFFFFFu;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-          const uint32_t E = mx >> 23;
-          const uint32_t f = (uint32_t)wo.bias_off + (uint32_t)col;
-          const int sh = wire_shard_of(f, wo);
-          const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
-          uint8_t* base = wire_shard_base(sh, wo);
-          if (lane < 16) base[pos] = (uint8_t)(wire_encode(v, E, wo.codec) & 0xFF);
-          if (lane == 0) base[wo.shard + pos / 16] = (uint8_t)E;
-        }
-      }
-    }
-  }
-
-  // ---------------- epilogue through LDS (per wave region, one 16-row block at a time)
+  if (do_colsum)
+    colsum_finish<NJ, WTN, EPI, SPLIT>(cs, lane, n0 + wn * WTN, SPLIT ? ws + (int64_t)split_k * M * N + (int64_t)ksplit * N
+                                                                      : colsum, wo);
   __syncthreads();  // all waves done reading the operand ring
-  constexpr int EW = WTN + 4;  // staged row stride in floats (16-B aligned, breaks bank aliasing)
-  float* stg = reinterpret_cast<float*>(smem) + wave * (16 * EW);
-  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  constexpr int C4 = WTN / 4;          // float4 chunks per staged row
-  constexpr int RPI = 64 / C4;         // rows covered per pass by the wave
+  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
+                                                 aux, ldaux, M, N, ksplit, ws, wo);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Staggered 4-phase 256x256 kernel (8 waves = two groups of 4; one wave of each group per SIMD).
+//
+// Waves are arranged as in the one-role 256x256 kernel (2 x 4; wave w owns rows (w>>2)*128.., cols (w&3)*64..,
+// a 128x64 sub-tile), so the epilogue is shared. Each K-tile runs as 4 phases, one per accumulator quadrant
+// (64x32 = 4x2 MFMA tiles x 2 k-steps = 16 MFMAs):
+//   phase 0: quadrant (0,0), reads A rows 0..63 + B cols 0..31 of the wave tile (12 fragments)
+//   phase 1: quadrant (0,1), reads B cols 32..63 (4)      phase 2: quadrant (1,1), reads A rows 64..127 (8)
+//   phase 3: quadrant (1,0), reads nothing
+// One phase = {glds pieces + fragment reads} barrier {lgkmcnt(0); 16 MFMAs} barrier. Group 1 (waves 4..7) runs
+// one barrier behind group 0 (an extra barrier before the loop, matched by one of group 0 after it), so between
+// any two barriers one wave of each SIMD issues MFMAs while its partner reads LDS and issues DMA.
+//
+// LDS: 2 stages x (A 256x64 + B 256x64 bf16) = 128 KiB, K-tile t in stage t&1. Global barrier index: group 0
+// reads phase p before barrier 2p+1 and runs its MFMAs before 2p+2; group 1 uses 2p+2 / 2p+3.
+//  * WAR: K-tile t+1 overwrites the stage of K-tile t-1, whose last reads (phase 2 of t-1, group 1) retired
+//    before barrier 8t-1; the pieces of t+1 are issued in phases 0..2 of t, after barrier 8t at the earliest.
+//  * RAW: K-tile t+1 is first read after barrier 8t+8 (group 0) / 8t+9 (group 1); every wave retires its own
+//    pieces (vmcnt(0)) before it arrives at barrier 8t+8: group 0 after its phase-3 MFMAs, group 1 before its
+//    phase-3 mid barrier. No other vector-memory operation is in flight in the loop.
+// Raw s_barrier only (a __syncthreads() would drain vmcnt); sched_barrier keeps every instruction on its side.
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// glds instruction i of a K-tile: 0..3 the A tile, 4..7 the B tile (this wave's 1 KiB piece).
+template <bool AK, bool BKC>
+__device__ __forceinline__ void pp_piece(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+                                         int64_t ldb, int m0, int n0, int k0, char* st, int wave, int lane, int i) {
+  constexpr int GA = OpTile<256, 512>::GLDS;
+  if (i < GA) stage_one<AK, 256, 512>(A, lda, m0, k0, st, wave, lane, i);
+  else stage_one<BKC, 256, 512>(B, ldb, n0, k0, st + OpTile<256, 512>::BYTES, wave, lane, i - GA);
+}
+
+// Quadrant Q of the phase schedule: fragment reads and MFMAs. fa[qm][ks][i]: A fragments of quadrant row qm;
+// fb[qn][ks][j]: B fragments of quadrant column qn (all indices compile-time after unrolling).
+template <int Q, bool AK, bool BKC>
+struct PPPhase {
+  static constexpr int QM = (Q == 0 || Q == 1) ? 0 : 1;
+  static constexpr int QN = (Q == 1 || Q == 2) ? 1 : 0;
+  __device__ static __forceinline__ void read(const char* sa, const char* sb, int wrow, int wcol, int lane,
+                                              s16x8 (&fa)[2][2][4], s16x8 (&fb)[2][2][2]) {
+    if constexpr (Q == 0 || Q == 2) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) stg[(row_l + r) * EW + j * 16 + col_l] = acc[i][j][r];
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own LDS writes landed (wave-private region)
-    if constexpr (EPI == kEpiWire && !SPLIT) {
-      // one lane per 16-column group: no cross-lane exponent exchange, 16-B mantissa stores
-      constexpr int G16 = WTN / 16;                    // groups per staged row
-      constexpr int RPG = 64 / G16;                    // rows per pass (lanes beyond 16 rows idle)
-      constexpr int PASSES = RPG >= 16 ? 1 : 16 / RPG;
-#pragma unroll
-      for (int pass = 0; pass < PASSES; ++pass) {
-        const int rr = pass * RPG + lane / G16;
-        if (RPG <= 16 || rr < 16) {
-          const int cc = (lane % G16) * 16;
-          float v[16];
-#pragma unroll
-          for (int u = 0; u < 16; u += 4) {
-            const float4 q = *reinterpret_cast<const float4*>(stg + rr * EW + cc + u);
-            v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
-          }
-          wire_epi16(v, reinterpret_cast<float*>(C), ldc, wo, m0 + wm * WTM + i * 16 + rr, n0 + wn * WTN + cc);
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      continue;
+        for (int i = 0; i < 4; ++i) fa[QM][ks][i] = read_frag<AK>(sa, wrow + QM * 64 + i * 16, ks, lane);
     }
+    if constexpr (Q == 0 || Q == 1) {
 #pragma unroll
-    for (int pass = 0; pass < 16 / RPI; ++pass) {
-      const int rr = pass * RPI + lane / C4;
-      const int cc = (lane % C4) * 4;
-      const float4 q = *reinterpret_cast<const float4*>(stg + rr * EW + cc);
-      float v[4] = {q.x, q.y, q.z, q.w};
-      const int row = m0 + wm * WTM + i * 16 + rr;
-      const int col = n0 + wn * WTN + cc;
-      if (SPLIT) {
-        float* slab = ws + (int64_t)ksplit * M * N;
-        *reinterpret_cast<float4*>(slab + (int64_t)row * N + col) = q;
-      } else {
-        epi4<EPI, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
-      }
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[QN][ks][j] = read_frag<BKC>(sb, wcol + QN * 32 + j * 16, ks, lane);
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
   }
+  __device__ static __forceinline__ void mfma(f32x4 (&acc)[8][4], const s16x8 (&fa)[2][2][4],
+                                              const s16x8 (&fb)[2][2][2], bool do_colsum, float (&cs)[4]) {
+    if constexpr (Q == 0 || Q == 1) {  // fused bias gradient: each B fragment is read once per K-tile
+      if (do_colsum) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) cs[QN * 2 + j] += frag_sum(fb[QN][ks][j]);
+      }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[QM * 4 + i][QN * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, fa[QM][ks][i]), __builtin_bit_cast(bf16x8, fb[QN][ks][j]),
+              acc[QM * 4 + i][QN * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+};
+
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
+__global__ void __launch_bounds__(512, 2)
+    gemm_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
+                   TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
+                   int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
+                   float* __restrict__ colsum, WireOut wo) {
+  constexpr int BM = 256, BN = 256, NT = 512;
+  constexpr int A_BYTES = OpTile<BM, NT>::BYTES, B_BYTES = OpTile<BN, NT>::BYTES;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  static_assert(OpTile<BM, NT>::GLDS == 4 && OpTile<BN, NT>::GLDS == 4, "8 glds pieces per K-tile");
+  constexpr int WTM = 128, WTN = 64;
+  constexpr int MI = WTM / 16, NJ = WTN / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tiles_n = N / BN;
+  const int tiles = (M / BM) * tiles_n;
+  const int nwg = tiles * split_k;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tile = wg % tiles;
+  const int ksplit = wg / tiles;
+  const int tiles_m = M / BM;
+  const int GM = tiles_m >= 4 ? 4 : tiles_m;
+  const int gr = tile / (GM * tiles_n);
+  const int gm = (tiles_m - gr * GM) < GM ? (tiles_m - gr * GM) : GM;
+  const int in_grp = tile % (GM * tiles_n);
+  const int m0 = (gr * GM + in_grp % gm) * BM;
+  const int n0 = (in_grp / gm) * BN;
+  const int k_per = K / split_k;
+  const int kbeg = ksplit * k_per;
+  const int nk = k_per / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wave >> 2;
+  const int wrow = grp * WTM;         // wave sub-tile origin inside the block tile
+  const int wcol = (wave & 3) * WTN;
+  const bool do_colsum = !BKC && colsum != nullptr && m0 == 0 && grp == 0;
+  float cs[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 fa[2][2][4], fb[2][2][2];
+
+  // prologue: K-tile 0, every wave its pieces; then the one-barrier stagger of group 1
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, kbeg, smem, wave, lane, i);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (grp == 1) pp_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sa = smem + (kt & 1) * STAGE;
+    const char* sb = sa + A_BYTES;
+    char* nst = smem + ((kt + 1) & 1) * STAGE;
+    const bool pf = kt + 1 < nk;
+    const int k1 = kbeg + (kt + 1) * BK;
+    // phase 0: pieces 0..2 of K-tile kt+1, A rows 0..63 + B cols 0..31 of kt
+    if (pf) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, k1, nst, wave, lane, i);
+    }
+    PPPhase<0, AK, BKC>::read(sa, sb, wrow, wcol, lane, fa, fb);
+    pp_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    PPPhase<0, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
+    pp_barrier();
+    // phase 1: pieces 3..5, B cols 32..63
+    if (pf) {
+#pragma unroll
+      for (int i = 3; i < 6; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, k1, nst, wave, lane, i);
+    }
+    PPPhase<1, AK, BKC>::read(sa, sb, wrow, wcol, lane, fa, fb);
+    pp_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    PPPhase<1, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
+    pp_barrier();
+    // phase 2: pieces 6..7, A rows 64..127
+    if (pf) {
+#pragma unroll
+      for (int i = 6; i < 8; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, k1, nst, wave, lane, i);
+    }
+    PPPhase<2, AK, BKC>::read(sa, sb, wrow, wcol, lane, fa, fb);
+    pp_barrier();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    PPPhase<2, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
+    pp_barrier();
+    // phase 3: no reads; retire this wave's pieces of kt+1 before barrier 8kt+8 (see the header)
+    if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    PPPhase<3, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
+    if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+  }
+  if (grp == 0) pp_barrier();  // match group 1's stagger barrier
+  __syncthreads();             // every operand read retired before the epilogue reuses the LDS
+
+  if (do_colsum)
+    colsum_finish<NJ, WTN, EPI, SPLIT>(cs, lane, n0 + wcol, SPLIT ? ws + (int64_t)split_k * M * N + (int64_t)ksplit * N
+                                                                   : colsum, wo);
+  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wrow, n0 + wcol, C, ldc, bias, aux,
+                                                 ldaux, M, N, ksplit, ws, wo);
 }
 
 // Ordered split-K reduction + epilogue (deterministic: slabs summed in split order).
@@ -447,35 +667,121 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Ordered reduction of the per-split bias-gradient partial sums (written after the slabs: ws[split_k*M*N + k*N]).
+template <int kUnused = 0>  // template: the header is included by several translation units
+__global__ void __launch_bounds__(256)
+    splitk_colsum_kernel(const float* __restrict__ part, int split_k, float* __restrict__ colsum, int N) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = part[n];
+  for (int k = 1; k < split_k; ++k) s += part[(int64_t)k * N + n];
+  colsum[n] = s;
+}
+
+// Split-K reduction for the wire epilogue: one thread per 16-column group sums the slabs in split order and
+// encodes the group into the all-reduce wire (owner shard also in f32). With colsum, the threads past the
+// M*N/16 groups reduce the bias partial sums, write colsum[] and encode the bias segment of the [W | b] bucket.
+template <int kUnused = 0>
+__global__ void __launch_bounds__(256)
+    splitk_reduce_wire_kernel(const float* __restrict__ ws, int split_k, float* __restrict__ C, int64_t ldc, int M,
+                              int N, float* __restrict__ colsum, WireOut wo) {
+  const int gpr = N / 16;
+  const int64_t groups = (int64_t)M * gpr;
+  const int64_t total = groups + (colsum ? gpr : 0);
+  const int64_t slab = (int64_t)M * N;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    float v[16];
+    const float* p;
+    int64_t stride;
+    int row, col;
+    if (g < groups) {
+      row = (int)(g / gpr);
+      col = (int)(g % gpr) * 16;
+      p = ws + (int64_t)row * N + col;
+      stride = slab;
+    } else {
+      row = -1;
+      col = (int)(g - groups) * 16;
+      p = ws + (int64_t)split_k * slab + col;
+      stride = N;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(p + u);
+      v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
+    }
+    for (int k = 1; k < split_k; ++k) {
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(p + k * stride + u);
+        v[u] += q.x; v[u + 1] += q.y; v[u + 2] += q.z; v[u + 3] += q.w;
+      }
+    }
+    if (row >= 0) {
+      wire_epi16(v, C, ldc, wo, row, col);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) colsum[col + u] = v[u];
+      if (wo.bias_off > 0) wire_store16(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
+    }
+  }
+}
+
 template <int BM, int BN>
 constexpr int lds_bytes() {
   constexpr int st = (BM + BN) * BK * 2;
   return ((3 * st <= 160 * 1024) ? 3 : 2) * st;
 }
 
+// Ping-pong main loop for 256x256 tiles (default); FAN_GEMM_PP=0 or gemm_set_pingpong(false) selects the
+// one-role loop (A/B comparisons in one process).
+inline bool use_pingpong() { return gemm_pingpong_flag().load(std::memory_order_relaxed); }
+
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
+void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
+  const int grid = (a.M / BM) * (a.N / BN) * sk;
+  if constexpr (BM == 256 && BN == 256 && WM * WN == 8) {
+    if (use_pingpong()) {
+      constexpr int lds = 2 * (BM + BN) * BK * 2;
+      auto k = gemm_pp_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT>;
+      FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+      hipLaunchKernelGGL(k, grid, 512, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
+                         (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
+                         a.colsum, wo);
+      return;
+    }
+  }
+  constexpr int lds = lds_bytes<BM, BN>();
+  auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, SPLIT>;
+  FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
+                     a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
+                     a.colsum, wo);
+}
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
 void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
-  const int tiles = (a.M / BM) * (a.N / BN);
-  const int grid = tiles * sk;
-  constexpr int lds = lds_bytes<BM, BN>();
+  const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_codec,
+                   a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
+                   a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0};
   if (sk > 1) {
-    auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, true>;
-    FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
-                       (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
-                       (float*)nullptr, WireOut{nullptr, 0, -1, 0, 0.f, 0});
-    hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
-                       (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
-                       a.ldaux, a.M, a.N);
+    // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + k*N]), then an ordered reduce that
+    // applies the epilogue (deterministic: slabs summed in split order)
+    launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, true>(a, sk, wo, s);
+    if constexpr (EPI == kEpiWire) {
+      const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
+      hipLaunchKernelGGL(splitk_reduce_wire_kernel<0>, stream_grid(items), 256, 0, s, (const float*)a.workspace, sk,
+                         (float*)a.C, a.ldc, a.M, a.N, a.colsum, wo);
+    } else {
+      hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
+                         (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
+                         a.ldaux, a.M, a.N);
+      if (a.colsum)
+        hipLaunchKernelGGL(splitk_colsum_kernel<0>, (a.N + 255) / 256, 256, 0, s,
+                           (const float*)a.workspace + (size_t)sk * a.M * a.N, sk, a.colsum, a.N);
+    }
   } else {
-    auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>;
-    FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
-                       (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1, (float*)nullptr,
-                       a.colsum,
-                       WireOut{a.wire, a.wire_shard, a.wire_own, a.wire_codec,
-                               a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
-                               a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0});
+    launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>(a, sk, wo, s);
   }
 }
 
@@ -494,7 +800,7 @@ void launch_epi(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_EPI_CASE(kEpiReluMask)
     case kEpiWire:  // only the bwd-weight layout (A and B MN-contiguous) produces wire-ready gradients
       if constexpr (!AK && !BKC) {
-        FAN_CHECK(sk == 1 && !a.c_bf16 && !a.accumulate, "wire epilogue: f32, no split-K, no accumulate");
+        FAN_CHECK(!a.c_bf16 && !a.accumulate, "wire epilogue: f32, no accumulate");
         launch_typed<BM, BN, WM, WN, AK, BKC, kEpiWire, float, false>(a, sk, s);
         break;
       }

@@ -15,6 +15,15 @@ extern template void launch_tile<true, false>(const GemmArgs&, int, int, int, in
 extern template void launch_tile<true, true>(const GemmArgs&, int, int, int, int, hipStream_t);
 }  // namespace gemm_detail
 
+std::atomic<bool>& gemm_pingpong_flag() {
+  // Off by default until it measures faster than the one-role loop (FAN_GEMM_PP=1 / gemm_set_pingpong(true)).
+  static std::atomic<bool> flag{[] {
+    const char* e = getenv("FAN_GEMM_PP");
+    return e && e[0] == '1';
+  }()};
+  return flag;
+}
+
 GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn, int tile_waves) {
   GemmPlan p{0, 0, 1, 8};
   if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % BK) return p;
@@ -38,9 +47,22 @@ GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_
     }
   }
   if (best < 0) return p;
-  const int tiles = (M / cand[best][0]) * (N / cand[best][1]);
   int sk = 1;
-  if (split_k > 0) {
+  // Narrow output with a long K (the MLP's 1024x4096 bwd-weight, K = minibatch): 128x128 tiles fill the CUs but
+  // stream twice the operand bytes per FLOP; 256x256 tiles with K split over the CUs win despite the f32 slab
+  // round trip (measured at K = 8192: 256x256 split 4 = 82 us vs 128x128 = 100 us).
+  if (tile_bm == 0 && split_k <= 0 && best == 3 && M % 256 == 0 && N % 256 == 0) {
+    const int t256 = (M / 256) * (N / 256);
+    int s = 1;
+    while (t256 * s < kNumCU && K % (BK * s * 2) == 0 && K / (s * 2) >= 1024) s *= 2;
+    if (t256 * s >= kNumCU) {
+      best = 0;
+      sk = s;
+    }
+  }
+  const int tiles = (M / cand[best][0]) * (N / cand[best][1]);
+  if (sk > 1) {
+  } else if (split_k > 0) {
     sk = split_k;
     if (K % (BK * sk)) return p;
   } else if (tiles * 2 <= kNumCU) {
@@ -66,9 +88,9 @@ bool gemm_bf16_supported(const GemmArgs& a) {
   if (((uintptr_t)a.C) & (a.c_bf16 ? 7 : 15)) return false;
   if (a.accumulate && a.c_bf16) return false;
   if (p.split_k > 1 && a.workspace == nullptr) return false;
-  if (a.colsum && (p.split_k > 1 || a.b_kcontig)) return false;
+  if (a.colsum && a.b_kcontig) return false;
   if (a.epilogue == kEpiWire) {
-    if (p.split_k > 1 || a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire) return false;
+    if (a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire) return false;
     if (a.wire_shard <= 0 || a.wire_shard % 256 || a.ldc % 16) return false;
     if (a.wire_codec != kBfpTrunc && a.wire_codec != kBfpRne) return false;
     if ((int64_t)a.M * a.ldc + a.N >= (int64_t(1) << 31)) return false;

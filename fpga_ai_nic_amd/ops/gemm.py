@@ -58,7 +58,12 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
         M, K, N = A.shape[1], A.shape[0], B.shape[1]
         tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
         buf, shard, own, codec = wire
-        Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, 1, None, tbm, tbn, colsum, tw, buf, int(shard),
+        sk = 0 if split_k is None else int(split_k)
+        bm, _bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
+        if bm == 0:
+            raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
+        ws = _workspace(C.device, sk * (M * N + N)) if sk > 1 else None
+        Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, tbm, tbn, colsum, tw, buf, int(shard),
                 int(own), int(codec))
         return C
     if C.is_cuda:
@@ -75,14 +80,13 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
                 gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile)
                 _nn.col_sum(B.t() if b_t else B, colsum)
                 return C
-            sk = 1
         tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
         if A.dtype == torch.bfloat16:
             bm, bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
             if bm == 0:
                 raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
             if sk > 1:
-                ws = _workspace(C.device, sk * M * N)
+                ws = _workspace(C.device, sk * (M * N + N))
         else:
             sk = 1
         Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, tbm, tbn, colsum, tw)

@@ -188,22 +188,36 @@ def test_col_sum(C):
     assert (out - x.float().sum(0) * 2).abs().max().item() < 1e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(1024, 4096, 2048), (4096, 1024, 2048), (4096, 4096, 2048), (512, 384, 256)])
-def test_gemm_fused_bias_grad(C, M, N, K):
-    """bwd-weight GEMM with the bias gradient (column sums of dZ) fused: both outputs vs fp32 references."""
+@pytest.mark.parametrize("M,N,K,sk,tile", [(1024, 4096, 2048, None, None), (4096, 1024, 2048, None, None),
+                                            (4096, 4096, 2048, None, None), (512, 384, 256, None, None),
+                                            (1024, 4096, 8192, None, None), (1024, 1024, 2048, 4, (256, 256)),
+                                            (512, 768, 1024, 2, None)])
+def test_gemm_fused_bias_grad(C, M, N, K, sk, tile):
+    """bwd-weight GEMM with the bias gradient (column sums of dZ) fused: both outputs vs fp32 references.
+    With split-K (auto at 1024x4096, K 8192; forced otherwise) the per-split partial column sums are reduced
+    after the slabs."""
     torch.manual_seed(5)
     X = torch.randn(K, M, device=DEV).to(torch.bfloat16)   # activations [batch][in]
     dZ = torch.randn(K, N, device=DEV).to(torch.bfloat16)  # upstream grad [batch][out]
     dW = torch.empty(M, N, device=DEV)
     db = torch.full((N,), float("nan"), device=DEV)
-    G.linear_bwd_weight(X, dZ, dW, bias_grad=db)
+    G.gemm(X, True, dZ, False, dW, G.EPI_NONE, colsum=db, split_k=sk, tile=tile)
     assert (dW - X.float().t() @ dZ.float()).abs().max().item() < 0.25
     assert (db - dZ.float().sum(0)).abs().max().item() < 1e-2 * K ** 0.5
 
 
+@pytest.fixture(params=[False, True], ids=["oneloop", "staggered"])
+def main_loop(request, C):
+    """Both 256x256 main loops: the one-role loop and the staggered 4-phase loop (gemm_set_pingpong)."""
+    Cx = G._ext.require()
+    Cx.gemm_set_pingpong(request.param)
+    yield request.param
+    Cx.gemm_set_pingpong(False)
+
+
 @pytest.mark.parametrize("K", [64, 128, 192, 1024, 4096])
-def test_gemm_256_tile_all_layouts_and_k(C, K):
-    """The 256x256 ping-pong schedule (forced tile) on all four operand layouts, K-tile counts 1, 2, 3 and
+def test_gemm_256_tile_all_layouts_and_k(C, main_loop, K):
+    """The 256x256 main loops (forced tile) on all four operand layouts, K-tile counts 1, 2, 3 and
     long loops, with and without split-K: vs an fp64 reference."""
     torch.manual_seed(K)
     M, N = 512, 768
@@ -222,7 +236,7 @@ def test_gemm_256_tile_all_layouts_and_k(C, K):
                 assert err < tol, f"a_t={a_t} b_t={b_t} split_k={sk}: max err {err}"
 
 
-def test_gemm_256_tile_epilogues(C):
+def test_gemm_256_tile_epilogues(C, main_loop):
     torch.manual_seed(9)
     M, N, K = 512, 512, 768
     X = torch.randn(M, K, device=DEV).to(torch.bfloat16)

@@ -218,3 +218,41 @@ def test_gemm_wire_epilogue_encodes_fused_bias(codec, nsh):
         assert np.array_equal(got[s * sb:s * sb + hi - lo], exp[s * sb:s * sb + hi - lo]), f"shard {s} mantissas"
         e0 = s * sb + shard
         assert np.array_equal(got[e0:e0 + (hi - lo) // 16], exp[e0:e0 + (hi - lo) // 16]), f"shard {s} exponents"
+
+
+@pytest.mark.parametrize("codec", ["bfp_rne", "bfp_trunc"])
+@pytest.mark.parametrize("sk,tile", [(2, None), (4, (256, 256)), (2, (256, 256))])
+def test_gemm_wire_epilogue_splitk(codec, sk, tile):
+    """Split-K bwd-weight with the wire epilogue: the slab reduce encodes W and the fused bias gradient. Byte-
+    identical to packing the same split GEMM's f32 output (slabs summed in the same order)."""
+    cin, cout, mb, nsh = 1024, 1024, 1024, 3
+    torch.manual_seed(sk)
+    x = (torch.randn(mb, cin, device="cuda") * 0.5).to(torch.bfloat16)
+    dz = (torch.randn(mb, cout, device="cuda") * 0.1).to(torch.bfloat16)
+    n = cin * cout + cout
+    shard = ((n + nsh - 1) // nsh + 255) // 256 * 256
+    own = 1
+    grad = torch.full((shard * nsh,), 7.0, device="cuda")
+    buf = torch.zeros(nsh * wire.shard_bytes(codec, shard), dtype=torch.uint8, device="cuda")
+    G.gemm(x, True, dz, False, grad[: cin * cout].view(cin, cout), G.EPI_WIRE, colsum=grad[cin * cout:n],
+           wire=(buf, shard, own, wire.codec_id(codec)), split_k=sk, tile=tile)
+    ref = torch.empty(cin, cout, device="cuda")
+    G.gemm(x, True, dz, False, ref, G.EPI_NONE, split_k=sk, tile=tile)
+    torch.cuda.synchronize()
+    db = grad[cin * cout:n].cpu()
+    assert (db - dz.float().sum(0).cpu()).abs().max().item() < 1e-2 * mb ** 0.5
+    flat = np.zeros(shard * nsh, np.float32)
+    flat[: cin * cout] = ref.cpu().numpy().reshape(-1)
+    flat[cin * cout:n] = db.numpy()
+    exp = O.pack(flat, shard, codec)
+    got = buf.cpu().numpy()
+    sb = wire.shard_bytes(codec, shard)
+    for s in range(nsh):
+        lo, hi = s * shard, min((s + 1) * shard, n)
+        assert np.array_equal(got[s * sb:s * sb + hi - lo], exp[s * sb:s * sb + hi - lo]), f"shard {s} mantissas"
+        e0 = s * sb + shard
+        assert np.array_equal(got[e0:e0 + (hi - lo) // 16], exp[e0:e0 + (hi - lo) // 16]), f"shard {s} exponents"
+    gw = grad.cpu()
+    lo, hi = own * shard, min((own + 1) * shard, cin * cout)
+    assert torch.equal(gw[lo:hi], ref.cpu().reshape(-1)[lo:hi]), "owner shard f32"
+    assert torch.all(gw[: lo] == 7.0) and torch.all(gw[hi: cin * cout] == 7.0), "non-owner shards untouched"

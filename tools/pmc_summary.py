@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc counter_collection CSVs per kernel (mean over dispatches).
+
+Usage: python tools/pmc_summary.py gpurun_out/pmc1/p_counter_collection.csv [more.csv ...] [--filter gemm]
+Derived: effective clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel time), MFMA busy share, L2 hit rate.
+"""
+import argparse
+import collections
+import csv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv", nargs="+")
+    ap.add_argument("--filter", default="")
+    a = ap.parse_args()
+    agg = collections.OrderedDict()
+    for f in a.csv:
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            if a.filter and a.filter not in name:
+                continue
+            key = (name[:110], r["Grid_Size"])
+            d = agg.setdefault(key, {"_n": collections.Counter(), "_dur": []})
+            c = r["Counter_Name"]
+            d.setdefault(c, collections.defaultdict(float))
+            d[c][r["Dispatch_Id"]] += float(r["Counter_Value"])
+            d["_meta"] = (r["VGPR_Count"], r["Accum_VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"])
+            d.setdefault("_t", {})[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for (name, grid), d in agg.items():
+        m = {c: sum(v.values()) / len(v) for c, v in d.items() if not c.startswith("_")}
+        t_ns = sum(d["_t"].values()) / len(d["_t"])
+        print(f"{name}  grid={grid} vgpr/agpr/sgpr/lds={d['_meta']}  t={t_ns/1e3:.1f}us")
+        for c, v in sorted(m.items()):
+            print(f"    {c:28s} {v:16.0f}")
+        if "GRBM_GUI_ACTIVE" in m:
+            print(f"    eff_clock_GHz               {m['GRBM_GUI_ACTIVE'] / 8 / t_ns:16.3f}")
+        if "SQ_WAVE_CYCLES" in m and "SQ_VALU_MFMA_BUSY_CYCLES" in m and "SQ_BUSY_CYCLES" in m:
+            print(f"    mfma_busy/(busy*4simd*?)    {m['SQ_VALU_MFMA_BUSY_CYCLES'] / max(1, m['SQ_BUSY_CYCLES']):16.3f}")
+        if "SQ_WAVE_CYCLES" in m:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+                if c in m:
+                    print(f"    {c+'/WAVE':28s} {m[c] / m['SQ_WAVE_CYCLES']:16.3f}")
+        if "TCC_HIT_sum" in m:
+            print(f"    L2_hit                      {m['TCC_HIT_sum'] / max(1, m['TCC_HIT_sum'] + m['TCC_MISS_sum']):16.3f}")
+
+
+if __name__ == "__main__":
+    main()
