@@ -59,9 +59,10 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
         tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
         buf, shard, own, codec = wire
         sk = 0 if split_k is None else int(split_k)
-        bm, _bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
+        bm, bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
         if bm == 0:
             raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
+        tbm, tbn = bm, bn  # launch exactly the planned tile (re-planning with an explicit split_k differs)
         ws = _workspace(C.device, sk * (M * N + N)) if sk > 1 else None
         Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, tbm, tbn, colsum, tw, buf, int(shard),
                 int(own), int(codec))
@@ -85,6 +86,7 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
             bm, bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
             if bm == 0:
                 raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
+            tbm, tbn = bm, bn  # launch exactly the planned tile (re-planning with an explicit split_k differs)
             if sk > 1:
                 ws = _workspace(C.device, sk * (M * N + N))
         else:
