@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
     ap.add_argument("--set", default="mlp", choices=["mlp", "bert"])
     ap.add_argument("--ab", action="store_true", help="also time the one-role main loop (ping-pong off)")
+    ap.add_argument("--epi-arms", action="store_true",
+                    help="bwd-weight shapes: also time the fused bias-gradient (colsum) and BFP wire epilogues")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
@@ -126,7 +128,21 @@ def main():
         err = (C.float() - (ref().float() * ((aux > 0) if epi == G.EPI_RELU_MASK else 1))).abs().max().item()
         tm, tr, tmm, tone = [], [], [], []
         Cx = G._ext.require()
+        arms = {}
+        if a.epi_arms and a_t and not b_t and dt == torch.bfloat16:
+            from fpga_ai_nic_amd.ops import wire as W
+
+            cs = torch.empty(N, device="cuda")
+            shard = (M * N + N + 255) // 256 * 256
+            wbuf = torch.empty(W.shard_bytes("bfp_rne", shard), dtype=torch.uint8, device="cuda")
+            wt = (wbuf, shard, -1, W.codec_id("bfp_rne"))
+            arms = {"colsum": lambda: G.gemm(A, a_t, B, b_t, C, epi, colsum=cs),
+                    "wire": lambda: G.gemm(A, a_t, B, b_t, C, G.EPI_WIRE, wire=wt),
+                    "wire_colsum": lambda: G.gemm(A, a_t, B, b_t, C, G.EPI_WIRE, colsum=cs, wire=wt)}
+        tarm = {k: [] for k in arms}
         for _ in range(a.rounds):
+            for k, fn in arms.items():
+                tarm[k].append(time_fn(fn, a.iters))
             if a.ab:  # same plan with the one-role main loop (256x256 tiles only differ)
                 Cx.gemm_set_pingpong(False)
                 tone.append(time_fn(mine, a.iters))
@@ -143,7 +159,9 @@ def main():
                           "torch_fused_us": round(r, 2), "torch_matmul_only_us": round(rm, 2),
                           "torch_matmul_tflops": round(flop / rm / 1e6, 1), "speedup_vs_torch_fused": round(r / m, 3),
                           "max_abs_err": err,
-                          **({"oneloop_us": round(statistics.median(tone), 2)} if tone else {})}), flush=True)
+                          **({"oneloop_us": round(statistics.median(tone), 2)} if tone else {}),
+                          **({"epi_arms_us": {k: round(statistics.median(v), 2) for k, v in tarm.items()}}
+                             if arms else {})}), flush=True)
 
 
 if __name__ == "__main__":
