@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--graph", action="store_true",
                     help="capture one training step in a HIP graph and replay it (world 1, inline engine)")
+    ap.add_argument("--side-stream", action="store_true",
+                    help="world 1: run the engine's requests (BFP decode + fused SGD) on its high-priority side stream, "
+                         "overlapped with the following GEMMs, instead of inline on the compute stream")
     ap.add_argument("--force-dist", action="store_true",
                     help="world 1 through the full multi-rank path (1-rank RCCL group, side-stream engine)")
     a = ap.parse_args()
@@ -74,7 +77,8 @@ def main():
         transport = ThreadFabric(1).transport(0)
     kind = "local" if a.compress == "local" else a.compress
     engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings,
-                         force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python", comm=comm)
+                         force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python", comm=comm,
+                         side_stream=a.side_stream)
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
     if world > 1:
