@@ -70,6 +70,7 @@ def compile_flags(tinc, abi):
         f"-I{CSRC}", f"-I{py_inc}", "-I/opt/rocm/include",
     ]
     fl += [f"-I{d}" for d in tinc]
+    fl += os.environ.get("FAN_EXTRA_CFLAGS", "").split()  # e.g. -DFAN_GEMM_4WAVE (experimental kernel variants)
     return fl
 
 
