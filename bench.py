@@ -165,6 +165,7 @@ def main():
                 "grad_bytes_f32_per_step": grad_bytes,
                 "effective_allreduce_algo_bw_GBps": round(grad_bytes / (ms / 1e3) / 1e9, 2),
                 "final_loss": round(loss, 5),
+                **({"engine_counters": engine.counters()} if hasattr(engine, "counters") else {}),
             },
         }
         print(json.dumps(rec), flush=True)

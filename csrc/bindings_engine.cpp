@@ -205,6 +205,22 @@ void register_engine(pybind11::module_& m) {
       .def("latency_ms", &AllReduceEngine::latency_ms, py::call_guard<py::gil_scoped_release>())
       .def("set_timing", &AllReduceEngine::set_timing)
       .def("diagnostics", &AllReduceEngine::diagnostics)
+      .def("counters",
+           [](const AllReduceEngine& e) {
+             const EngineCounters& c = e.counters();
+             py::dict d;
+             d["requests"] = c.requests;
+             d["logical_bytes"] = c.logical_bytes;
+             d["wire_bytes"] = c.wire_bytes;
+             d["host_wait_s"] = c.host_wait_s;
+             d["host_waits"] = c.host_waits;
+             d["host_spins"] = c.host_spins;
+             d["device_ms"] = c.device_ms;
+             d["timed_requests"] = c.timed_requests;
+             return d;
+           },
+           "perf counters (the NIC's latency / host-stall registers): requests, bytes, host wait, device time")
+      .def("reset_counters", &AllReduceEngine::reset_counters)
       .def_property_readonly("requests", &AllReduceEngine::requests);
 }
 

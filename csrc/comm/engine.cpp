@@ -275,7 +275,11 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
     FAN_HIP_CHECK(hipStreamWaitEvent(stream_, sl.ready, 0));
   }
   sl.timed = timing_;
+  sl.counted = false;
   if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t0, sl.stream));
+  counters_.requests++;
+  counters_.logical_bytes += n_valid * 4;
+  counters_.wire_bytes += wire_bytes(L);
   if (prepacked) {
     FAN_CHECK(prepack_shape(n_valid)[0] > 0, "prepacked input needs the mesh algorithm and a BFP codec");
     FAN_CHECK(prepacked_elems % 16 == 0 && prepacked_elems <= L.n_pad, "bad prepacked_elems");
@@ -339,6 +343,18 @@ void AllReduceEngine::synchronize(int slot, double timeout_s) {
   const double t0 = now_s();
   const double tmo = timeout_s > 0 ? timeout_s : cfg_.timeout_s;
   int spins = 0;
+  struct WaitAccount {  // host stall accounting on every exit path (including the timeout throw)
+    EngineCounters& c;
+    const double t0;
+    const int& spins;
+    ~WaitAccount() {
+      if (spins > 0) {
+        c.host_waits++;
+        c.host_spins += (uint64_t)spins;
+        c.host_wait_s += now_s() - t0;
+      }
+    }
+  } account{counters_, t0, spins};
   while (!query(slot)) {
     if (++spins > 64) {
       std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 5));
@@ -361,6 +377,11 @@ float AllReduceEngine::latency_ms(int slot) {
   synchronize(slot);
   float ms = 0.f;
   FAN_HIP_CHECK(hipEventElapsedTime(&ms, sl.t0, sl.t1));
+  if (!sl.counted) {
+    sl.counted = true;
+    counters_.device_ms += ms;
+    counters_.timed_requests++;
+  }
   return ms;
 }
 

@@ -47,6 +47,19 @@ struct EngineLayout {
   int64_t part = 0;         // ring: padded elements per ring part
 };
 
+// Per-engine performance counters: the reference NIC's perf/debug registers re-expressed (hw/all_reduce.sv:92-98,
+// 892-1085: lpbk_latency active cycles, stall_host_in/out; sw/mlp_mpi_example_f32.cpp:100-112: the getters).
+struct EngineCounters {
+  uint64_t requests = 0;
+  int64_t logical_bytes = 0;   // fp32 gradient bytes requested (n_valid * 4)
+  int64_t wire_bytes = 0;      // bytes this rank sends over the fabric
+  double host_wait_s = 0.0;    // host time blocked in synchronize() (stall_host analogue)
+  uint64_t host_waits = 0;     // synchronize() calls that had to wait
+  uint64_t host_spins = 0;     // done-word polls while waiting
+  double device_ms = 0.0;      // summed device time of timed requests (lpbk_latency analogue)
+  uint64_t timed_requests = 0;
+};
+
 class AllReduceEngine {
  public:
   static constexpr int kSlots = 8;
@@ -82,6 +95,8 @@ class AllReduceEngine {
   void set_timing(bool on) { timing_ = on; }
   std::string diagnostics(int slot) const;
   uint64_t requests() const { return seq_; }
+  const EngineCounters& counters() const { return counters_; }
+  void reset_counters() { counters_ = EngineCounters{}; }
   int64_t wire_bytes(const EngineLayout& L) const;
 
  private:
@@ -90,6 +105,7 @@ class AllReduceEngine {
     uint32_t seq = 0;
     bool pending = false;   // epilogue not yet committed
     bool timed = false;
+    bool counted = false;   // device time already added to counters_
     hipStream_t stream = nullptr;  // stream the request runs on (comm stream, or the producer when inline)
     std::vector<std::function<void()>> thunks;
     double t_issue = 0.0;
@@ -117,6 +133,7 @@ class AllReduceEngine {
   uint32_t seq_ = 0;
   int next_slot_ = 0;
   bool timing_ = false;
+  EngineCounters counters_;
   std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
 };
 

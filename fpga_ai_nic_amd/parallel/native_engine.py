@@ -204,5 +204,14 @@ class NativeAllReduce:
     def diagnostics(self, h: NativeHandle) -> str:
         return self.C.diagnostics(h.slot)
 
+    def counters(self) -> dict:
+        """Engine perf counters (reference: the NIC's lpbk_latency / stall_host registers read by
+        get_all_reduce_latency / get_host_stall_cycles, sw/mlp_mpi_example_f32.cpp:100-112): requests, logical and
+        wire bytes, host time blocked in synchronize(), summed device time of timed requests."""
+        return dict(self.C.counters())
+
+    def reset_counters(self):
+        self.C.reset_counters()
+
 
 __all__ = ["NativeAllReduce", "NativeHandle", "NUM_SLOTS"]

@@ -152,3 +152,26 @@ def test_mlp_mpi_cli_native_engine_gpu():
     text = out.getvalue()
     assert "PERFDUMP,BP," in text and "SAMPLES/S" in text
     assert np.isfinite(res["loss"])
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_engine_perf_counters(force):
+    """Perf counters (the NIC's latency / host-stall registers): requests, logical / wire bytes, host wait time
+    and summed device time of timed requests."""
+    eng = NativeAllReduce(_native_transport() if force else None, codec="bfp_rne", force_comm=force)
+    eng.reset_counters()
+    eng.timing = True
+    n = 1 << 20
+    L = eng.layout(n)
+    grad = torch.randn(L.n_pad, device="cuda")
+    w = torch.zeros(L.n_pad, device="cuda")
+    hs = [eng.allreduce_sgd(grad, w, n_valid=n, lr=0.1) for _ in range(3)]
+    for h in hs:
+        h.synchronize(30)
+        assert h.latency_ms() is not None and h.latency_ms() > 0
+    c = eng.counters()
+    assert c["requests"] == 3
+    assert c["logical_bytes"] == 3 * n * 4
+    assert c["wire_bytes"] == 3 * eng.wire_bytes(L)
+    assert c["timed_requests"] == 3 and c["device_ms"] > 0
+    assert c["host_wait_s"] >= 0 and c["host_waits"] <= 3
