@@ -36,6 +36,18 @@ def mlp_shapes(mb: int):
 MLP_SHAPES = mlp_shapes(2048)
 
 
+def ref_shapes(mb: int = 5376, c: int = 2048):
+    """The reference run.sh workload (10 x 2048^2 f32 FC layers, MB 5376): one layer's three GEMMs, plus the
+    same products with every operand K-contiguous (what a transposed-weight path would run)."""
+    return [
+        ("ref_fwd", mb, c, c, False, False, G.EPI_NONE),
+        ("ref_bwdd", mb, c, c, False, True, G.EPI_NONE),
+        ("ref_bwdw", c, c, mb, True, False, G.EPI_NONE),
+        ("ref_fwd_kk", mb, c, c, False, True, G.EPI_NONE),
+        ("ref_bwdw_kk", c, c, mb, False, True, G.EPI_NONE),
+    ]
+
+
 def bert_shapes(tokens: int):
     """BERT-base encoder-layer backward GEMMs (BASELINE config 5) at ``tokens`` rows per GPU."""
     import sys as _s
@@ -64,18 +76,18 @@ def main():
     ap.add_argument("--shapes", default="")
     ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
     ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
-    ap.add_argument("--set", default="mlp", choices=["mlp", "bert"])
+    ap.add_argument("--set", default="mlp", choices=["mlp", "bert", "ref"])
     ap.add_argument("--ab", action="store_true", help="also time the one-role main loop (ping-pong off)")
     ap.add_argument("--epi-arms", action="store_true",
                     help="bwd-weight shapes: also time the fused bias-gradient (colsum) and BFP wire epilogues")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
-    shapes = mlp_shapes(a.mb) if a.set == "mlp" else bert_shapes(a.mb)
+    shapes = mlp_shapes(a.mb) if a.set == "mlp" else bert_shapes(a.mb) if a.set == "bert" else ref_shapes()
     for name, M, N, K, a_t, b_t, epi in shapes:
         if a.shapes and name not in a.shapes.split(","):
             continue
-        if a.dtype == "f32" and K > 4096:
+        if a.dtype == "f32" and K > 8192:
             continue
         A = (torch.rand(K, M, device="cuda") * 2 - 1).to(dt) if a_t else (torch.rand(M, K, device="cuda") * 2 - 1).to(dt)
         B = (torch.rand(N, K, device="cuda") * 2 - 1).to(dt) if b_t else (torch.rand(K, N, device="cuda") * 2 - 1).to(dt)

@@ -1,12 +1,14 @@
 // fp32 MFMA GEMM for gfx950 (v_mfma_f32_16x16x4_f32: exact f32 fma chain, no xf32 on CDNA4).
 //
 // Serves the reference-equivalent f32 MLP (sw/mlp_mpi_example_f32.cpp: libxsmm fc fwd/bwd in f32).
-// Block tile 128x128x32, 4 waves (2x2), each wave 64x64 = 4x4 tiles of 16x16.
-// LDS image for BOTH operands is [outer][k] (128-B rows of 32 f32), 16-B chunk c of row r stored at
-// c ^ ((r>>1)&7). K-contiguous operands are staged with global_load_lds_dwordx4 (swizzle on the
-// source address); MN-contiguous operands are register-staged and transposed on the LDS write.
-// Within each 16-wide k chunk lane l feeds k = 4*(l>>4) + i to MFMA i (a consistent permutation of
-// the k order for A and B), so every fragment read is one ds_read_b128.
+// Block tile 128x128x32, 4 waves (2x2), each wave 64x64 = 4x4 tiles of 16x16. Both operands are staged with
+// global_load_lds_dwordx4 (no VGPR round trip, no synchronous register staging), swizzle on the source address:
+//   * K-contiguous operand: LDS image [outer][k] (128-B rows of 32 f32), 16-B chunk c of row r at c ^ ((r>>1)&7);
+//     a fragment is one ds_read_b128;
+//   * MN-contiguous operand: LDS image [k][outer] (512-B rows of 128 f32), 16-float block b of row k at
+//     b ^ ((k>>2)&3); a fragment is 4 ds_read_b32 (lanes of the 4 k-row groups hit 4 disjoint bank quarters).
+// Within each 16-wide k chunk lane l feeds k = 4*(l>>4) + i to MFMA i (a consistent permutation of the k order
+// for A and B).
 #include "gemm/gemm.h"
 #include "gemm/glds.h"
 
@@ -27,42 +29,36 @@ template <bool KCONTIG>
 __device__ __forceinline__ void stage(const float* __restrict__ g, int64_t ld, int o0, int k0, char* tile, int wave,
                                       int lane) {
   const int t = wave * 64 + lane;
-  if (KCONTIG) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 4; ++i) {
+    const float* src;
+    if (KCONTIG) {
       const int row = i * 32 + (t >> 3);
-      const int cs = t & 7;
-      const int c = cs ^ swz(row);
-      const float* src = g + (int64_t)(o0 + row) * ld + k0 + c * 4;
-      glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(tile + i * 4096 + wave * 1024)));
-    }
-  } else {
-    float4 v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      const int c = (t & 7) ^ swz(row);
+      src = g + (int64_t)(o0 + row) * ld + k0 + c * 4;
+    } else {
       const int krow = i * 8 + (t >> 5);
-      const int oc = (t & 31) * 4;
-      v[i] = *reinterpret_cast<const float4*>(g + (int64_t)(k0 + krow) * ld + o0 + oc);
+      const int col = ((t & 31) * 4) ^ (((krow >> 2) & 3) << 4);
+      src = g + (int64_t)(k0 + krow) * ld + o0 + col;
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int krow = i * 8 + (t >> 5);
-      const int oc = (t & 31) * 4;
-      const float vv[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int o = oc + u;
-        const int off = o * 128 + (((krow >> 2) ^ swz(o)) << 4) + (krow & 3) * 4;
-        *reinterpret_cast<float*>(tile + off) = vv[u];
-      }
-    }
+    glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(tile + i * 4096 + wave * 1024)));
   }
 }
 
+template <bool KCONTIG>
 __device__ __forceinline__ f32x4 frag(const char* tile, int o, int kc, int lane) {
-  const int row = o + (lane & 15);
-  const int c = kc * 4 + (lane >> 4);
-  return *reinterpret_cast<const f32x4*>(tile + row * 128 + ((c ^ swz(row)) << 4));
+  if (KCONTIG) {
+    const int row = o + (lane & 15);
+    const int c = kc * 4 + (lane >> 4);
+    return *reinterpret_cast<const f32x4*>(tile + row * 128 + ((c ^ swz(row)) << 4));
+  } else {
+    const int k0 = kc * 16 + 4 * (lane >> 4);
+    const int col = (o + (lane & 15)) ^ ((lane >> 4) << 4);  // (k >> 2) & 3 == lane >> 4 for k0..k0+3
+    f32x4 r;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = *reinterpret_cast<const float*>(tile + (k0 + u) * 512 + col * 4);
+    return r;
+  }
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -110,9 +106,9 @@ __global__ void __launch_bounds__(NT, 2)
     for (int kc = 0; kc < 2; ++kc) {
       f32x4 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag(sa, wm * 64 + i * 16, kc, lane);
+      for (int i = 0; i < 4; ++i) af[i] = frag<AK>(sa, wm * 64 + i * 16, kc, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag(sb, wn * 64 + j * 16, kc, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(sb, wn * 64 + j * 16, kc, lane);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
