@@ -152,6 +152,11 @@ def run(argv=None, out=sys.stdout):
             print(f"ALLREDUCE: algo={engine.algo} codec={engine.codec} rings={engine.rings} "
                   f"wire_bytes/step={engine.stats['wire_bytes'] / max(1, engine.stats['requests']) * model.L:.4g}",
                   file=out)
+            if cfg.profile and hasattr(engine, "counters"):
+                # the NIC's host-stall register (get_host_stall_cycles, sw/mlp_mpi_example_f32.cpp:108-112)
+                c = engine.counters()
+                print(f"ALLREDUCE host wait = {c['host_wait_s'] / max(1, cfg.iters):.6g} s/iter "
+                      f"({c['host_waits']} blocking waits, {c['requests']} requests)", file=out)
     if a.dump_norms and rank == world - 1:  # the reference prints from the last rank
         for i, l in enumerate(model.layers):
             print(f"L1 of layer's {i} dweights after training : {float(l.gw.double().abs().sum()):.25g}", file=out)

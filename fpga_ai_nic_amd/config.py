@@ -33,7 +33,7 @@ class TrainConfig:
     rings: int = 1
     slice_elems: int = 1 << 22
     transport: str = "torch"       # torch | native | p2p
-    engine: str = "python"         # python | native
+    engine: str = "native"         # native (C++ engine, GPU) | python; CPU runs always use python
     compat_owner_fp32: bool = False
     lr: float = 0.1
     momentum: float = 0.0
