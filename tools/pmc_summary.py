@@ -2,7 +2,8 @@
 """Summarise rocprofv3 --pmc counter_collection CSVs per kernel (mean over dispatches).
 
 Usage: python tools/pmc_summary.py gpurun_out/pmc1/p_counter_collection.csv [more.csv ...] [--filter gemm]
-Derived: effective clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel time), MFMA busy share, L2 hit rate.
+Derived: effective clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel time; meaningless below ~0.3 ms), MFMA busy share,
+L2 hit rate, FETCH/WRITE bandwidth (GB/s over the dispatch; counters from separate passes are averaged per kernel).
 """
 import argparse
 import collections
@@ -24,9 +25,9 @@ def main():
             d = agg.setdefault(key, {"_n": collections.Counter(), "_dur": []})
             c = r["Counter_Name"]
             d.setdefault(c, collections.defaultdict(float))
-            d[c][r["Dispatch_Id"]] += float(r["Counter_Value"])
+            d[c][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])  # per pass: dispatch ids restart
             d["_meta"] = (r["VGPR_Count"], r["Accum_VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"])
-            d.setdefault("_t", {})[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            d.setdefault("_t", {})[(f, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     for (name, grid), d in agg.items():
         m = {c: sum(v.values()) / len(v) for c, v in d.items() if not c.startswith("_")}
         t_ns = sum(d["_t"].values()) / len(d["_t"])
@@ -41,8 +42,11 @@ def main():
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
                 if c in m:
                     print(f"    {c+'/WAVE':28s} {m[c] / m['SQ_WAVE_CYCLES']:16.3f}")
-        if "TCC_HIT_sum" in m:
+        if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m:
             print(f"    L2_hit                      {m['TCC_HIT_sum'] / max(1, m['TCC_HIT_sum'] + m['TCC_MISS_sum']):16.3f}")
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):  # KiB per dispatch -> GB/s over the dispatch
+            if c in m:
+                print(f"    {c + '_GBps':28s} {m[c] * 1024 / t_ns:16.1f}")
 
 
 if __name__ == "__main__":
