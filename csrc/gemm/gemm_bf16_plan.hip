@@ -24,9 +24,35 @@ std::atomic<bool>& gemm_pingpong_flag() {
   return flag;
 }
 
+// Measured plans for shapes where the heuristic below is not the fastest (bench/gemm_bench.py --sweep on MI355X,
+// profiles/r1_gemm_bert_sweep.jsonl): the BERT-base encoder-layer backward GEMMs at 4096 tokens (BASELINE config
+// 5). Under-filled grids there favour the big tile (and a split-K that keeps one round of workgroups) over
+// "at least one workgroup per CU".
+struct TunedPlan {
+  int M, N, K, bm, bn, sk;
+};
+static constexpr TunedPlan kTuned[] = {
+    {4096, 3072, 768, 256, 256, 1},   // ffn_out dgrad: 29.4 us vs 34.4 (128x256)
+    {3072, 768, 4096, 256, 256, 4},   // ffn_out wgrad: 42.2 us vs 50.5 (128x128)
+    {768, 3072, 4096, 256, 256, 4},   // ffn_in wgrad: 42.2 us vs 51.0 (128x128)
+    {768, 768, 4096, 128, 128, 4},    // attn_out wgrad: 23.2 us vs 28.2 (split 8)
+    {768, 2304, 4096, 128, 256, 4},   // qkv wgrad: 32.6 us vs 38.6 (128x128 split 4)
+};
+
 GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn, int tile_waves) {
   GemmPlan p{0, 0, 1, 8};
   if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % BK) return p;
+  if (tile_bm == 0 && split_k <= 0) {
+    for (const TunedPlan& t : kTuned) {
+      if (t.M == M && t.N == N && t.K == K && K % (BK * t.sk) == 0) {
+        p.bm = t.bm;
+        p.bn = t.bn;
+        p.split_k = t.sk;
+        p.waves = kDefaultWaves;
+        return p;
+      }
+    }
+  }
   // Measured on MI355X (bench/gemm_bench.py --sweep, MLP shapes + 4k/8k squares): take the largest tile
   // that still gives >= one workgroup per CU (256), preferring 128x256 over 256x128; split K only when
   // even 128x128 tiles leave more than half the CUs idle (split-K costs an f32 slab round trip).
