@@ -15,6 +15,20 @@
 
 namespace fan {
 
+// Upper bound on the workgroups of one wire kernel (env FAN_WIRE_MAX_BLOCKS, default 2048): these memory-bound
+// kernels run on the comm stream beside the GEMMs at world > 1, and every CU they occupy cannot host a GEMM
+// workgroup (profiles/r1_gemm_cu_contention_probe.txt), so the footprint is a tunable. Measured at world 1 through
+// the multi-rank path: capping it at 512 / 128 / 64 made the step 0.4 / 4 / 11 % slower
+// (profiles/r1_wire_grid_cap_ab.txt) — the kernels are on the critical path more than they crowd the GEMMs.
+static int wire_max_blocks() {
+  static const int v = [] {
+    const char* e = getenv("FAN_WIRE_MAX_BLOCKS");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : 2048;
+  }();
+  return v;
+}
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -162,7 +176,7 @@ void launch_wire_pack(int codec, int in_dtype, const void* in, void* out, size_t
                       hipStream_t stream) {
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock);
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (in_dtype == kF32)
       hipLaunchKernelGGL((wire_pack_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in, (uint8_t*)out,
@@ -179,7 +193,7 @@ void launch_wire_pack_range(int codec, int in_dtype, const void* in, void* out, 
   check_ns(n_s);
   FAN_CHECK(begin % 16 == 0 && end % 16 == 0 && begin <= end, "pack_range: bounds must be multiples of 16");
   if (end == begin) return;
-  const int grid = stream_grid((end - begin) / 8, kBlock);
+  const int grid = stream_grid((end - begin) / 8, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (in_dtype == kF32)
       hipLaunchKernelGGL((wire_pack_range_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in,
@@ -195,7 +209,7 @@ void launch_wire_unpack(int codec, int out_dtype, const void* in, void* out, siz
                         hipStream_t stream) {
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock);
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (out_dtype == kF32)
       hipLaunchKernelGGL((wire_unpack_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)in, (float*)out,
@@ -210,7 +224,7 @@ void launch_wire_unpack(int codec, int out_dtype, const void* in, void* out, siz
 template <typename TL, int C>
 static void reduce_dispatch(const void* slots, size_t slot_stride, int n_slots, int self_pos, const void* local,
                             void* out_wire, float* out_f32, size_t n_s, hipStream_t stream) {
-  const int grid = stream_grid(n_s / 8, kBlock);
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
   const uint8_t* sl = (const uint8_t*)slots;
   const TL* lo = (const TL*)local;
   uint8_t* ow = (uint8_t*)out_wire;
@@ -250,7 +264,7 @@ void launch_wire_sgd(int codec, const void* wire, size_t n_s, int n_shards, int 
   if (skip_period < 1) skip_period = 1 << 30;
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock);
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
   const uint8_t* w = (const uint8_t*)wire;
   FAN_CODEC_SWITCH(codec, {
     if (lp && mom)
