@@ -69,3 +69,28 @@ def test_geometry():
     assert sl % 256 == 0 and n_pad == blocks * 3 * sl and n_pad >= 1000
     n, sl, blocks, n_pad = A.ring_geometry(25_000_000, 8, 1 << 22)
     assert blocks == 1 and n_pad - 25_000_000 < 8 * 256
+
+
+def test_gemm_plans_for_workload_shapes():
+    """bf16 GEMM tile / split-K plans (host code, CPU): the MLP flagship shapes at minibatch 8192 and the measured
+    table for the BERT-base backward shapes (profiles/r1_gemm_bert_sweep.jsonl)."""
+    if not _ext.available():
+        pytest.skip("native extension not built")
+    C = _ext.require()
+    expect = {
+        (8192, 4096, 4096): (256, 256, 1),   # fwd1 / bwd-data 1: 512 tiles
+        (8192, 1024, 4096): (128, 256, 1),   # fwd2: 256 tiles
+        (4096, 4096, 8192): (256, 256, 1),   # bwd-weight 1
+        (4096, 1024, 8192): (256, 256, 4),   # bwd-weight 2: 64 tiles x split 4
+        (1024, 4096, 8192): (256, 256, 4),   # bwd-weight 0
+        (4096, 3072, 768): (256, 256, 1),    # BERT ffn_out dgrad (table)
+        (3072, 768, 4096): (256, 256, 4),    # BERT ffn_out wgrad (table)
+        (768, 768, 4096): (128, 128, 4),     # BERT attn_out wgrad (table)
+        (768, 2304, 4096): (128, 256, 4),    # BERT qkv wgrad (table)
+    }
+    for (M, N, K), (bm, bn, sk) in expect.items():
+        p = C.gemm_plan(M, N, K)
+        assert (p[0], p[1], p[2]) == (bm, bn, sk), f"{M}x{N}x{K}: {p}"
+        # re-planning with the resolved tile and split is the identity (what ops/gemm.py launches)
+        assert tuple(C.gemm_plan(M, N, K, p[2], p[0], p[1])[:3]) == (bm, bn, sk)
+    assert C.gemm_plan(100, 128, 64)[0] == 0  # unsupported: M % 128
