@@ -1,4 +1,5 @@
 #!/bin/bash
+# Component benches on one GPU: all-reduce codec throughput, BERT overlap, GEMMs vs hipBLASLt.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

@@ -1,4 +1,5 @@
 #!/bin/bash
+# GEMM kernel tests + GEMM bench vs hipBLASLt (rebuilds the extension first if a source is newer).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
