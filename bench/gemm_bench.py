@@ -120,7 +120,7 @@ def main():
         if a.sweep and dt == torch.bfloat16:
             res = {}
             for tile in ((256, 256), (256, 128), (128, 256), (128, 128)):
-                for waves in (8,):
+                for waves in (8, 4):
                     for sk in (1, 2, 3, 4, 6, 8):
                         if M % tile[0] or N % tile[1] or K % (64 * sk):
                             continue
