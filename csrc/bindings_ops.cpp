@@ -155,6 +155,10 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_supported", &gemm_supported);
   m.def("gemm_set_pingpong", [](bool on) { gemm_pingpong_flag().store(on); },
         "256x256 GEMM tiles: ping-pong main loop (default) or the one-role loop");
+  m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {
+          gemm_set_stamp_buffer(t ? t->data_ptr() : nullptr);
+        },
+        "diagnostic builds only: int64 GPU buffer [8 wg][8 waves][64 K-tiles][5] for the GEMM loop's s_memtime stamps");
   m.def("gemm_plan", &gemm_plan, "bf16 GEMM tile/split-K plan (bm, bn, split_k, waves); bm == 0: unsupported",
         pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0,
         pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0, pybind11::arg("tile_waves") = 0);

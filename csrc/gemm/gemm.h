@@ -64,6 +64,9 @@ void launch_gemm_bf16(const GemmArgs& a, hipStream_t stream);
 
 // 256x256 tiles: staggered 4-phase main loop (true; env FAN_GEMM_PP=1 starts with true) or the one-role loop.
 std::atomic<bool>& gemm_pingpong_flag();
+// diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
+void gemm_set_stamp_buffer(void* p);
+void* gemm_stamp_buffer();
 
 bool gemm_f32_supported(const GemmArgs& a);
 void launch_gemm_f32(const GemmArgs& a, hipStream_t stream);

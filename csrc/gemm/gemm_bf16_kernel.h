@@ -38,6 +38,18 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4_t;
 constexpr int BK = 64;
 constexpr int kDefaultWaves = 8;
 
+#ifdef FAN_GEMM_STAMPS
+// Diagnostic build only (FAN_EXTRA_CFLAGS=-DFAN_GEMM_STAMPS): s_memtime stamps of the one-role loop for the first
+// kStampWG workgroups, [wg][wave][kt][point] with points 0 loop top, 1 after vmcnt, 2 after barrier, 3 after the
+// DMA issue, 4 after the fragment reads are issued. Never in a production build.
+constexpr int kStampWG = 8, kStampKT = 64, kStampPts = 5;
+#define FAN_STAMP(pt)                                                                                        \
+  if (wo.stamps && blockIdx.x < kStampWG && kt < kStampKT && lane == 0)                                       \
+  wo.stamps[(((size_t)blockIdx.x * 8 + wave) * kStampKT + kt) * kStampPts + (pt)] = __builtin_amdgcn_s_memtime()
+#else
+#define FAN_STAMP(pt)
+#endif
+
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
 template <int OUTER, int NT>
@@ -183,6 +195,9 @@ struct WireOut {
   int codec;      // kBfpTrunc / kBfpRne
   float inv_shard;  // 1 / shard (shard index without a 64-bit integer division)
   int bias_off;     // > 0: flat offset of the bias segment, encoded from the fused column sum
+#ifdef FAN_GEMM_STAMPS
+  unsigned long long* stamps;  // diagnostic builds: s_memtime stamp buffer (see FAN_STAMP)
+#endif
 };
 
 // flat index -> (shard, position); f < 2^31, shard >= 256: the float estimate is off by at most one
@@ -323,7 +338,8 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
 }
 
 // 8 waves (2 per SIMD) or 4 waves (1 per SIMD, up to 512 VGPR+AGPR per lane: large per-wave tiles).
-template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
+template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT,
+          bool DMA1 = false>
 __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
     gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                      TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
@@ -391,18 +407,34 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
   }
 
   for (int kt = 0; kt < nk; ++kt) {
+    FAN_STAMP(0);
     // retire stage kt (this wave's DMA), leaving the younger stages in flight
     if (S == 3 && kt + 1 < nk) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    FAN_STAMP(1);
     __builtin_amdgcn_s_barrier();  // every wave retired stage kt and finished computing kt-1
-    if (kt + S - 1 < nk) {
-      char* st = smem + ((kt + S - 1) % S) * STAGE;
-      stage_tile<AK, BM, NT>(A, lda, m0, kbeg + (kt + S - 1) * BK, st, wave, lane);
-      stage_tile<BKC, BN, NT>(B, ldb, n0, kbeg + (kt + S - 1) * BK, st + A_BYTES, wave, lane);
+    FAN_STAMP(2);
+    const bool pf = kt + S - 1 < nk;
+    char* pst = smem + ((kt + S - 1) % S) * STAGE;
+    const int pk = kbeg + (kt + S - 1) * BK;
+    if constexpr (DMA1 && S == 2 && NT == 512) {
+      // DMA by waves 0..3 only (one per SIMD; waves w and w+4 share a SIMD): their partners go straight to the
+      // fragment reads and MFMAs while the CU's load path drains the 64 KB stage burst. Measured in one process
+      // (profiles/r1_gemm_dma_one_wave_ab.jsonl): bwd-weight layout (both operands MN-contiguous, 48 transposing
+      // fragment reads per wave and K-tile) 3-10 % faster; with a K-contiguous A 12-25 % slower, so only the
+      // bwd-weight layout uses it (launch_main).
+      if (pf && wave < 4) {
+        stage_tile<AK, BM, 256>(A, lda, m0, pk, pst, wave, lane);
+        stage_tile<BKC, BN, 256>(B, ldb, n0, pk, pst + A_BYTES, wave, lane);
+      }
+    } else if (pf) {
+      stage_tile<AK, BM, NT>(A, lda, m0, pk, pst, wave, lane);
+      stage_tile<BKC, BN, NT>(B, ldb, n0, pk, pst + A_BYTES, wave, lane);
     }
+    FAN_STAMP(3);
     const char* sa = smem + (kt % S) * STAGE;
     const char* sb = sa + A_BYTES;
     if constexpr (DBL) {
@@ -420,6 +452,7 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
           for (int j = 0; j < NJ; ++j) cs[j] += frag_sum(bfr[ks][j]);
         }
       }
+      FAN_STAMP(4);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         __builtin_amdgcn_s_setprio(1);
@@ -760,7 +793,7 @@ void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     }
   }
   constexpr int lds = lds_bytes<BM, BN>();
-  auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, SPLIT>;
+  auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, SPLIT, !AK && !BKC>;
   FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
                      a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
@@ -771,7 +804,11 @@ template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename T
 void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_codec,
                    a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
-                   a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0};
+                   a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0
+#ifdef FAN_GEMM_STAMPS
+                   , (unsigned long long*)gemm_stamp_buffer()
+#endif
+  };
   if (sk > 1) {
     // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + k*N]), then an ordered reduce that
     // applies the epilogue (deterministic: slabs summed in split order)

@@ -4,6 +4,17 @@
 
 namespace fan {
 
+static std::atomic<void*> g_stamp_buffer{nullptr};
+void* gemm_stamp_buffer() { return g_stamp_buffer.load(std::memory_order_relaxed); }
+void gemm_set_stamp_buffer(void* p) {
+#ifdef FAN_GEMM_STAMPS
+  g_stamp_buffer.store(p);
+#else
+  (void)p;
+  FAN_CHECK(false, "built without FAN_GEMM_STAMPS");
+#endif
+}
+
 using gemm_detail::BK;
 using gemm_detail::kDefaultWaves;
 using gemm_detail::launch_tile;
