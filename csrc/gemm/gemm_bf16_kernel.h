@@ -793,6 +793,10 @@ void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     }
   }
   constexpr int lds = lds_bytes<BM, BN>();
+  // bwd-weight layout (both operands MN-contiguous): next stage's DMA by one wave per SIMD; the other layouts issue
+  // it from every wave right after the barrier. (Issuing it between the two k-steps' MFMA clusters made fwd1 5 %
+  // faster in isolation but the flagship step 3 % slower, same box: profiles/r1_gemm_dma_position_layout_ab.jsonl,
+  // r1_gemm_dma_position_flagship_ab.log.)
   auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, SPLIT, !AK && !BKC>;
   FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
