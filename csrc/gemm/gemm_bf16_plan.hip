@@ -2,6 +2,9 @@
 // instantiated in its own translation unit (gemm_bf16_l*.hip) so the ~200 kernels build in parallel.
 #include "gemm/gemm_bf16_kernel.h"
 
+#include <cstdio>
+#include <vector>
+
 namespace fan {
 
 static std::atomic<void*> g_stamp_buffer{nullptr};
@@ -50,10 +53,47 @@ static constexpr TunedPlan kTuned[] = {
     {768, 2304, 4096, 128, 256, 4},   // qkv wgrad: 32.6 us vs 38.6 (128x128 split 4)
 };
 
+// Plan overrides from the environment, for in-step A/B of tile choices without a rebuild:
+// FAN_GEMM_PLAN="MxNxK=bm,bn,sk;MxNxK=bm,bn,sk". Parsed once; a malformed value raises on every plan.
+struct EnvPlans {
+  std::vector<TunedPlan> plans;
+  bool bad = false;
+};
+static const EnvPlans& env_plans() {
+  static const EnvPlans ep = [] {
+    EnvPlans r;
+    const char* e = getenv("FAN_GEMM_PLAN");
+    for (const char* q = e; q && *q;) {
+      TunedPlan t{};
+      int used = 0;
+      if (sscanf(q, "%dx%dx%d=%d,%d,%d%n", &t.M, &t.N, &t.K, &t.bm, &t.bn, &t.sk, &used) != 6 ||
+          (t.bm != 128 && t.bm != 256) || (t.bn != 128 && t.bn != 256) || t.sk < 1) {
+        r.bad = true;
+        break;
+      }
+      r.plans.push_back(t);
+      q += used;
+      if (*q == ';') ++q;
+    }
+    return r;
+  }();
+  FAN_CHECK(!ep.bad, "FAN_GEMM_PLAN: expected MxNxK=bm,bn,sk[;...] with bm, bn in {128, 256}");
+  return ep;
+}
+
 GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn, int tile_waves) {
   GemmPlan p{0, 0, 1, 8};
   if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % BK) return p;
   if (tile_bm == 0 && split_k <= 0) {
+    for (const TunedPlan& t : env_plans().plans) {
+      if (t.M == M && t.N == N && t.K == K && M % t.bm == 0 && N % t.bn == 0 && K % (BK * t.sk) == 0) {
+        p.bm = t.bm;
+        p.bn = t.bn;
+        p.split_k = t.sk;
+        p.waves = kDefaultWaves;
+        return p;
+      }
+    }
     for (const TunedPlan& t : kTuned) {
       if (t.M == M && t.N == N && t.K == K && K % (BK * t.sk) == 0) {
         p.bm = t.bm;

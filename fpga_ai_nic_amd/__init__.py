@@ -13,4 +13,7 @@ all-reduce and applies SGD on the NIC), re-designed for AMD Instinct MI355X (gfx
 """
 __version__ = "0.1.0"
 
+import torch  # noqa: F401  (before any import of _C.so: a C++ exception raised by _C with torch's Python module
+#                            not yet initialised corrupted the heap at interpreter exit)
+
 from . import _ext  # noqa: F401

@@ -94,3 +94,24 @@ def test_gemm_plans_for_workload_shapes():
         # re-planning with the resolved tile and split is the identity (what ops/gemm.py launches)
         assert tuple(C.gemm_plan(M, N, K, p[2], p[0], p[1])[:3]) == (bm, bn, sk)
     assert C.gemm_plan(100, 128, 64)[0] == 0  # unsupported: M % 128
+
+
+def test_gemm_plan_env_override():
+    """FAN_GEMM_PLAN overrides the planned tile / split for listed shapes (in-step A/B without a rebuild);
+    a malformed value raises instead of being ignored. Runs in a subprocess (the env is read once)."""
+    import os
+    import subprocess
+    import sys
+
+    if not _ext.available():
+        pytest.skip("native extension not built")
+    code = ("import fpga_ai_nic_amd._ext as E; C = E.require(); "
+            "print(C.gemm_plan(8192, 4096, 1024)[:3], C.gemm_plan(1024, 4096, 8192)[:3], "
+            "C.gemm_plan(8192, 4096, 4096)[:3])")
+    env = dict(os.environ, FAN_GEMM_PLAN="8192x4096x1024=128,256,1;1024x4096x8192=256,256,2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split("\n")[-2] == "(128, 256, 1) (256, 256, 2) (256, 256, 1)"
+    env["FAN_GEMM_PLAN"] = "8192x4096x1024=96,256,1"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "FAN_GEMM_PLAN" in r.stderr
