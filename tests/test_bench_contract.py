@@ -1,0 +1,53 @@
+"""bench.py driver contract, rehearsed on CPU: the same script the round-end scaling run launches under
+torch.distributed.run (one rank per GPU over RCCL) runs here with gloo ranks, and rank 0 alone prints ONE JSON
+line whose fields match the contract (whole-job value, weak scaling, dp<N>, steps / warmup echoed)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_json_contract(world, tmp_path):
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+            "--mb-per-gpu", "16"]
+    if world > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout  # rank 0 only, one line
+    rec = recs[0]
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in rec, k
+    assert rec["n_gpus"] == world and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["scaling"] == "weak" and rec["higher_is_better"] is True and rec["dtype"] == "bf16"
+    cfg = rec["config"]
+    assert cfg["model"] == "mlp-1024-4096-4096-1024" and cfg["parallelism"] == f"dp{world}"
+    assert cfg["global_batch"] == 16 * world
+    # value is the whole-job aggregate: global batch x steps / (max-over-ranks) elapsed time
+    assert rec["value"] == pytest.approx(cfg["global_batch"] / (rec["ms_per_step"] / 1e3), rel=1e-2)
+    assert rec["extra"]["final_loss"] > 0
