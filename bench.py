@@ -59,6 +59,9 @@ def main():
                          "overlapped with the following GEMMs, instead of inline on the compute stream")
     ap.add_argument("--force-dist", action="store_true",
                     help="world 1 through the full multi-rank path (1-rank RCCL group, side-stream engine)")
+    ap.add_argument("--epi", default="comm", choices=["comm", "producer"],
+                    help="side-stream engine: run each request's decode+SGD epilogue on the comm stream (overlapped "
+                         "with the remaining backward) or on the compute stream after the last backward GEMM")
     a = ap.parse_args()
 
     rank, world, local, device = D.init_distributed(force=a.force_dist)
@@ -79,6 +82,8 @@ def main():
     engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings,
                          force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python", comm=comm,
                          side_stream=a.side_stream)
+    if a.epi == "producer" and hasattr(engine, "epilogue_on_producer"):
+        engine.epilogue_on_producer = True
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
     if world > 1:
@@ -158,6 +163,8 @@ def main():
                 "engine": a.engine if device.type == "cuda" else "python",
                 "hip_graph": graphed,
                 "fused_sgd": True,
+                "epilogue_stream": ("compute" if getattr(engine, "epilogue_on_producer", False) else "comm")
+                if engine is not None and not getattr(engine, "inline", True) else "inline",
             },
             "extra": {
                 "achieved_tflops": round(flops / 1e12, 2),

@@ -197,6 +197,8 @@ void register_engine(pybind11::module_& m) {
           },
           py::arg("slot"), py::arg("after_current") = true, py::call_guard<py::gil_scoped_release>())
       .def("wait_stream", [](AllReduceEngine& e, int slot) { e.wait_stream(slot, fan_stream()); })
+      .def_property("epilogue_on_producer", &AllReduceEngine::epilogue_on_producer,
+                    &AllReduceEngine::set_epilogue_on_producer)
       .def("query", &AllReduceEngine::query)
       .def("done_word", &AllReduceEngine::done_word)
       .def("slot_seq", &AllReduceEngine::slot_seq)

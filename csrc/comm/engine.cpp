@@ -118,7 +118,7 @@ std::array<int64_t, 3> AllReduceEngine::prepack_shape(int64_t n) const {
   return {L.shard, world_, local ? -1 : rank_};
 }
 
-std::vector<std::function<void()>> AllReduceEngine::run_mesh(const EngineLayout& L, const void* grad, int gdt,
+std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const void* grad, int gdt,
                                                              float* master, bf16_t* lp, float* mom, int64_t n_valid,
                                                              SgdParams p, bool update, float* out_sum,
                                                              const uint8_t* prepacked, int64_t prepacked_elems) {
@@ -134,11 +134,11 @@ std::vector<std::function<void()>> AllReduceEngine::run_mesh(const EngineLayout&
   if ((N == 1 && !cfg_.force_comm) || comm_ == nullptr) {
     if (prepacked) {  // the producer's encoding IS the (single-rank) result: no reduce pass
       const uint8_t* W = prepacked;
-      return {[=] { epilogue(c, st, W, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
+      return {[=](hipStream_t es) { epilogue(c, es, W, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
     }
     uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
     launch_wire_reduce(c, gdt, S, sb, 1, 0, g, S, nullptr, (size_t)s, st);
-    return {[=] { epilogue(c, st, S, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
+    return {[=](hipStream_t es) { epilogue(c, es, S, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
   }
   uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
   const uint8_t* P = prepacked ? prepacked : g;
@@ -154,10 +154,10 @@ std::vector<std::function<void()>> AllReduceEngine::run_mesh(const EngineLayout&
   uint8_t* G = scratch("mesh_G" + std::to_string(sb * N), sb * N);
   comm_->all_gather(S, G, sb, st);
   const int64_t n_pad = L.n_pad;
-  return {[=] { epilogue(c, st, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
+  return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
 }
 
-std::vector<std::function<void()>> AllReduceEngine::run_ring(const EngineLayout& L, const void* grad, int gdt,
+std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const void* grad, int gdt,
                                                              float* master, bf16_t* lp, float* mom, int64_t n_valid,
                                                              SgdParams p, bool update, float* out_sum) {
   const int N = world_, c = cfg_.codec;
@@ -236,25 +236,25 @@ std::vector<std::function<void()>> AllReduceEngine::run_ring(const EngineLayout&
     }
     if (N > 1) comm_->sendrecv(sends, recvs, st);
   }
-  std::vector<std::function<void()>> thunks;
+  std::vector<EpiThunk> thunks;
   for (auto& rs : rings) {
     const int64_t off = rs.off, part = L.part, blocks = L.blocks;
     uint8_t* G = rs.G;
     if (compat) {
       const int own = (rs.pos - 1 + N) % N;
       float* f32 = rs.fp32;
-      thunks.push_back([=] {
-        epilogue(c, st, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum, own, N);
+      thunks.push_back([=](hipStream_t es) {
+        epilogue(c, es, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum, own, N);
         for (int64_t b = 0; b < blocks; ++b) {
           const int64_t o2 = off + (b * N + own) * S;
           const int64_t nv = std::max<int64_t>(0, std::min<int64_t>(n_valid - o2, S));
           if (nv > 0)
             launch_wire_sgd(kRawF32, f32 + b * S, (size_t)S, 1, -1, 0, master + o2, lp ? lp + o2 : nullptr,
-                            mom ? mom + o2 : nullptr, p, (size_t)nv, st);
+                            mom ? mom + o2 : nullptr, p, (size_t)nv, es);
         }
       });
     } else {
-      thunks.push_back([=] { epilogue(c, st, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum); });
+      thunks.push_back([=](hipStream_t es) { epilogue(c, es, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum); });
     }
   }
   return thunks;
@@ -298,32 +298,41 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
 void AllReduceEngine::commit(int slot, hipStream_t producer) {
   Slot& sl = slots_.at(slot);
   if (!sl.pending) return;
-  // inline requests already run on the producer's stream: stream order is the dependency
-  if (producer && producer != sl.stream) {
+  sl.epi_stream = sl.stream;
+  if (epi_on_producer_ && !inline_ && producer && producer != sl.stream) {
+    // Epilogue on the producer (compute) stream: it waits for the request's communication phase, then the
+    // decode+SGD runs there, ordered after everything already enqueued on it and not concurrently with
+    // the producer's GEMMs (a side-stream epilogue takes CU slots from their tiles).
+    FAN_HIP_CHECK(hipEventRecord(sl.update, sl.stream));
+    FAN_HIP_CHECK(hipStreamWaitEvent(producer, sl.update, 0));
+    sl.epi_stream = producer;
+  } else if (producer && producer != sl.stream) {
+    // inline requests already run on the producer's stream: stream order is the dependency
     FAN_HIP_CHECK(hipEventRecord(sl.update, producer));
     FAN_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.update, 0));
   }
-  for (auto& t : sl.thunks) t();
+  for (auto& t : sl.thunks) t(sl.epi_stream);
   sl.thunks.clear();
-  if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t1, sl.stream));
+  if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t1, sl.epi_stream));
   // Side-stream requests: completion word written by the GPU into host-mapped memory (the NIC's "write 1 to
-  // done_addr + done_id"). Inline requests sit on the critical compute stream, where the extra packet costs
-  // more than it buys: their completion is the done event.
-  if (!inline_) FAN_HIP_CHECK(hipStreamWriteValue32(sl.stream, flags_dev_ + slot * 16, sl.seq, 0));
-  FAN_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
+  // done_addr + done_id"). Requests finishing on the critical compute stream (inline, or epilogue on the
+  // producer) skip the extra packet there: their completion is the done event.
+  if (sl.epi_stream == sl.stream && !inline_)
+    FAN_HIP_CHECK(hipStreamWriteValue32(sl.stream, flags_dev_ + slot * 16, sl.seq, 0));
+  FAN_HIP_CHECK(hipEventRecord(sl.done, sl.epi_stream));
   sl.pending = false;
 }
 
 void AllReduceEngine::wait_stream(int slot, hipStream_t s) {
   Slot& sl = slots_.at(slot);
   if (sl.pending) commit(slot, nullptr);
-  if (s != sl.stream) FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
+  if (s != sl.epi_stream) FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
 }
 
 bool AllReduceEngine::query(int slot) {
   const Slot& sl = slots_.at(slot);
   if (sl.pending) return false;
-  if (inline_) return hipEventQuery(sl.done) == hipSuccess;
+  if (inline_ || sl.epi_stream != sl.stream) return hipEventQuery(sl.done) == hipSuccess;
   return flags_host_[slot * 16] == sl.seq;
 }
 

@@ -60,6 +60,9 @@ struct EngineCounters {
   uint64_t timed_requests = 0;
 };
 
+// Deferred epilogue of a request (decode + SGD), launched on the given stream at commit().
+using EpiThunk = std::function<void(hipStream_t)>;
+
 class AllReduceEngine {
  public:
   static constexpr int kSlots = 8;
@@ -93,6 +96,10 @@ class AllReduceEngine {
   void synchronize(int slot, double timeout_s = -1.0);   // host: bounded wait (throws with diagnostics)
   float latency_ms(int slot);
   void set_timing(bool on) { timing_ = on; }
+  // Side-stream engine: run each request's epilogue on the stream passed to commit() (after its communication
+  // phase) instead of on the comm stream.
+  void set_epilogue_on_producer(bool on) { epi_on_producer_ = on; }
+  bool epilogue_on_producer() const { return epi_on_producer_; }
   std::string diagnostics(int slot) const;
   uint64_t requests() const { return seq_; }
   const EngineCounters& counters() const { return counters_; }
@@ -107,14 +114,15 @@ class AllReduceEngine {
     bool timed = false;
     bool counted = false;   // device time already added to counters_
     hipStream_t stream = nullptr;  // stream the request runs on (comm stream, or the producer when inline)
-    std::vector<std::function<void()>> thunks;
+    hipStream_t epi_stream = nullptr;  // stream the epilogue was enqueued on (== stream unless epi_on_producer_)
+    std::vector<EpiThunk> thunks;
     double t_issue = 0.0;
   };
   uint8_t* scratch(const std::string& key, size_t bytes);
-  std::vector<std::function<void()>> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
+  std::vector<EpiThunk> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                               float* out_sum, const uint8_t* prepacked, int64_t prepacked_elems);
-  std::vector<std::function<void()>> run_ring(const EngineLayout& L, const void* grad, int gdt, float* master,
+  std::vector<EpiThunk> run_ring(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                               float* out_sum);
 
@@ -123,6 +131,7 @@ class AllReduceEngine {
   EngineConfig cfg_;
   std::vector<std::vector<int>> orders_;
   hipStream_t stream_ = nullptr;
+  bool epi_on_producer_ = false;
   // world 1 without forced collectives: nothing to overlap, so requests run inline on the producer's
   // stream (no cross-stream event packets); run_stream_ is the stream of the request being issued.
   bool inline_ = false;

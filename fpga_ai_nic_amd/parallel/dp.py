@@ -75,7 +75,8 @@ def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str
 class DataParallelTrainer:
     def __init__(self, model: MLP, engine: CompressedAllReduce | None, *, lr: float = 0.1,
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
-                 loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True):
+                 loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True,
+                 commit_at_end: bool | None = None):
         self.m = model
         self.engine = engine
         self.world = engine.world if engine is not None else 1
@@ -90,6 +91,10 @@ class DataParallelTrainer:
         self.times = {"fwd": 0.0, "loss": 0.0, "bwd": 0.0, "bwd_first": 0.0, "steps": 0}
         self.step_count = 0
         # fuse the BFP encode into the bwd-weight GEMM when the engine accepts prepacked wire input
+        # commit every request's epilogue after the whole backward is enqueued (required when the engine runs
+        # epilogues on the compute stream: a per-layer commit would stall it on that layer's communication)
+        self.commit_at_end = (bool(getattr(engine, "epilogue_on_producer", False)) if commit_at_end is None
+                              else commit_at_end)
         self.prepack = (prepack and engine is not None and getattr(engine, "prepack", False) and self.cuda
                         and model.dtype == torch.bfloat16)
 
@@ -165,7 +170,7 @@ class DataParallelTrainer:
                                                   name=f"fc{i}", **kw)
                 m.backward_data(i)
                 if h is not None:
-                    self.pending[i] = h.commit_after_current()
+                    self.pending[i] = h if self.commit_at_end else h.commit_after_current()
                     self.last_handle = self.pending[i]
                 else:
                     self._sgd_local(l)
@@ -175,6 +180,10 @@ class DataParallelTrainer:
                 self.times["bwd_first"] += t1 - t0
                 self.times["bwd"] += t1 - t0
                 t0 = t1
+        if self.commit_at_end:  # issue order L-1..0: the epilogues run in the order their all-reduces finish
+            for i in reversed(range(m.L)):
+                if self.pending[i] is not None:
+                    self.pending[i].commit_after_current()
         if prof:
             self._sync()
             self.times["bwd"] += time.perf_counter() - t0

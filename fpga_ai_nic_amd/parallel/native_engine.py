@@ -55,7 +55,8 @@ class NativeHandle:
         if self._pending:
             return False
         C = self.engine.C
-        if self.engine.inline:  # completion is the slot's done event (a reused slot is a later request)
+        if self.engine.inline or self.engine.epilogue_on_producer:
+            # completion is the slot's done event (a reused slot holds a later request on the same stream order)
             return C.query(self.slot)
         return ((C.done_word(self.slot) - self.seq) & 0xFFFFFFFF) < (1 << 31)
 
@@ -132,6 +133,18 @@ class NativeAllReduce:
     def timing(self, on):
         self._timing = bool(on)
         self.C.set_timing(self._timing)
+
+    @property
+    def epilogue_on_producer(self) -> bool:
+        """Side-stream engine: each request's decode+SGD epilogue runs on the stream that commits it (after the
+        request's communication phase) rather than on the comm stream, so it never shares CUs with the
+        producer's GEMMs. Callers then commit once the producer's overlapped work is enqueued (the trainer
+        commits all of a step's requests after the last backward GEMM)."""
+        return bool(self.C.epilogue_on_producer)
+
+    @epilogue_on_producer.setter
+    def epilogue_on_producer(self, on):
+        self.C.epilogue_on_producer = bool(on) and not self.inline
 
     @property
     def stream(self):

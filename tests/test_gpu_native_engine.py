@@ -140,6 +140,30 @@ def test_native_trainer_matches_python_trainer():
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
 
 
+def test_trainer_epilogue_on_producer_matches_comm_stream():
+    """Forced 1-rank RCCL path: the side-stream engine with its epilogues on the comm stream (committed per
+    layer) and on the compute stream (committed after the last backward GEMM) train bit-identically."""
+    from fpga_ai_nic_amd.models.mlp import MLP
+    from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer
+
+    res = []
+    for on_producer in (False, True):
+        eng = NativeAllReduce(_native_transport(), codec="bfp_rne", force_comm=True)
+        eng.epilogue_on_producer = on_producer
+        m = MLP([256, 512, 256, 128], dtype=torch.bfloat16, device="cuda", seed=3,
+                pad_fn=lambda n, e=eng: e.layout(n).n_pad)
+        tr = DataParallelTrainer(m, eng, lr=0.05)
+        assert tr.commit_at_end == on_producer
+        g = torch.Generator().manual_seed(0)
+        x = (torch.rand(256, 256, generator=g) * 2 - 1).to("cuda", torch.bfloat16)
+        y = torch.randint(0, 128, (256,), generator=g, dtype=torch.int32).cuda()
+        losses = [tr.step(x, y).float().mean().item() for _ in range(4)]
+        tr.finish()
+        res.append((losses, [l.master.cpu() for l in m.layers]))
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
 def test_mlp_mpi_cli_native_engine_gpu():
     """The reference entry point on GPU with the C++ engine (world 1): report lines + finite loss."""
     import io

@@ -33,7 +33,7 @@ def _threads(N, fn):
     return out, errs
 
 
-def _run(N, algo, rings, codec, n, max_slice=1024, lr=0.5, dtype=torch.float32, compat=False):
+def _run(N, algo, rings, codec, n, max_slice=1024, lr=0.5, dtype=torch.float32, compat=False, epi_producer=False):
     C = _ext.require()
     fabric = C.LoopbackFabric(N, 60.0)
     rng = np.random.default_rng(N * 100 + rings)
@@ -41,6 +41,9 @@ def _run(N, algo, rings, codec, n, max_slice=1024, lr=0.5, dtype=torch.float32, 
     w0 = rng.standard_normal(n).astype(np.float32)
     engines = [NativeAllReduce(None, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice,
                                comm=fabric.comm(r), compat_owner_fp32=compat) for r in range(N)]
+    for e in engines:
+        e.epilogue_on_producer = epi_producer
+        assert e.epilogue_on_producer == epi_producer
     L = engines[0].layout(n)
 
     def fn(r):
@@ -86,6 +89,12 @@ def _run(N, algo, rings, codec, n, max_slice=1024, lr=0.5, dtype=torch.float32, 
 @pytest.mark.parametrize("algo,rings", [("mesh", 1), ("ring", 1), ("ring", 7)])
 def test_loopback_schedules_bitexact(N, algo, rings):
     _run(N, algo, rings, "bfp_rne", n=20000)
+
+
+@pytest.mark.parametrize("algo,rings", [("mesh", 1), ("ring", 2)])
+def test_loopback_epilogue_on_producer_stream(algo, rings):
+    # the decode+SGD epilogue enqueued on the committing (compute) stream after the comm phase: same bits
+    _run(4, algo, rings, "bfp_rne", n=20000, epi_producer=True)
 
 
 @pytest.mark.parametrize("codec", ["bfp_trunc", "raw_f32", "raw_bf16"])
