@@ -59,7 +59,7 @@ def main():
                          "overlapped with the following GEMMs, instead of inline on the compute stream")
     ap.add_argument("--force-dist", action="store_true",
                     help="world 1 through the full multi-rank path (1-rank RCCL group, side-stream engine)")
-    ap.add_argument("--epi", default="comm", choices=["comm", "producer"],
+    ap.add_argument("--epi", default="producer", choices=["comm", "producer"],
                     help="side-stream engine: run each request's decode+SGD epilogue on the comm stream (overlapped "
                          "with the remaining backward) or on the compute stream after the last backward GEMM")
     a = ap.parse_args()
@@ -82,8 +82,8 @@ def main():
     engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings,
                          force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python", comm=comm,
                          side_stream=a.side_stream)
-    if a.epi == "producer" and hasattr(engine, "epilogue_on_producer"):
-        engine.epilogue_on_producer = True
+    if hasattr(engine, "epilogue_on_producer"):
+        engine.epilogue_on_producer = a.epi == "producer"
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
     if world > 1:

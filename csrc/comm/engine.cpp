@@ -38,6 +38,7 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
   for (auto& s : slots_) {
     FAN_HIP_CHECK(hipEventCreateWithFlags(&s.ready, hipEventDisableTiming));
     FAN_HIP_CHECK(hipEventCreateWithFlags(&s.update, hipEventDisableTiming));
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.comm_done, hipEventDisableTiming));
     FAN_HIP_CHECK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     FAN_HIP_CHECK(hipEventCreate(&s.t0));
     FAN_HIP_CHECK(hipEventCreate(&s.t1));
@@ -47,8 +48,10 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
 AllReduceEngine::~AllReduceEngine() {
   hipStreamSynchronize(stream_);
   for (auto& s : slots_) {
+    hipEventSynchronize(s.done);  // epilogues may have run on a producer stream and still read the scratch
     hipEventDestroy(s.ready);
     hipEventDestroy(s.update);
+    hipEventDestroy(s.comm_done);
     hipEventDestroy(s.done);
     hipEventDestroy(s.t0);
     hipEventDestroy(s.t1);
@@ -288,6 +291,8 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
                                         prepacked, prepacked_elems)
                              : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
   FAN_HIP_CHECK(hipGetLastError());
+  // end of this request's communication phase: what an epilogue on the producer stream waits for
+  if (!inline_) FAN_HIP_CHECK(hipEventRecord(sl.comm_done, stream_));
   sl.pending = true;
   sl.seq = ++seq_;
   sl.t_issue = now_s();
@@ -303,8 +308,7 @@ void AllReduceEngine::commit(int slot, hipStream_t producer) {
     // Epilogue on the producer (compute) stream: it waits for the request's communication phase, then the
     // decode+SGD runs there, ordered after everything already enqueued on it and not concurrently with
     // the producer's GEMMs (a side-stream epilogue takes CU slots from their tiles).
-    FAN_HIP_CHECK(hipEventRecord(sl.update, sl.stream));
-    FAN_HIP_CHECK(hipStreamWaitEvent(producer, sl.update, 0));
+    FAN_HIP_CHECK(hipStreamWaitEvent(producer, sl.comm_done, 0));
     sl.epi_stream = producer;
   } else if (producer && producer != sl.stream) {
     // inline requests already run on the producer's stream: stream order is the dependency

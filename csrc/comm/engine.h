@@ -108,7 +108,7 @@ class AllReduceEngine {
 
  private:
   struct Slot {
-    hipEvent_t ready = nullptr, update = nullptr, done = nullptr, t0 = nullptr, t1 = nullptr;
+    hipEvent_t ready = nullptr, update = nullptr, comm_done = nullptr, done = nullptr, t0 = nullptr, t1 = nullptr;
     uint32_t seq = 0;
     bool pending = false;   // epilogue not yet committed
     bool timed = false;

@@ -16,6 +16,7 @@ GPU only (the engine launches HIP kernels); CPU paths use the Python engine.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -124,6 +125,11 @@ class NativeAllReduce:
         self._prepack_bufs: dict = {}
         self._timing = False
         self.stats = {"requests": 0, "wire_bytes": 0, "logical_bytes": 0}
+        # Side-stream engines run their decode+SGD epilogues on the committing (compute) stream by default:
+        # with the epilogue on the comm stream, training on the 1-rank RCCL path came out NOT bit-identical to
+        # the inline engine and varied run to run (bwd-data outputs changed after their GEMM had run;
+        # tools/probes/race_probe.py, profiles/r1_comm_epilogue_discrepancy.txt). FAN_EPI=comm re-selects it.
+        self.epilogue_on_producer = os.environ.get("FAN_EPI", "producer") != "comm"
 
     @property
     def timing(self):

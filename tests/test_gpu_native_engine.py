@@ -140,28 +140,45 @@ def test_native_trainer_matches_python_trainer():
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
 
 
-def test_trainer_epilogue_on_producer_matches_comm_stream():
-    """Forced 1-rank RCCL path: the side-stream engine with its epilogues on the comm stream (committed per
-    layer) and on the compute stream (committed after the last backward GEMM) train bit-identically."""
+def _train_forced(on_producer, sizes=(256, 512, 256, 128), mb=256, steps=4):
     from fpga_ai_nic_amd.models.mlp import MLP
-    from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer
+    from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine
 
-    res = []
-    for on_producer in (False, True):
+    if on_producer is None:  # inline world-1 engine: the reference semantics
+        eng = make_engine(ThreadFabric(1).transport(0), "bfp", impl="native")
+    else:
         eng = NativeAllReduce(_native_transport(), codec="bfp_rne", force_comm=True)
         eng.epilogue_on_producer = on_producer
-        m = MLP([256, 512, 256, 128], dtype=torch.bfloat16, device="cuda", seed=3,
-                pad_fn=lambda n, e=eng: e.layout(n).n_pad)
-        tr = DataParallelTrainer(m, eng, lr=0.05)
-        assert tr.commit_at_end == on_producer
-        g = torch.Generator().manual_seed(0)
-        x = (torch.rand(256, 256, generator=g) * 2 - 1).to("cuda", torch.bfloat16)
-        y = torch.randint(0, 128, (256,), generator=g, dtype=torch.int32).cuda()
-        losses = [tr.step(x, y).float().mean().item() for _ in range(4)]
-        tr.finish()
-        res.append((losses, [l.master.cpu() for l in m.layers]))
-    assert res[0][0] == res[1][0]
-    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+    m = MLP(list(sizes), dtype=torch.bfloat16, device="cuda", seed=3, pad_fn=lambda n, e=eng: e.layout(n).n_pad)
+    tr = DataParallelTrainer(m, eng, lr=0.05)
+    assert tr.commit_at_end == bool(on_producer)
+    g = torch.Generator().manual_seed(0)
+    x = (torch.rand(mb, sizes[0], generator=g) * 2 - 1).to("cuda", torch.bfloat16)
+    y = torch.randint(0, sizes[-1], (mb,), generator=g, dtype=torch.int32).cuda()
+    losses = [tr.step(x, y).float().mean().item() for _ in range(steps)]
+    tr.finish()
+    return losses, [l.master.cpu() for l in m.layers]
+
+
+@pytest.mark.parametrize("sizes,mb", [((256, 512, 256, 128), 256), ((1024, 4096, 4096, 1024), 2048)])
+def test_multirank_path_trains_like_inline(sizes, mb):
+    """Forced 1-rank RCCL path with the default engine (side-stream comm, decode+SGD epilogues on the compute
+    stream after the last backward GEMM) trains bit-identically to the inline world-1 engine, run after run."""
+    ref = _train_forced(None, sizes, mb)
+    assert NativeAllReduce(_native_transport(), codec="bfp_rne", force_comm=True).epilogue_on_producer
+    for _ in range(2):
+        got = _train_forced(True, sizes, mb)
+        assert got[0] == ref[0]
+        assert all(torch.equal(a, b) for a, b in zip(got[1], ref[1]))
+
+
+@pytest.mark.xfail(reason="open issue: with the epilogue on the comm stream (FAN_EPI=comm), bwd-data outputs change "
+                          "after their GEMM ran (tools/probes/race_probe.py); not the default", strict=False)
+def test_multirank_comm_stream_epilogue_trains_like_inline():
+    ref = _train_forced(None, (1024, 4096, 4096, 1024), 2048)
+    got = _train_forced(False, (1024, 4096, 4096, 1024), 2048)
+    assert got[0] == ref[0]
+    assert all(torch.equal(a, b) for a, b in zip(got[1], ref[1]))
 
 
 def test_mlp_mpi_cli_native_engine_gpu():
