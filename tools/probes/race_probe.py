@@ -63,7 +63,7 @@ def run(arm, sync_each=False):
 
 SNAP = {}
 ref, ns = run("inline")
-for arm in ("producer_serial", "comm_serial"):
+for arm in (sys.argv[2].split(",") if len(sys.argv) > 2 else ("producer_serial", "comm_serial")):
     w, _ = run(arm)
     for i, (a, b) in enumerate(zip(w, ref)):
         d = (a - b).abs()
@@ -71,6 +71,6 @@ for arm in ("producer_serial", "comm_serial"):
         print(f"{arm:14s} {'master' if i < 3 else 'dz'} {i % 3 + (i >= 3)} n={ns[i]} n_pad={a.numel()} differing={nz.numel()} max={d.max().item():.3e} "
               f"first={nz[:6].tolist()} last={nz[-3:].tolist()}", flush=True)
 
-for (i, lp_a, ms_a, dz_a), (j, lp_b, ms_b, dz_b) in zip(SNAP["producer"], SNAP["comm"]):
+for (i, lp_a, ms_a, dz_a), (j, lp_b, ms_b, dz_b) in zip(SNAP.get("producer", []), SNAP.get("comm", [])):
     print(f"before bwd-data of layer {i}: lp differs at {int((lp_a != lp_b).sum())}, master at "
           f"{int((ms_a != ms_b).sum())}, input dz at {int((dz_a != dz_b).sum())}", flush=True)
