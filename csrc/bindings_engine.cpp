@@ -193,7 +193,7 @@ void register_engine(pybind11::module_& m) {
       .def(
           "commit",
           [](AllReduceEngine& e, int slot, bool after_current) {
-            e.commit(slot, after_current ? fan_stream() : nullptr);
+            e.commit(slot, after_current, after_current ? fan_stream() : nullptr);
           },
           py::arg("slot"), py::arg("after_current") = true, py::call_guard<py::gil_scoped_release>())
       .def("wait_stream", [](AllReduceEngine& e, int slot) { e.wait_stream(slot, fan_stream()); })

@@ -2,6 +2,7 @@
 #include "comm/engine.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <functional>
 #include <sstream>
 #include <thread>
@@ -35,11 +36,18 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
   void* d = nullptr;
   FAN_HIP_CHECK(hipHostGetDevicePointer(&d, h, 0));
   flags_dev_ = reinterpret_cast<uint32_t*>(d);
+  // Cross-stream events: FAN_EVENT_FENCE=system|device selects the release scope of the event marker
+  // (diagnostic for the comm-stream epilogue ordering issue, profiles/r1_comm_epilogue_discrepancy.txt).
+  unsigned evf = hipEventDisableTiming;
+  if (const char* f = std::getenv("FAN_EVENT_FENCE")) {
+    if (!std::strcmp(f, "system")) evf |= hipEventReleaseToSystem;
+    else if (!std::strcmp(f, "device")) evf |= hipEventReleaseToDevice;
+  }
   for (auto& s : slots_) {
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.ready, hipEventDisableTiming));
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.update, hipEventDisableTiming));
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.comm_done, hipEventDisableTiming));
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.ready, evf));
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.update, evf));
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.comm_done, evf));
+    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.done, evf));
     FAN_HIP_CHECK(hipEventCreate(&s.t0));
     FAN_HIP_CHECK(hipEventCreate(&s.t1));
   }
@@ -139,7 +147,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
       const uint8_t* W = prepacked;
       return {[=](hipStream_t es) { epilogue(c, es, W, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
     }
-    uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
+    uint8_t* S = scratch("mesh_S" + std::to_string(sb) + epi_key_, sb);
     launch_wire_reduce(c, gdt, S, sb, 1, 0, g, S, nullptr, (size_t)s, st);
     return {[=](hipStream_t es) { epilogue(c, es, S, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
   }
@@ -154,7 +162,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
   uint8_t* R = scratch("mesh_R" + std::to_string(sb * N), sb * N);
   comm_->all_to_all(P, R, sb, st);
   launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
-  uint8_t* G = scratch("mesh_G" + std::to_string(sb * N), sb * N);
+  uint8_t* G = scratch("mesh_G" + std::to_string(sb * N) + epi_key_, sb * N);
   comm_->all_gather(S, G, sb, st);
   const int64_t n_pad = L.n_pad;
   return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
@@ -191,12 +199,12 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
     rs.down = o[(pos - 1 + N) % N];
     rs.up = o[(pos + 1) % N];
     rs.plan = ring_plan(N, pos, L.blocks);
-    rs.G = scratch("ring_G" + std::to_string(i) + "_" + k, sb * nsl);
+    rs.G = scratch("ring_G" + std::to_string(i) + "_" + k + epi_key_, sb * nsl);
     rs.send = scratch("ring_send" + std::to_string(i) + "_" + k, sb);
     rs.recv[0] = scratch("ring_recv0_" + std::to_string(i) + "_" + k, sb);
     rs.recv[1] = scratch("ring_recv1_" + std::to_string(i) + "_" + k, sb);
     rs.last_partial = nullptr;
-    rs.fp32 = compat ? reinterpret_cast<float*>(scratch("ring_fp32_" + std::to_string(i) + "_" + k, 4 * S * L.blocks))
+    rs.fp32 = compat ? reinterpret_cast<float*>(scratch("ring_fp32_" + std::to_string(i) + "_" + k + epi_key_, 4 * S * L.blocks))
                      : nullptr;
     rings.push_back(rs);
   }
@@ -287,6 +295,9 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
     FAN_CHECK(prepack_shape(n_valid)[0] > 0, "prepacked input needs the mesh algorithm and a BFP codec");
     FAN_CHECK(prepacked_elems % 16 == 0 && prepacked_elems <= L.n_pad, "bad prepacked_elems");
   }
+  // buffers the deferred epilogue reads are per slot: a later request of the same size must not overwrite
+  // them before this one commits (the trainer commits every request at the end of backward)
+  epi_key_ = "_s" + std::to_string(slot);
   sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum,
                                         prepacked, prepacked_elems)
                              : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
@@ -296,21 +307,21 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   sl.pending = true;
   sl.seq = ++seq_;
   sl.t_issue = now_s();
-  if (!defer) commit(slot, nullptr);
+  if (!defer) commit(slot, false, nullptr);
   return slot;
 }
 
-void AllReduceEngine::commit(int slot, hipStream_t producer) {
+void AllReduceEngine::commit(int slot, bool after_producer, hipStream_t producer) {
   Slot& sl = slots_.at(slot);
   if (!sl.pending) return;
   sl.epi_stream = sl.stream;
-  if (epi_on_producer_ && !inline_ && producer && producer != sl.stream) {
+  if (epi_on_producer_ && !inline_ && after_producer && producer != sl.stream) {
     // Epilogue on the producer (compute) stream: it waits for the request's communication phase, then the
     // decode+SGD runs there, ordered after everything already enqueued on it and not concurrently with
     // the producer's GEMMs (a side-stream epilogue takes CU slots from their tiles).
     FAN_HIP_CHECK(hipStreamWaitEvent(producer, sl.comm_done, 0));
     sl.epi_stream = producer;
-  } else if (producer && producer != sl.stream) {
+  } else if (after_producer && producer != sl.stream) {
     // inline requests already run on the producer's stream: stream order is the dependency
     FAN_HIP_CHECK(hipEventRecord(sl.update, producer));
     FAN_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.update, 0));
@@ -329,7 +340,7 @@ void AllReduceEngine::commit(int slot, hipStream_t producer) {
 
 void AllReduceEngine::wait_stream(int slot, hipStream_t s) {
   Slot& sl = slots_.at(slot);
-  if (sl.pending) commit(slot, nullptr);
+  if (sl.pending) commit(slot, true, s);
   if (s != sl.epi_stream) FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
 }
 
@@ -352,7 +363,7 @@ std::string AllReduceEngine::diagnostics(int slot) const {
 
 void AllReduceEngine::synchronize(int slot, double timeout_s) {
   Slot& sl = slots_.at(slot);
-  if (sl.pending) commit(slot, nullptr);
+  if (sl.pending) commit(slot, false, nullptr);
   const double t0 = now_s();
   const double tmo = timeout_s > 0 ? timeout_s : cfg_.timeout_s;
   int spins = 0;

@@ -87,8 +87,10 @@ class AllReduceEngine {
   // (shard elements, shards, owner shard whose f32 values the reduce needs or -1) for a prepacked bucket,
   // or shard elements 0 when this configuration cannot take prepacked input.
   std::array<int64_t, 3> prepack_shape(int64_t n) const;
-  // Enqueue the deferred SGD epilogue after everything currently enqueued on `producer`.
-  void commit(int slot, hipStream_t producer);
+  // Enqueue the deferred SGD epilogue; with `after_producer`, after everything currently enqueued on
+  // `producer`. The flag is separate from the handle because the default (legacy null) stream IS nullptr:
+  // torch's default stream hands us 0, and treating that as "no producer" skipped the ordering wait.
+  void commit(int slot, bool after_producer, hipStream_t producer);
   void wait_stream(int slot, hipStream_t s);            // GPU-side wait
   bool query(int slot);                                  // host: request done?
   uint32_t done_word(int slot) const { return flags_host_[slot * 16]; }  // last completed sequence number
@@ -144,6 +146,7 @@ class AllReduceEngine {
   bool timing_ = false;
   EngineCounters counters_;
   std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
+  std::string epi_key_;  // scratch-key suffix of the request being built (its slot)
 };
 
 }  // namespace fan

@@ -125,10 +125,10 @@ class NativeAllReduce:
         self._prepack_bufs: dict = {}
         self._timing = False
         self.stats = {"requests": 0, "wire_bytes": 0, "logical_bytes": 0}
-        # Side-stream engines run their decode+SGD epilogues on the committing (compute) stream by default:
-        # with the epilogue on the comm stream, training on the 1-rank RCCL path came out NOT bit-identical to
-        # the inline engine and varied run to run (bwd-data outputs changed after their GEMM had run;
-        # tools/probes/race_probe.py, profiles/r1_comm_epilogue_discrepancy.txt). FAN_EPI=comm re-selects it.
+        # Side-stream engines run their decode+SGD epilogues on the committing (compute) stream by default
+        # (1.22 vs 1.25 ms/step on the forced 1-rank RCCL path, profiles/r1_null_stream_commit_fix.txt);
+        # FAN_EPI=comm runs them on the comm stream, committed per layer. Both train bit-identically to the
+        # inline engine since commit() stopped reading torch's default stream (handle 0) as "no producer".
         self.epilogue_on_producer = os.environ.get("FAN_EPI", "producer") != "comm"
 
     @property

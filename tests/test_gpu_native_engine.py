@@ -160,7 +160,12 @@ def _train_forced(on_producer, sizes=(256, 512, 256, 128), mb=256, steps=4):
     return losses, [l.master.cpu() for l in m.layers]
 
 
-@pytest.mark.parametrize("sizes,mb", [((256, 512, 256, 128), 256), ((1024, 4096, 4096, 1024), 2048)])
+# (512, 512, 512, 512): three buckets of the same size -- the deferred epilogues must not share a gathered
+# wire buffer (scratch is keyed per request slot)
+_FORCED_CASES = [((256, 512, 256, 128), 256), ((512, 512, 512, 512), 256), ((1024, 4096, 4096, 1024), 2048)]
+
+
+@pytest.mark.parametrize("sizes,mb", _FORCED_CASES)
 def test_multirank_path_trains_like_inline(sizes, mb):
     """Forced 1-rank RCCL path with the default engine (side-stream comm, decode+SGD epilogues on the compute
     stream after the last backward GEMM) trains bit-identically to the inline world-1 engine, run after run."""
@@ -172,11 +177,14 @@ def test_multirank_path_trains_like_inline(sizes, mb):
         assert all(torch.equal(a, b) for a, b in zip(got[1], ref[1]))
 
 
-@pytest.mark.xfail(reason="open issue: with the epilogue on the comm stream (FAN_EPI=comm), bwd-data outputs change "
-                          "after their GEMM ran (tools/probes/race_probe.py); not the default", strict=False)
-def test_multirank_comm_stream_epilogue_trains_like_inline():
-    ref = _train_forced(None, (1024, 4096, 4096, 1024), 2048)
-    got = _train_forced(False, (1024, 4096, 4096, 1024), 2048)
+@pytest.mark.parametrize("sizes,mb", _FORCED_CASES)
+def test_multirank_comm_stream_epilogue_trains_like_inline(sizes, mb):
+    """Epilogue on the comm stream, committed per layer after its bwd-data GEMM: bit-identical to inline.
+    Regression: torch's default stream is handle 0 and the engine used to read that as "no producer", so
+    the epilogue was not ordered after the bwd-data GEMM still reading the weights it overwrites
+    (profiles/r1_comm_epilogue_discrepancy.txt, profiles/r1_null_stream_commit_fix.txt)."""
+    ref = _train_forced(None, sizes, mb)
+    got = _train_forced(False, sizes, mb)
     assert got[0] == ref[0]
     assert all(torch.equal(a, b) for a, b in zip(got[1], ref[1]))
 
