@@ -111,6 +111,15 @@ uint8_t* AllReduceEngine::scratch(const std::string& key, size_t bytes) {
   return reinterpret_cast<uint8_t*>(p);
 }
 
+uint8_t* AllReduceEngine::epi_scratch(const std::string& base, size_t bytes) {
+  // one buffer per request slot; on a key's first use all kSlots are allocated at once, so the slot rotation
+  // never allocates later (inside a timed loop)
+  const std::string key = base + "_s" + std::to_string(epi_slot_);
+  if (scratch_.find(key) == scratch_.end())
+    for (int s = 0; s < kSlots; ++s) scratch(base + "_s" + std::to_string(s), bytes);
+  return scratch(key, bytes);
+}
+
 // Epilogue over a gathered wire region: fused decode + SGD (and/or decoded sum output).
 static void epilogue(int codec, hipStream_t st, const uint8_t* G, int64_t shard, int n_shards, int64_t off,
                      int64_t len, float* master, bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
@@ -147,7 +156,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
       const uint8_t* W = prepacked;
       return {[=](hipStream_t es) { epilogue(c, es, W, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
     }
-    uint8_t* S = scratch("mesh_S" + std::to_string(sb) + epi_key_, sb);
+    uint8_t* S = epi_scratch("mesh_S" + std::to_string(sb), sb);
     launch_wire_reduce(c, gdt, S, sb, 1, 0, g, S, nullptr, (size_t)s, st);
     return {[=](hipStream_t es) { epilogue(c, es, S, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
   }
@@ -162,7 +171,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
   uint8_t* R = scratch("mesh_R" + std::to_string(sb * N), sb * N);
   comm_->all_to_all(P, R, sb, st);
   launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
-  uint8_t* G = scratch("mesh_G" + std::to_string(sb * N) + epi_key_, sb * N);
+  uint8_t* G = epi_scratch("mesh_G" + std::to_string(sb * N), sb * N);
   comm_->all_gather(S, G, sb, st);
   const int64_t n_pad = L.n_pad;
   return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
@@ -199,12 +208,12 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
     rs.down = o[(pos - 1 + N) % N];
     rs.up = o[(pos + 1) % N];
     rs.plan = ring_plan(N, pos, L.blocks);
-    rs.G = scratch("ring_G" + std::to_string(i) + "_" + k + epi_key_, sb * nsl);
+    rs.G = epi_scratch("ring_G" + std::to_string(i) + "_" + k, sb * nsl);
     rs.send = scratch("ring_send" + std::to_string(i) + "_" + k, sb);
     rs.recv[0] = scratch("ring_recv0_" + std::to_string(i) + "_" + k, sb);
     rs.recv[1] = scratch("ring_recv1_" + std::to_string(i) + "_" + k, sb);
     rs.last_partial = nullptr;
-    rs.fp32 = compat ? reinterpret_cast<float*>(scratch("ring_fp32_" + std::to_string(i) + "_" + k + epi_key_, 4 * S * L.blocks))
+    rs.fp32 = compat ? reinterpret_cast<float*>(epi_scratch("ring_fp32_" + std::to_string(i) + "_" + k, 4 * S * L.blocks))
                      : nullptr;
     rings.push_back(rs);
   }
@@ -297,7 +306,7 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   }
   // buffers the deferred epilogue reads are per slot: a later request of the same size must not overwrite
   // them before this one commits (the trainer commits every request at the end of backward)
-  epi_key_ = "_s" + std::to_string(slot);
+  epi_slot_ = slot;
   sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum,
                                         prepacked, prepacked_elems)
                              : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);

@@ -146,7 +146,10 @@ class AllReduceEngine {
   bool timing_ = false;
   EngineCounters counters_;
   std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
-  std::string epi_key_;  // scratch-key suffix of the request being built (its slot)
+  int epi_slot_ = 0;  // slot of the request being built
+  // Scratch that a deferred epilogue reads: per request slot, so a later request of the same size cannot
+  // overwrite it before this request commits (the trainer commits every request at the end of backward).
+  uint8_t* epi_scratch(const std::string& base, size_t bytes);
 };
 
 }  // namespace fan
