@@ -232,6 +232,7 @@ class CompressedAllReduce:
         self._events: list = []
         self.timing = False  # per-request device timestamps (Handle.latency_ms)
         self._scratch: dict = {}
+        self._cur_slot = 0
         self._slot = 0
         self.fault = faults.FaultInjector.from_env()
         self.stats = {"requests": 0, "wire_bytes": 0, "logical_bytes": 0}
@@ -260,8 +261,10 @@ class CompressedAllReduce:
             return 2 * (N - 1) * wire.shard_bytes(self.codec_id, L.shard)
         return L.rings * L.blocks * 2 * (N - 1) * wire.shard_bytes(self.codec_id, L.slice_elems)
 
-    def _buf(self, L: BucketLayout, name: str, nbytes: int, dtype=torch.uint8):
-        key = (L.key, name)
+    def _buf(self, L: BucketLayout, name: str, nbytes: int, dtype=torch.uint8, per_slot: bool = False):
+        """Persistent scratch per bucket layout. ``per_slot``: a buffer a deferred epilogue reads — one per
+        request slot, so a later same-size request cannot overwrite it before this request commits."""
+        key = (L.key, name, self._cur_slot) if per_slot else (L.key, name)
         t = self._scratch.get(key)
         if t is None:
             t = torch.zeros(nbytes // torch.empty(0, dtype=dtype).element_size(), dtype=dtype, device=self.device)
@@ -324,6 +327,7 @@ class CompressedAllReduce:
     def _launch(self, comm_fn, name, L, defer=False, update_after=None) -> Handle:
         slot = self._slot
         self._slot = (slot + 1) % NUM_SLOTS
+        self._cur_slot = slot  # per-slot scratch of the request comm_fn builds
         self.stats["requests"] += 1
         self.stats["wire_bytes"] += self.wire_bytes(L)
         self.stats["logical_bytes"] += L.n * 4
@@ -405,7 +409,7 @@ class CompressedAllReduce:
         N, r, s, c = self.world, self.rank, L.shard, self.codec_id
         sb = wire.shard_bytes(c, s)
         g = grad.view(-1)[: L.n_pad]
-        S = self._buf(L, "mesh_S", sb)
+        S = self._buf(L, "mesh_S", sb, per_slot=N == 1 and not self.force_comm)
         if N == 1 and not self.force_comm:
             wire.reduce(S, 1, 0, g[:s], S, None, s, c)
             return [lambda: finish(S, s, 1, 0, s)]
@@ -425,7 +429,7 @@ class CompressedAllReduce:
             self.transport.all_to_all(cs, cs_r)
             self._verify_rows(R.view(N, sb), cs_r, list(range(N)), "mesh all_to_all")
         wire.reduce(R, N, r, g[r * s:(r + 1) * s], S, None, s, c)
-        G = self._buf(L, "mesh_G", sb * N)
+        G = self._buf(L, "mesh_G", sb * N, per_slot=True)
         self.transport.all_gather(S, G)
         if self.verify:
             cs_g = torch.empty(N, 3, dtype=torch.int64, device=G.device)
@@ -447,11 +451,11 @@ class CompressedAllReduce:
                 off=i * L.part,
                 down=order[(pos - 1) % N], up=order[(pos + 1) % N], pos=pos,
                 plan=ring_plan(N, pos, L.blocks),
-                G=self._buf(L, f"ring_G{i}", sb * nsl),
+                G=self._buf(L, f"ring_G{i}", sb * nsl, per_slot=True),
                 send=self._buf(L, f"ring_send{i}", sb),
                 recv=[self._buf(L, f"ring_recv{i}_0", sb), self._buf(L, f"ring_recv{i}_1", sb)],
                 last_partial=None,
-                fp32=self._buf(L, f"ring_fp32_{i}", 4 * S * L.blocks, torch.float32) if compat else None,
+                fp32=self._buf(L, f"ring_fp32_{i}", 4 * S * L.blocks, torch.float32, per_slot=True) if compat else None,
             ))
         nrows = len(rings[0]["plan"])
         # group rows into communication rounds: a SEND_LOCAL row joins the previous round (OUTPUT_SEND overlap)

@@ -104,3 +104,46 @@ def test_plan_every_slice_owned_once_and_all_received():
             assert sorted(owned) == list(range(N * blocks))
             assert all(len(v) == 1 for v in owned.values())
             assert all(g == set(range(N * blocks)) for g in got)
+
+
+@pytest.mark.parametrize("N", [1, 2, 3])
+@pytest.mark.parametrize("algo", ["mesh", "ring"])
+def test_deferred_same_size_requests_keep_their_own_result(N, algo):
+    """Two same-size requests issued with defer=True and committed only after both were issued (how the
+    trainer commits at the end of backward): each epilogue must apply ITS OWN reduced gradient. A gathered
+    wire buffer shared per bucket size let the second request's result overwrite the first's."""
+    n = 2000
+    rng = np.random.default_rng(7 + N)
+    grads = [[rng.standard_normal(n).astype(np.float32) * (1 + r + 3 * b) for r in range(N)] for b in range(2)]
+    w0 = rng.standard_normal(n).astype(np.float32)
+
+    def fn(t):
+        eng = CompressedAllReduce(t, codec="bfp_rne", algo=algo, device="cpu")
+        L = eng.layout(n)
+        outs = []
+        for deferred in (True, False):
+            ws, hs = [], []
+            for b in range(2):
+                g = torch.zeros(L.n_pad)
+                g[:n] = torch.from_numpy(grads[b][t.rank])
+                w = torch.zeros(L.n_pad)
+                w[:n] = torch.from_numpy(w0)
+                h = eng.allreduce_sgd(g, w, None, None, n_valid=n, lr=0.5, defer=deferred)
+                if not deferred:
+                    h.synchronize()
+                ws.append(w)
+                hs.append(h)
+            for h in hs:
+                h.commit()
+                h.synchronize()
+            outs.append([w.numpy().copy() for w in ws])
+        return outs
+
+    for deferred, immediate in fabric_run(N, fn):
+        for a, b in zip(deferred, immediate):
+            assert np.array_equal(a, b)
+        assert not np.array_equal(deferred[0], deferred[1])
+
+
+def fabric_run(N, fn):
+    return ThreadFabric(N, timeout_s=60).run(fn)
