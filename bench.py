@@ -3,49 +3,51 @@
 
 BASELINE.json config 3: bf16 MLP, BFP-compressed all-reduce of every layer's gradient bucket with the SGD
 weight update fused into the all-gather epilogue, comm overlapped with backward on a side HIP stream.
-Metric: whole-job training throughput in samples/s (weak scaling: per-GPU batch fixed as N grows).
+Metric: whole-job training throughput in samples/s (weak scaling: per-GPU batch fixed as N grows), plus the
+all-reduce algo-BW of the requests that ran inside the timed steps (device timestamps of each request's
+communication phase, ``extra.allreduce``).
 
-Contract: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under torch.distributed.run, one rank per
-GPU over RCCL). W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier +
-torch.cuda.synchronize() on both sides; max time over ranks; rank 0 prints ONE JSON line.
+Contract: ``python bench.py --gpus N --steps K --warmup W``. Under torch.distributed.run (RANK / WORLD_SIZE set)
+every process is one rank on one GPU over RCCL. Without that environment and N > 1, this script starts
+``torch.distributed.run --nproc-per-node N`` itself as a CHILD process before anything touches the GPU, and
+exits with its code (the parent never initialises HIP). W untimed warmup steps, then EXACTLY K timed steps
+bracketed by barrier + torch.cuda.synchronize() on both sides; max time over ranks; rank 0 prints ONE JSON line.
 
 Synthetic data (random bf16 inputs, random labels) and random-init weights of the named architecture.
+Reference workload shapes: sw/run.sh:16 (global MB 5376 over 3 ranks = 1792 per rank) — reported as
+``extra.mb1792`` next to the headline per-GPU batch.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from fpga_ai_nic_amd.models.mlp import MLP  # noqa: E402
-from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine  # noqa: E402
-from fpga_ai_nic_amd.parallel.transport import (NativeTransport, ThreadFabric, TorchDistTransport,  # noqa: E402
-                                                make_p2p_comm)
-from fpga_ai_nic_amd.utils import dist as D  # noqa: E402
-
 SIZES = [1024, 4096, 4096, 1024]
+REF_MB_PER_RANK = 1792  # sw/run.sh:16: global MB 5376 / 3 ranks
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     # per-GPU minibatch (weak scaling). The reference fixes only the architecture for this config; 8192 rows per
     # GPU keeps the MFMA GEMMs out of the tile-quantisation regime (measured: 2048 -> 4.6M samples/s,
-    # 8192 -> 6.9M samples/s on one MI355X) and gives the overlapped all-reduce a ~1.2 ms backward to hide in.
+    # 8192 -> 7.2M samples/s on one MI355X) and gives the overlapped all-reduce a ~1.1 ms backward to hide in.
+    # The reference's own per-rank batch (1792) is measured as well and reported in extra.mb1792.
     ap.add_argument("--mb-per-gpu", type=int, default=8192)
+    ap.add_argument("--ref-mb", type=int, default=REF_MB_PER_RANK,
+                    help="also time K steps at this per-GPU batch (extra.mb<ref>); 0 disables")
     ap.add_argument("--compress", default="bfp", choices=["bfp", "raw", "raw_bf16", "rccl", "local"])
     ap.add_argument("--rounding", default="rne", choices=["rne", "trunc"])
     ap.add_argument("--algo", default="mesh", choices=["mesh", "ring"])
     ap.add_argument("--rings", type=int, default=1)
-    ap.add_argument("--transport", default="torch", choices=["torch", "native", "p2p"],
+    ap.add_argument("--transport", default="native", choices=["torch", "native", "p2p"],
                     help="torch/native: RCCL collectives; p2p: direct HIP-IPC peer writes + stream flags "
                          "(C++ engine only)")
     ap.add_argument("--engine", default="native", choices=["python", "native"],
@@ -62,7 +64,59 @@ def main():
     ap.add_argument("--epi", default="producer", choices=["comm", "producer"],
                     help="side-stream engine: run each request's decode+SGD epilogue on the comm stream (overlapped "
                          "with the remaining backward) or on the compute stream after the last backward GEMM")
-    a = ap.parse_args()
+    ap.add_argument("--no-trace", action="store_true",
+                    help="do not record per-request device timestamps inside the timed steps (extra.allreduce)")
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a, argv) -> int | None:
+    """--gpus N > 1 without a torch.distributed environment: run N ranks under torch.distributed.run as a child
+    process (this process never touches the GPU) and return its exit code; None when no launch is needed."""
+    if a.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / CUDA-tensor sharing across processes)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+def _time_steps(step, steps, device, D):
+    import torch
+
+    D.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    return t0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse_args(argv)
+    rc = self_launch(a, argv)
+    if rc is not None:
+        return rc
+
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fpga_ai_nic_amd.models.mlp import MLP
+    from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine
+    from fpga_ai_nic_amd.parallel.transport import (NativeTransport, ThreadFabric, TorchDistTransport,
+                                                    make_p2p_comm)
+    from fpga_ai_nic_amd.utils import dist as D
 
     rank, world, local, device = D.init_distributed(force=a.force_dist)
     if world != a.gpus and rank == 0:
@@ -71,18 +125,17 @@ def main():
         print("[bench] no GPU visible: running the CPU path (functional only)", file=sys.stderr)
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     comm = None
+    impl = a.engine if device.type == "cuda" else "python"
     if world > 1 or a.force_dist:
-        transport = NativeTransport(force_collectives=a.force_dist) if a.transport == "native" else \
-            TorchDistTransport(force_collectives=a.force_dist)
-        if a.transport == "p2p" and device.type == "cuda" and a.engine == "native":
+        transport = NativeTransport(force_collectives=a.force_dist) if (a.transport == "native" and impl == "native") \
+            else TorchDistTransport(force_collectives=a.force_dist)
+        if a.transport == "p2p" and device.type == "cuda" and impl == "native":
             comm = make_p2p_comm()
     else:
         transport = ThreadFabric(1).transport(0)
-    kind = "local" if a.compress == "local" else a.compress
-    engine = make_engine(transport, kind, rounding=a.rounding, algo=a.algo, rings=a.rings,
-                         force_comm=a.force_dist, impl=a.engine if device.type == "cuda" else "python", comm=comm,
-                         side_stream=a.side_stream)
-    if hasattr(engine, "epilogue_on_producer"):
+    engine = make_engine(transport, a.compress, rounding=a.rounding, algo=a.algo, rings=a.rings,
+                         force_comm=a.force_dist, impl=impl, comm=comm, side_stream=a.side_stream)
+    if hasattr(engine, "epilogue_on_producer") and not getattr(engine, "inline", True):
         engine.epilogue_on_producer = a.epi == "producer"
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
     model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
@@ -91,50 +144,69 @@ def main():
             transport.broadcast_(l.master, 0)
         model.sync_lp()
     trainer = DataParallelTrainer(model, engine, lr=a.lr)
-    mb = a.mb_per_gpu
-    g = torch.Generator().manual_seed(1234 + rank)
-    x = (torch.rand(mb, SIZES[0], generator=g) * 2 - 1).to(device=device, dtype=dtype)
-    y = torch.randint(0, SIZES[-1], (mb,), generator=g, dtype=torch.int32).to(device)
+    # device-timed communication phase of every request inside the timed steps (C++ engine, multi-rank path)
+    can_trace = (not a.no_trace and hasattr(engine, "trace") and not getattr(engine, "inline", True))
 
-    for _ in range(a.warmup):
-        trainer.step(x, y)
-    trainer.finish()
-    step = lambda: trainer.step(x, y)  # noqa: E731
-    graphed = False
-    if a.graph and device.type == "cuda" and world == 1 and (engine is None or getattr(engine, "inline", False)):
-        # the whole step (fwd, loss, bwd GEMMs, BFP encode, fused SGD) is a fixed kernel sequence on one
-        # stream at world 1: capture it once, replay per step (removes the host launch path entirely)
-        try:
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                trainer.step(x, y)
-                trainer.finish_async()
+    def batch(mb, seed):
+        g = torch.Generator().manual_seed(seed + rank)
+        x = (torch.rand(mb, SIZES[0], generator=g) * 2 - 1).to(device=device, dtype=dtype)
+        y = torch.randint(0, SIZES[-1], (mb,), generator=g, dtype=torch.int32).to(device)
+        return x, y
+
+    def run(mb, seed, graph_ok):
+        """W warmup + K timed steps at per-GPU batch mb: (elapsed s max over ranks, host enqueue s, loss,
+        trace summary or None, graphed)."""
+        x, y = batch(mb, seed)
+        for _ in range(a.warmup):
+            trainer.step(x, y)
+        trainer.finish()
+        step = lambda: trainer.step(x, y)  # noqa: E731
+        graphed = False
+        if graph_ok and a.graph and device.type == "cuda" and world == 1 and \
+                (engine is None or getattr(engine, "inline", False)):
+            # the whole step (fwd, loss, bwd GEMMs, BFP encode, fused SGD) is a fixed kernel sequence on one
+            # stream at world 1: capture it once, replay per step (removes the host launch path entirely)
+            try:
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    trainer.step(x, y)
+                    trainer.finish_async()
+                torch.cuda.synchronize()
+                step = gr.replay
+                graphed = True
+            except RuntimeError as e:  # capture unsupported for this configuration: stay eager
+                print(f"[bench] HIP graph capture failed ({e}); running eagerly", file=sys.stderr)
+                torch.cuda.synchronize()
+        if can_trace:
+            engine.trace(True)
+        t0 = _time_steps(step, a.steps, device, D)
+        loss_rows = model.loss_rows
+        t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
+        trainer.finish()
+        if device.type == "cuda":
             torch.cuda.synchronize()
-            step = gr.replay
-            graphed = True
-        except RuntimeError as e:  # capture unsupported for this configuration: stay eager
-            print(f"[bench] HIP graph capture failed ({e}); running eagerly", file=sys.stderr)
-            torch.cuda.synchronize()
-    D.barrier()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    loss_rows = model.loss_rows
-    t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
-    trainer.finish()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    D.barrier()
-    elapsed = D.max_over_ranks(time.perf_counter() - t0)
-    loss = float(loss_rows.float().mean().item())
+        D.barrier()
+        elapsed = D.max_over_ranks(time.perf_counter() - t0)
+        tr = None
+        if can_trace:
+            tr = engine.trace_summary()
+            engine.trace(False)
+            tr["comm_ms"] = D.max_over_ranks(tr["comm_ms"])  # the slowest rank's communication time
+        return elapsed, t_enqueue, float(loss_rows.float().mean().item()), tr, graphed
+
+    mb = a.mb_per_gpu
+    elapsed, t_enqueue, loss, tr, graphed = run(mb, 1234, True)
+    ref = None
+    if a.ref_mb and a.ref_mb != mb:
+        e2, _, _, tr2, _ = run(a.ref_mb, 4321, False)
+        ref = {"mb_per_gpu": a.ref_mb, "global_batch": a.ref_mb * world,
+               "samples_per_s": round(a.ref_mb * world * a.steps / e2, 2), "ms_per_step": round(e2 / a.steps * 1e3, 4),
+               "allreduce": _allreduce_report(tr2, world)}
 
     ms = elapsed / a.steps * 1e3
     global_batch = mb * world
     value = global_batch * a.steps / elapsed
     flops = model.flops_per_sample() * global_batch * a.steps / elapsed
-    grad_bytes = sum(l.n for l in model.layers) * 4
     if rank == 0:
         rec = {
             "metric": "MLP training samples/sec (1024-4096-4096-1024, BFP all-reduce + fused SGD)",
@@ -159,8 +231,8 @@ def main():
                 "rounding": a.rounding,
                 "algo": a.algo,
                 "rings": engine.rings if engine is not None else 0,
-                "transport": a.transport if world > 1 else "none",
-                "engine": a.engine if device.type == "cuda" else "python",
+                "transport": a.transport if (world > 1 or a.force_dist) else "none",
+                "engine": impl,
                 "hip_graph": graphed,
                 "fused_sgd": True,
                 "epilogue_stream": ("compute" if getattr(engine, "epilogue_on_producer", False) else "comm")
@@ -169,15 +241,37 @@ def main():
             "extra": {
                 "achieved_tflops": round(flops / 1e12, 2),
                 "host_enqueue_ms_per_step": round(t_enqueue / a.steps * 1e3, 4),
-                "grad_bytes_f32_per_step": grad_bytes,
-                "effective_allreduce_algo_bw_GBps": round(grad_bytes / (ms / 1e3) / 1e9, 2),
+                "grad_bytes_f32_per_step": sum(l.n for l in model.layers) * 4,
+                "allreduce": _allreduce_report(tr, world),
+                f"mb{a.ref_mb}": ref,
                 "final_loss": round(loss, 5),
                 **({"engine_counters": engine.counters()} if hasattr(engine, "counters") else {}),
             },
         }
         print(json.dumps(rec), flush=True)
     D.cleanup()
+    return 0
+
+
+def _allreduce_report(tr, world):
+    """All-reduce algo-BW of the requests inside the timed steps: logical (f32 gradient) bytes / summed device time
+    of their communication phases (request start on the comm stream -> end of the all-gather, slowest rank);
+    bus-BW = algo-BW x 2(N-1)/N; wire-BW = bytes this rank actually sent (BFP-packed) / the same time.
+    None when no collective ran (world 1 inline engine: no wire)."""
+    if not tr or not tr.get("requests") or tr.get("comm_ms", 0) <= 0:
+        return None
+    s = tr["comm_ms"] / 1e3
+    algo = tr["logical_bytes"] / s / 1e9
+    return {
+        "requests": tr["requests"],
+        "comm_ms_total": round(tr["comm_ms"], 4),
+        "allreduce_algo_bw_GBps": round(algo, 2),
+        "bus_bw_GBps": round(algo * 2 * (world - 1) / world, 2) if world > 1 else 0.0,
+        "wire_bw_GBps": round(tr["wire_bytes"] / s / 1e9, 2),
+        "phase_ms": {k: round(tr[k], 4) for k in ("pack_ms", "exchange_ms", "reduce_ms", "gather_ms", "epilogue_ms")},
+        "dropped": tr.get("dropped", 0),
+    }
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -192,18 +192,47 @@ void register_engine(pybind11::module_& m) {
       .def_property_readonly("codec", &AllReduceEngine::codec)
       .def(
           "commit",
-          [](AllReduceEngine& e, int slot, bool after_current) {
-            e.commit(slot, after_current, after_current ? fan_stream() : nullptr);
+          [](AllReduceEngine& e, int slot, bool after_current, uint32_t seq) {
+            e.commit(slot, after_current, after_current ? fan_stream() : nullptr, seq);
           },
-          py::arg("slot"), py::arg("after_current") = true, py::call_guard<py::gil_scoped_release>())
-      .def("wait_stream", [](AllReduceEngine& e, int slot) { e.wait_stream(slot, fan_stream()); })
+          py::arg("slot"), py::arg("after_current") = true, py::arg("seq") = 0u,
+          py::call_guard<py::gil_scoped_release>())
+      .def(
+          "wait_stream", [](AllReduceEngine& e, int slot, uint32_t seq) { e.wait_stream(slot, fan_stream(), seq); },
+          py::arg("slot"), py::arg("seq") = 0u)
       .def_property("epilogue_on_producer", &AllReduceEngine::epilogue_on_producer,
                     &AllReduceEngine::set_epilogue_on_producer)
-      .def("query", &AllReduceEngine::query)
+      .def("query", &AllReduceEngine::query, py::arg("slot"), py::arg("seq") = 0u)
       .def("done_word", &AllReduceEngine::done_word)
       .def("slot_seq", &AllReduceEngine::slot_seq)
       .def("synchronize", &AllReduceEngine::synchronize, py::arg("slot"), py::arg("timeout_s") = -1.0,
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("seq") = 0u, py::call_guard<py::gil_scoped_release>())
+      .def("set_tracing", &AllReduceEngine::set_tracing, py::arg("on"), py::arg("capacity") = 1024)
+      .def_property_readonly("tracing", &AllReduceEngine::tracing)
+      .def(
+          "trace_summary",
+          [](AllReduceEngine& e) {
+            TraceSummary t;
+            {
+              py::gil_scoped_release nogil;  // waits for the traced requests
+              t = e.trace_summary();
+            }
+            py::dict d;
+            d["requests"] = t.requests;
+            d["dropped"] = t.dropped;
+            d["logical_bytes"] = t.logical_bytes;
+            d["wire_bytes"] = t.wire_bytes;
+            d["pack_ms"] = t.ms[kTpPacked];
+            d["exchange_ms"] = t.ms[kTpExchanged];
+            d["reduce_ms"] = t.ms[kTpReduced];
+            d["gather_ms"] = t.ms[kTpCommEnd];
+            d["epilogue_ms"] = t.ms[kTpEpiEnd];
+            d["comm_ms"] = t.comm_ms;
+            d["total_ms"] = t.total_ms;
+            return d;
+          },
+          "per-phase device time summed over the traced requests (pack / all-to-all / reduce / all-gather / "
+          "epilogue; hw/all_reduce.sv:892-1085 per-state counters)")
       .def("latency_ms", &AllReduceEngine::latency_ms, py::call_guard<py::gil_scoped_release>())
       .def("set_timing", &AllReduceEngine::set_timing)
       .def("diagnostics", &AllReduceEngine::diagnostics)
@@ -219,6 +248,7 @@ void register_engine(pybind11::module_& m) {
              d["host_spins"] = c.host_spins;
              d["device_ms"] = c.device_ms;
              d["timed_requests"] = c.timed_requests;
+             d["forced_commits"] = c.forced_commits;
              return d;
            },
            "perf counters (the NIC's latency / host-stall registers): requests, bytes, host wait, device time")

@@ -64,6 +64,8 @@ AllReduceEngine::~AllReduceEngine() {
     hipEventDestroy(s.t0);
     hipEventDestroy(s.t1);
   }
+  for (auto& t : trace_pool_)
+    for (auto& e : t.ev) hipEventDestroy(e);
   for (auto& kv : scratch_) hipFree(kv.second.first);
   if (flags_host_) hipHostFree((void*)flags_host_);
   hipStreamDestroy(stream_);
@@ -168,9 +170,12 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     launch_wire_pack(c, gdt, g, Pb, (size_t)s, N, st);
     P = Pb;
   }
+  mark(kTpPacked);
   uint8_t* R = scratch("mesh_R" + std::to_string(sb * N), sb * N);
   comm_->all_to_all(P, R, sb, st);
+  mark(kTpExchanged);
   launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
+  mark(kTpReduced);
   uint8_t* G = epi_scratch("mesh_G" + std::to_string(sb * N), sb * N);
   comm_->all_gather(S, G, sb, st);
   const int64_t n_pad = L.n_pad;
@@ -287,7 +292,13 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   const int slot = next_slot_;
   next_slot_ = (slot + 1) % kSlots;
   Slot& sl = slots_[slot];
-  FAN_CHECK(!sl.pending, "request slot still has an uncommitted epilogue (more than 8 requests in flight)");
+  // The slot still holds a request whose epilogue was never committed (more than kSlots requests deferred, e.g.
+  // a deep model whose trainer commits at the end of backward): commit it now, ordered after everything the
+  // producer has enqueued so far (the hardware analogue: the NIC's 8-deep command queue never drops a request).
+  if (sl.pending) {
+    counters_.forced_commits++;
+    commit_slot(sl, slot, true, producer);
+  }
   const EngineLayout L = layout(n_valid);
   sl.stream = run_stream_ = inline_ ? producer : stream_;
   if (!inline_) {
@@ -297,9 +308,22 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   sl.timed = timing_;
   sl.counted = false;
   if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t0, sl.stream));
+  const int64_t wb = wire_bytes(L);
   counters_.requests++;
   counters_.logical_bytes += n_valid * 4;
-  counters_.wire_bytes += wire_bytes(L);
+  counters_.wire_bytes += wb;
+  sl.trace = -1;
+  cur_trace_ = -1;
+  if (tracing_) {
+    if (trace_used_ < trace_pool_.size()) {
+      sl.trace = cur_trace_ = (int)trace_used_++;
+      trace_pool_[cur_trace_].logical_bytes = n_valid * 4;
+      trace_pool_[cur_trace_].wire_bytes = wb;
+      mark(kTpStart);
+    } else {
+      trace_dropped_++;
+    }
+  }
   if (prepacked) {
     FAN_CHECK(prepack_shape(n_valid)[0] > 0, "prepacked input needs the mesh algorithm and a BFP codec");
     FAN_CHECK(prepacked_elems % 16 == 0 && prepacked_elems <= L.n_pad, "bad prepacked_elems");
@@ -307,21 +331,31 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   // buffers the deferred epilogue reads are per slot: a later request of the same size must not overwrite
   // them before this one commits (the trainer commits every request at the end of backward)
   epi_slot_ = slot;
+  trace_marked_ = 1u << kTpStart;
   sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum,
                                         prepacked, prepacked_elems)
                              : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
   FAN_HIP_CHECK(hipGetLastError());
+  // phases this schedule does not have (ring hops, the world-1 local path) collapse onto the end of comm
+  for (int tp = kTpPacked; tp <= kTpCommEnd; ++tp)
+    if (!(trace_marked_ & (1u << tp))) mark(tp);
+  cur_trace_ = -1;
   // end of this request's communication phase: what an epilogue on the producer stream waits for
   if (!inline_) FAN_HIP_CHECK(hipEventRecord(sl.comm_done, stream_));
   sl.pending = true;
   sl.seq = ++seq_;
   sl.t_issue = now_s();
-  if (!defer) commit(slot, false, nullptr);
+  if (!defer) commit_slot(sl, slot, false, nullptr);
   return slot;
 }
 
-void AllReduceEngine::commit(int slot, bool after_producer, hipStream_t producer) {
+void AllReduceEngine::commit(int slot, bool after_producer, hipStream_t producer, uint32_t seq) {
   Slot& sl = slots_.at(slot);
+  if (seq != 0 && seq != sl.seq) return;  // superseded: committed when its slot was reused
+  commit_slot(sl, slot, after_producer, producer);
+}
+
+void AllReduceEngine::commit_slot(Slot& sl, int slot, bool after_producer, hipStream_t producer) {
   if (!sl.pending) return;
   sl.epi_stream = sl.stream;
   if (epi_on_producer_ && !inline_ && after_producer && producer != sl.stream) {
@@ -338,6 +372,7 @@ void AllReduceEngine::commit(int slot, bool after_producer, hipStream_t producer
   for (auto& t : sl.thunks) t(sl.epi_stream);
   sl.thunks.clear();
   if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t1, sl.epi_stream));
+  if (sl.trace >= 0) FAN_HIP_CHECK(hipEventRecord(trace_pool_[sl.trace].ev[kTpEpiEnd], sl.epi_stream));
   // Side-stream requests: completion word written by the GPU into host-mapped memory (the NIC's "write 1 to
   // done_addr + done_id"). Requests finishing on the critical compute stream (inline, or epilogue on the
   // producer) skip the extra packet there: their completion is the done event.
@@ -347,17 +382,66 @@ void AllReduceEngine::commit(int slot, bool after_producer, hipStream_t producer
   sl.pending = false;
 }
 
-void AllReduceEngine::wait_stream(int slot, hipStream_t s) {
+void AllReduceEngine::wait_stream(int slot, hipStream_t s, uint32_t seq) {
   Slot& sl = slots_.at(slot);
-  if (sl.pending) commit(slot, true, s);
-  if (s != sl.epi_stream) FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
+  // A superseded request (seq != slot's) was committed at reuse. If the newer request is still pending, the
+  // slot's done event still marks the old request's completion; otherwise it marks the newer one, which is
+  // later in every stream order the old request shares (a conservative wait). Never commit the newer one here.
+  const bool own = seq == 0 || seq == sl.seq;
+  if (own && sl.pending) commit_slot(sl, slot, true, s);
+  if (s != sl.epi_stream || !own) FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
 }
 
-bool AllReduceEngine::query(int slot) {
+bool AllReduceEngine::query(int slot, uint32_t seq) {
   const Slot& sl = slots_.at(slot);
+  if (seq != 0 && seq != sl.seq) {
+    // superseded request: its completion is the slot's done event while the newer request is pending, and is
+    // implied by the done word / done event of the newer one otherwise
+    if (!inline_ && ((flags_host_[slot * 16] - seq) & 0xFFFFFFFFu) < (1u << 31)) return true;
+    return hipEventQuery(sl.done) == hipSuccess;
+  }
   if (sl.pending) return false;
   if (inline_ || sl.epi_stream != sl.stream) return hipEventQuery(sl.done) == hipSuccess;
   return flags_host_[slot * 16] == sl.seq;
+}
+
+void AllReduceEngine::set_tracing(bool on, int capacity) {
+  tracing_ = on;
+  if (!on) return;
+  // a new trace window: wait for the previous window's requests before their events are re-recorded
+  for (size_t i = 0; i < trace_used_; ++i) hipEventSynchronize(trace_pool_[i].ev[kTpEpiEnd]);
+  while ((int)trace_pool_.size() < capacity) {
+    RequestTrace t;
+    for (auto& e : t.ev) FAN_HIP_CHECK(hipEventCreate(&e));
+    trace_pool_.push_back(t);
+  }
+  trace_used_ = 0;
+  trace_dropped_ = 0;
+}
+
+TraceSummary AllReduceEngine::trace_summary() {
+  TraceSummary r;
+  r.dropped = trace_dropped_;
+  for (int s = 0; s < kSlots; ++s)  // traced epilogues still deferred: their end point is not recorded yet
+    if (slots_[s].pending && slots_[s].trace >= 0)
+      throw std::runtime_error("trace_summary: a traced request's epilogue is not committed yet");
+  for (size_t i = 0; i < trace_used_; ++i) {
+    RequestTrace& t = trace_pool_[i];
+    FAN_HIP_CHECK(hipEventSynchronize(t.ev[kTpEpiEnd]));
+    float ms = 0.f;
+    for (int p = 1; p < kTpCount; ++p) {
+      FAN_HIP_CHECK(hipEventElapsedTime(&ms, t.ev[p - 1], t.ev[p]));
+      r.ms[p] += ms;
+    }
+    FAN_HIP_CHECK(hipEventElapsedTime(&ms, t.ev[kTpStart], t.ev[kTpCommEnd]));
+    r.comm_ms += ms;
+    FAN_HIP_CHECK(hipEventElapsedTime(&ms, t.ev[kTpStart], t.ev[kTpEpiEnd]));
+    r.total_ms += ms;
+    r.requests++;
+    r.logical_bytes += t.logical_bytes;
+    r.wire_bytes += t.wire_bytes;
+  }
+  return r;
 }
 
 std::string AllReduceEngine::diagnostics(int slot) const {
@@ -370,9 +454,9 @@ std::string AllReduceEngine::diagnostics(int slot) const {
   return os.str();
 }
 
-void AllReduceEngine::synchronize(int slot, double timeout_s) {
+void AllReduceEngine::synchronize(int slot, double timeout_s, uint32_t seq) {
   Slot& sl = slots_.at(slot);
-  if (sl.pending) commit(slot, false, nullptr);
+  if ((seq == 0 || seq == sl.seq) && sl.pending) commit_slot(sl, slot, false, nullptr);
   const double t0 = now_s();
   const double tmo = timeout_s > 0 ? timeout_s : cfg_.timeout_s;
   int spins = 0;
@@ -388,7 +472,7 @@ void AllReduceEngine::synchronize(int slot, double timeout_s) {
       }
     }
   } account{counters_, t0, spins};
-  while (!query(slot)) {
+  while (!query(slot, seq)) {
     if (++spins > 64) {
       std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 5));
       if (comm_ && (spins & 255) == 0) {

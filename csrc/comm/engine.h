@@ -58,6 +58,30 @@ struct EngineCounters {
   uint64_t host_spins = 0;     // done-word polls while waiting
   double device_ms = 0.0;      // summed device time of timed requests (lpbk_latency analogue)
   uint64_t timed_requests = 0;
+  uint64_t forced_commits = 0;  // deferred epilogues committed because their slot was needed (> kSlots deferred)
+};
+
+// Device-side request trace: GPU timestamps (timing events) at the phase boundaries of each request, the MI355X
+// counterpart of the NIC's per-state cycle counters (lpbk_latency and the stall_* attributions,
+// hw/all_reduce.sv:892-1085) and of get_all_reduce_latency (sw/mlp_mpi_example_f32.cpp:100-106). Points are
+// recorded on the stream the phase runs on; the ring schedule has no separate pack / exchange / reduce phases
+// (every hop fuses them), so its middle points coincide with the end of communication.
+enum TracePoint : int {
+  kTpStart = 0,   // request starts on the comm stream (producer done, previous request drained)
+  kTpPacked,      // pack / encode pass done (mesh)
+  kTpExchanged,   // all-to-all of the packed shards done (mesh)
+  kTpReduced,     // owner-shard reduce done (mesh)
+  kTpCommEnd,     // all-gather done: end of the communication phase
+  kTpEpiEnd,      // decode + SGD epilogue done
+  kTpCount
+};
+
+struct TraceSummary {
+  uint64_t requests = 0, dropped = 0;
+  int64_t logical_bytes = 0, wire_bytes = 0;
+  double ms[kTpCount] = {0, 0, 0, 0, 0, 0};  // ms[p] = summed time between point p-1 and p (ms[0] unused)
+  double comm_ms = 0.0;                       // summed kTpStart -> kTpCommEnd
+  double total_ms = 0.0;                      // summed kTpStart -> kTpEpiEnd
 };
 
 // Deferred epilogue of a request (decode + SGD), launched on the given stream at commit().
@@ -90,14 +114,22 @@ class AllReduceEngine {
   // Enqueue the deferred SGD epilogue; with `after_producer`, after everything currently enqueued on
   // `producer`. The flag is separate from the handle because the default (legacy null) stream IS nullptr:
   // torch's default stream hands us 0, and treating that as "no producer" skipped the ordering wait.
-  void commit(int slot, bool after_producer, hipStream_t producer);
-  void wait_stream(int slot, hipStream_t s);            // GPU-side wait
-  bool query(int slot);                                  // host: request done?
+  // `seq` (0: whoever holds the slot) names the request: a handle whose slot was since reused by a newer
+  // request never commits or waits on that newer request's behalf (its own epilogue was committed when the
+  // slot was reused, see submit()).
+  void commit(int slot, bool after_producer, hipStream_t producer, uint32_t seq = 0);
+  void wait_stream(int slot, hipStream_t s, uint32_t seq = 0);  // GPU-side wait
+  bool query(int slot, uint32_t seq = 0);                       // host: request done?
   uint32_t done_word(int slot) const { return flags_host_[slot * 16]; }  // last completed sequence number
   uint32_t slot_seq(int slot) const { return slots_.at(slot).seq; }
-  void synchronize(int slot, double timeout_s = -1.0);   // host: bounded wait (throws with diagnostics)
+  void synchronize(int slot, double timeout_s = -1.0, uint32_t seq = 0);  // host: bounded wait (throws)
   float latency_ms(int slot);
   void set_timing(bool on) { timing_ = on; }
+  // Request tracing (device timestamps per phase, see TracePoint): enabling resets the trace pool; requests
+  // beyond its capacity are counted as dropped. trace_summary() waits for the traced requests.
+  void set_tracing(bool on, int capacity = 1024);
+  bool tracing() const { return tracing_; }
+  TraceSummary trace_summary();
   // Side-stream engine: run each request's epilogue on the stream passed to commit() (after its communication
   // phase) instead of on the comm stream.
   void set_epilogue_on_producer(bool on) { epi_on_producer_ = on; }
@@ -119,7 +151,18 @@ class AllReduceEngine {
     hipStream_t epi_stream = nullptr;  // stream the epilogue was enqueued on (== stream unless epi_on_producer_)
     std::vector<EpiThunk> thunks;
     double t_issue = 0.0;
+    int trace = -1;  // index into trace_pool_ (-1: not traced)
   };
+  struct RequestTrace {
+    hipEvent_t ev[kTpCount] = {};
+    int64_t logical_bytes = 0, wire_bytes = 0;
+  };
+  // record trace point tp of the request being built on the stream its phases run on
+  void mark(int tp) {
+    trace_marked_ |= 1u << tp;
+    if (cur_trace_ >= 0) FAN_HIP_CHECK(hipEventRecord(trace_pool_[cur_trace_].ev[tp], run_stream_));
+  }
+  void commit_slot(Slot& sl, int slot, bool after_producer, hipStream_t producer);
   uint8_t* scratch(const std::string& key, size_t bytes);
   std::vector<EpiThunk> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
@@ -147,6 +190,12 @@ class AllReduceEngine {
   EngineCounters counters_;
   std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
   int epi_slot_ = 0;  // slot of the request being built
+  bool tracing_ = false;
+  std::vector<RequestTrace> trace_pool_;
+  size_t trace_used_ = 0;
+  uint64_t trace_dropped_ = 0;
+  int cur_trace_ = -1;  // trace of the request being built
+  unsigned trace_marked_ = 0;  // trace points the schedule of the request being built has recorded
   // Scratch that a deferred epilogue reads: per request slot, so a later request of the same size cannot
   // overwrite it before this request commits (the trainer commits every request at the end of backward).
   uint8_t* epi_scratch(const std::string& base, size_t bytes);

@@ -234,6 +234,7 @@ class CompressedAllReduce:
         self._scratch: dict = {}
         self._cur_slot = 0
         self._slot = 0
+        self._slot_owner: list = [None] * NUM_SLOTS  # last request issued on each slot
         self.fault = faults.FaultInjector.from_env()
         self.stats = {"requests": 0, "wire_bytes": 0, "logical_bytes": 0}
         # debug mode: every message travels with a checksum + the request sequence number,
@@ -327,6 +328,12 @@ class CompressedAllReduce:
     def _launch(self, comm_fn, name, L, defer=False, update_after=None) -> Handle:
         slot = self._slot
         self._slot = (slot + 1) % NUM_SLOTS
+        prev = self._slot_owner[slot]
+        if prev is not None and prev._pending is not None:
+            # more than NUM_SLOTS requests deferred: the slot's previous request must commit before its per-slot
+            # scratch is reused (ordered after everything enqueued so far on the producer stream)
+            prev.commit_after_current()
+            self.stats["forced_commits"] = self.stats.get("forced_commits", 0) + 1
         self._cur_slot = slot  # per-slot scratch of the request comm_fn builds
         self.stats["requests"] += 1
         self.stats["wire_bytes"] += self.wire_bytes(L)
@@ -334,6 +341,7 @@ class CompressedAllReduce:
         if not self.cuda or self.inline:
             thunks = comm_fn()
             h = Handle(self, slot, None, name, pending=thunks)
+            self._slot_owner[slot] = h
             return h if defer else h.commit()
         ready = self._event()
         ready.record(torch.cuda.current_stream(self.device))
@@ -348,6 +356,7 @@ class CompressedAllReduce:
             t_end = torch.cuda.Event(enable_timing=True)
             thunks = list(thunks) + [lambda: t_end.record(self.stream)]
         h = Handle(self, slot, None, name, pending=thunks)
+        self._slot_owner[slot] = h
         if t_start is not None:
             h._timing = (t_start, t_end)
         return h if defer else h.commit(update_after)

@@ -118,26 +118,32 @@ class DataParallelTrainer:
         m.act[0] = x
         t0 = time.perf_counter()
         with tracing.range("fwd"):
-            self._wait_updates()
             for i in range(m.L):
+                self._wait_layer(i)  # layer i's weights updated (reference: per-layer wait, sw:757-787)
                 m.forward_layer(i)
+            self.last_handle = None
         if self.profile:
             self._sync()
             self.times["fwd"] += time.perf_counter() - t0
 
-    def _wait_updates(self):
-        """Weights must be updated before they are read again. All requests of a step run in issue order
-        (L-1 .. 0) on the engine's single comm stream, so on GPU ONE wait on the last-issued handle covers
-        them all (each cross-stream wait costs a barrier packet on the compute queue)."""
-        if self.last_handle is None:
+    def _wait_layer(self, i: int):
+        """Layer i's weights must be updated before its forward reads them: a GPU-side wait on layer i's
+        request only (free when its epilogue already runs on this stream), so layer i's forward starts as soon
+        as ITS update lands rather than after the whole step's (reference: the host waits per layer request,
+        sw/mlp_mpi_example_f32.cpp:757-787)."""
+        h = self.pending[i]
+        if h is None:
             return
         if self.cuda:
-            self.last_handle.wait()
+            h.wait()
         else:
-            for h in self.pending:
-                if h is not None:
-                    h.synchronize()
-        self.pending = [None] * self.m.L
+            h.synchronize()
+        self.pending[i] = None
+
+    def _wait_updates(self):
+        """Every outstanding update has landed (GPU-side order on the current stream; host waits on CPU)."""
+        for i in range(self.m.L):
+            self._wait_layer(i)
         self.last_handle = None
 
     def backward_pass(self, labels: torch.Tensor):

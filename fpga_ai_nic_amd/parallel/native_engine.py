@@ -38,48 +38,54 @@ class NativeHandle:
         self.t_issue = time.time()
         self._pending = pending
 
+    def _superseded(self) -> bool:
+        return self.engine.C.slot_seq(self.slot) != self.seq
+
+    @property
+    def pending(self) -> bool:
+        """Epilogue not yet enqueued (a request whose slot was reused was committed by the engine then)."""
+        if self._pending and self._superseded():
+            self._pending = False
+        return self._pending
+
     def commit(self, update_after=None):
         """Enqueue the deferred epilogue; with ``update_after`` (any truthy value, e.g. an event recorded on
         the current stream) it is ordered after everything enqueued so far on the current stream."""
-        if self._pending:
-            self.engine.C.commit(self.slot, update_after is not None)
+        if self.pending:
+            self.engine.C.commit(self.slot, update_after is not None, self.seq)
             self._pending = False
         return self
 
     def commit_after_current(self):
-        if self._pending:
-            self.engine.C.commit(self.slot, True)
+        if self.pending:
+            self.engine.C.commit(self.slot, True, self.seq)
             self._pending = False
         return self
 
     def done(self) -> bool:
-        if self._pending:
+        if self.pending:
             return False
-        C = self.engine.C
-        if self.engine.inline or self.engine.epilogue_on_producer:
-            # completion is the slot's done event (a reused slot holds a later request on the same stream order)
-            return C.query(self.slot)
-        return ((C.done_word(self.slot) - self.seq) & 0xFFFFFFFF) < (1 << 31)
+        return bool(self.engine.C.query(self.slot, self.seq))
 
     def wait(self, stream=None):
         self.commit_after_current()
         if stream is None:
-            self.engine.C.wait_stream(self.slot)
+            self.engine.C.wait_stream(self.slot, self.seq)
         else:
             with torch.cuda.stream(stream):
-                self.engine.C.wait_stream(self.slot)
+                self.engine.C.wait_stream(self.slot, self.seq)
 
     def synchronize(self, timeout: float | None = None):
         self.commit_after_current()
         if self.done():
             return
         try:
-            self.engine.C.synchronize(self.slot, -1.0 if timeout is None else float(timeout))
+            self.engine.C.synchronize(self.slot, -1.0 if timeout is None else float(timeout), self.seq)
         except RuntimeError as e:
             raise CommTimeoutError(f"all-reduce '{self.name}': {e}") from e
 
     def latency_ms(self) -> float | None:
-        if self._pending or self.engine.C.slot_seq(self.slot) != self.seq:
+        if self._pending or self._superseded():
             return None
         v = self.engine.C.latency_ms(self.slot)
         return None if v < 0 else v
@@ -231,6 +237,17 @@ class NativeAllReduce:
 
     def reset_counters(self):
         self.C.reset_counters()
+
+    def trace(self, on: bool = True, capacity: int = 1024):
+        """Start (reset) or stop device-side request tracing: GPU timestamps at every phase boundary of each
+        request (pack / all-to-all / reduce / all-gather / epilogue), see :meth:`trace_summary`."""
+        self.C.set_tracing(bool(on), int(capacity))
+
+    def trace_summary(self) -> dict:
+        """Per-phase device time (ms) summed over the requests traced since :meth:`trace` — the NIC's per-state
+        cycle counters (hw/all_reduce.sv:892-1085) — plus ``comm_ms`` (request start to end of the all-gather)
+        and the traced requests' logical / wire bytes. Waits for the traced requests."""
+        return dict(self.C.trace_summary())
 
 
 __all__ = ["NativeAllReduce", "NativeHandle", "NUM_SLOTS"]

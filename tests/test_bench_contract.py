@@ -51,3 +51,21 @@ def test_bench_json_contract(world, tmp_path):
     # value is the whole-job aggregate: global batch x steps / (max-over-ranks) elapsed time
     assert rec["value"] == pytest.approx(cfg["global_batch"] / (rec["ms_per_step"] / 1e3), rel=1e-2)
     assert rec["extra"]["final_loss"] > 0
+
+
+def test_bench_self_launches_ranks(tmp_path):
+    """``python bench.py --gpus 2`` with no torch.distributed environment starts its 2 ranks itself (a
+    torch.distributed.run child; the parent never touches the GPU) and still prints exactly one JSON line."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--mb-per-gpu", "16", "--ref-mb", "8"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 32
+    ref = rec["extra"]["mb8"]
+    assert ref["global_batch"] == 16 and ref["samples_per_s"] > 0
+    assert "effective_allreduce_algo_bw_GBps" not in rec["extra"]

@@ -147,3 +147,42 @@ def test_deferred_same_size_requests_keep_their_own_result(N, algo):
 
 def fabric_run(N, fn):
     return ThreadFabric(N, timeout_s=60).run(fn)
+
+
+@pytest.mark.parametrize("N", [1, 2])
+@pytest.mark.parametrize("algo", ["mesh", "ring"])
+def test_more_deferred_requests_than_slots(N, algo):
+    """A 10-layer model (the reference run.sh workload) defers 10 same-size requests before committing: more
+    than the 8 request slots. The 9th request reuses slot 0 — the engine must commit request 1 first (its
+    per-slot scratch is about to be overwritten) so every request still applies ITS OWN reduced gradient."""
+    n, R = 1000, 10
+    rng = np.random.default_rng(11 + N)
+    grads = [[rng.standard_normal(n).astype(np.float32) * (1 + r + b) for r in range(N)] for b in range(R)]
+    w0 = rng.standard_normal(n).astype(np.float32)
+
+    def fn(t):
+        eng = CompressedAllReduce(t, codec="bfp_rne", algo=algo, device="cpu")
+        L = eng.layout(n)
+        outs = []
+        for deferred in (True, False):
+            ws, hs = [], []
+            for b in range(R):
+                g = torch.zeros(L.n_pad)
+                g[:n] = torch.from_numpy(grads[b][t.rank])
+                w = torch.zeros(L.n_pad)
+                w[:n] = torch.from_numpy(w0)
+                h = eng.allreduce_sgd(g, w, None, None, n_valid=n, lr=0.5, defer=deferred)
+                if not deferred:
+                    h.synchronize()
+                ws.append(w)
+                hs.append(h)
+            for h in hs:
+                h.commit()
+                h.synchronize()
+            outs.append([w.numpy().copy() for w in ws])
+        return outs, eng.stats.get("forced_commits", 0)
+
+    for (deferred, immediate), forced in fabric_run(N, fn):
+        assert forced == R - 8
+        for a, b in zip(deferred, immediate):
+            assert np.array_equal(a, b)

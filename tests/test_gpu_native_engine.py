@@ -162,7 +162,10 @@ def _train_forced(on_producer, sizes=(256, 512, 256, 128), mb=256, steps=4):
 
 # (512, 512, 512, 512): three buckets of the same size -- the deferred epilogues must not share a gathered
 # wire buffer (scratch is keyed per request slot)
-_FORCED_CASES = [((256, 512, 256, 128), 256), ((512, 512, 512, 512), 256), ((1024, 4096, 4096, 1024), 2048)]
+# (256,)*11: ten layers, more deferred requests than the engine's 8 slots (the reference run.sh workload is 10
+# layers): the 9th and 10th submits commit the oldest requests first
+_FORCED_CASES = [((256, 512, 256, 128), 256), ((512, 512, 512, 512), 256), ((1024, 4096, 4096, 1024), 2048),
+                 ((256,) * 11, 256)]
 
 
 @pytest.mark.parametrize("sizes,mb", _FORCED_CASES)
@@ -224,3 +227,50 @@ def test_engine_perf_counters(force):
     assert c["wire_bytes"] == 3 * eng.wire_bytes(L)
     assert c["timed_requests"] == 3 and c["device_ms"] > 0
     assert c["host_wait_s"] >= 0 and c["host_waits"] <= 3
+
+
+def test_superseded_handle_never_acts_for_the_newer_request():
+    """10 deferred requests on 8 slots: requests 1 and 2 are committed by the engine when requests 9 and 10 reuse
+    their slots. Their old handles then report completion of THEIR request and never commit (or wait on behalf
+    of) the newer pending request that now holds the slot."""
+    eng = NativeAllReduce(_native_transport(), codec="bfp_rne", force_comm=True)
+    eng.reset_counters()
+    n = 1 << 14
+    L = eng.layout(n)
+    grad = torch.randn(L.n_pad, device="cuda")
+    ws = [torch.zeros(L.n_pad, device="cuda") for _ in range(10)]
+    hs = [eng.allreduce_sgd(grad, ws[i], n_valid=n, lr=0.1, defer=True) for i in range(10)]
+    assert eng.counters()["forced_commits"] == 2
+    assert not hs[0].pending and hs[8].pending and hs[0].slot == hs[8].slot
+    hs[0].wait()
+    hs[0].synchronize(30)
+    assert hs[0].done()
+    assert hs[8].pending, "the old handle committed the newer request"
+    for h in hs:
+        h.commit_after_current()
+    for h in hs:
+        h.synchronize(30)
+    torch.cuda.synchronize()
+    assert all(torch.equal(w, ws[0]) for w in ws) and ws[0].abs().sum() > 0
+
+
+def test_request_trace_phases():
+    """Device-side request trace (the NIC's per-state cycle counters): per-phase GPU time of every request in the
+    trace window; phases add up to the request's total, communication is start -> end of the all-gather."""
+    eng = NativeAllReduce(_native_transport(), codec="bfp_rne", force_comm=True)
+    n = 1 << 20
+    L = eng.layout(n)
+    grad = torch.randn(L.n_pad, device="cuda")
+    w = torch.zeros(L.n_pad, device="cuda")
+    eng.allreduce_sgd(grad, w, n_valid=n, lr=0.1).synchronize(30)  # scratch allocated outside the window
+    eng.trace(True)
+    for _ in range(4):
+        eng.allreduce_sgd(grad, w, n_valid=n, lr=0.1)
+    t = eng.trace_summary()
+    eng.trace(False)
+    assert t["requests"] == 4 and t["dropped"] == 0
+    assert t["logical_bytes"] == 4 * n * 4
+    phases = t["pack_ms"] + t["exchange_ms"] + t["reduce_ms"] + t["gather_ms"]
+    assert t["comm_ms"] > 0 and abs(phases - t["comm_ms"]) < 1e-3 + 1e-3 * t["comm_ms"]
+    assert abs(phases + t["epilogue_ms"] - t["total_ms"]) < 1e-3 + 1e-3 * t["total_ms"]
+    assert min(t[k] for k in ("pack_ms", "exchange_ms", "reduce_ms", "gather_ms", "epilogue_ms")) >= 0
