@@ -48,6 +48,19 @@ def ref_shapes(mb: int = 5376, c: int = 2048):
     ]
 
 
+def ragged_shapes():
+    """Shapes that are not tile multiples: the reference workload's per-rank batch at 8 / 4 ranks (global MB 5376,
+    sw/run.sh:16) and its 448-row sweep (sw/run.sh:24-29) on 2048-wide layers, plus 1000-wide layers."""
+    out = []
+    for mb in (672, 1344, 448):
+        out += [(f"r{mb}_fwd", mb, 2048, 2048, False, False, G.EPI_NONE),
+                (f"r{mb}_bwdd", mb, 2048, 2048, False, True, G.EPI_NONE),
+                (f"r{mb}_bwdw", 2048, 2048, mb, True, False, G.EPI_NONE)]
+    out += [("w1000_fwd", 8192, 1000, 1000, False, False, G.EPI_NONE),
+            ("w1000_bwdw", 1000, 1000, 8192, True, False, G.EPI_NONE)]
+    return out
+
+
 def bert_shapes(tokens: int):
     """BERT-base encoder-layer backward GEMMs (BASELINE config 5) at ``tokens`` rows per GPU."""
     import sys as _s
@@ -76,14 +89,15 @@ def main():
     ap.add_argument("--shapes", default="")
     ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
     ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
-    ap.add_argument("--set", default="mlp", choices=["mlp", "bert", "ref"])
+    ap.add_argument("--set", default="mlp", choices=["mlp", "bert", "ref", "ragged"])
     ap.add_argument("--ab", action="store_true", help="also time the one-role main loop (ping-pong off)")
     ap.add_argument("--epi-arms", action="store_true",
                     help="bwd-weight shapes: also time the fused bias-gradient (colsum) and BFP wire epilogues")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
-    shapes = mlp_shapes(a.mb) if a.set == "mlp" else bert_shapes(a.mb) if a.set == "bert" else ref_shapes()
+    shapes = (mlp_shapes(a.mb) if a.set == "mlp" else bert_shapes(a.mb) if a.set == "bert" else
+              ragged_shapes() if a.set == "ragged" else ref_shapes())
     for name, M, N, K, a_t, b_t, epi in shapes:
         if a.shapes and name not in a.shapes.split(","):
             continue

@@ -20,6 +20,11 @@
 //     (f32) / 8-B (bf16) row segments, with bias / ReLU / ReLU-mask (bwd-data) / accumulate fused.
 //   * split-K: K is split over workgroups, f32 partial slabs + an ordered (deterministic) reduce kernel
 //     that applies the same epilogue.
+//   * any M, N, K that are multiples of 8 (reference: libxsmm falls back to the whole dimension when MB or C does
+//     not divide the blocking, sw/mlp_mpi_example_f32.cpp:498-506): tiles are ceil-divided; a workgroup whose
+//     tile crosses an operand edge (a uniform flag) stages every out-of-range 16-B chunk from a zero page
+//     (global_load_lds has no predicate, so the lane reads zeros instead), so the MFMAs accumulate exact zeros
+//     there, and its epilogue stores only in-range elements. Interior tiles run the unpredicated path.
 #pragma once
 #include "bfp/bfp_format.h"
 #include "gemm/gemm.h"
@@ -52,6 +57,11 @@ constexpr int kStampWG = 8, kStampKT = 64, kStampPts = 5;
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
+// Zero page for the edge tiles' out-of-range operand chunks (one per code object; zero-initialised).
+static __device__ __attribute__((aligned(256))) uint4 g_gemm_zero16[16];
+
+__host__ __device__ constexpr int cdiv_i(int a, int b) { return (a + b - 1) / b; }
+
 template <int OUTER, int NT>
 struct OpTile {
   static constexpr int BYTES = OUTER * BK * 2;
@@ -61,33 +71,40 @@ struct OpTile {
 };
 
 // Issue glds instruction i (of OpTile::GLDS) of one operand tile (outer extent OUTER from o0, k extent 64 from
-// k0) with NT threads: this wave's 1 KiB piece of it.
-template <bool KCONTIG, int OUTER, int NT>
+// k0) with NT threads: this wave's 1 KiB piece of it. EDGE: chunks at outer >= o_lim or k >= k_lim (both
+// multiples of 8, so a 16-B chunk is wholly in or out) load the zero page instead.
+template <bool KCONTIG, int OUTER, int NT, bool EDGE = false>
 __device__ __forceinline__ void stage_one(const bf16_t* __restrict__ g, int64_t ld, int o0, int k0, char* lds,
-                                          int wave, int lane, int i) {
+                                          int wave, int lane, int i, int o_lim = 0, int k_lim = 0) {
   using T = OpTile<OUTER, NT>;
   const int t = wave * 64 + lane;
   const bf16_t* src;
+  bool out = false;
   if (KCONTIG) {
     const int row = i * (T::IB / 128) + (t >> 3);  // rows of 128 B
     const int c = (t & 7) ^ ((row >> 1) & 7);
     src = g + (int64_t)(o0 + row) * ld + k0 + c * 8;
+    if (EDGE) out = o0 + row >= o_lim || k0 + c * 8 >= k_lim;
   } else {
     const int half = i / T::PER_HALF;                               // 128-column half
     const int krow = (i % T::PER_HALF) * (T::IB / 256) + (t >> 4);  // k-rows of 256 B
     const int cs = t & 15;
     const int blk = (cs >> 1) ^ mn_swz(krow);
-    src = g + (int64_t)(k0 + krow) * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8;
+    const int col = o0 + half * 128 + blk * 16 + (cs & 1) * 8;
+    src = g + (int64_t)(k0 + krow) * ld + col;
+    if (EDGE) out = k0 + krow >= k_lim || col >= o_lim;
   }
+  if (EDGE && out) src = reinterpret_cast<const bf16_t*>(g_gemm_zero16);
   glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(lds + i * T::IB + wave * 1024)));
 }
 
 // Stage one whole operand tile.
-template <bool KCONTIG, int OUTER, int NT>
+template <bool KCONTIG, int OUTER, int NT, bool EDGE = false>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int64_t ld, int o0, int k0, char* lds,
-                                           int wave, int lane) {
+                                           int wave, int lane, int o_lim = 0, int k_lim = 0) {
 #pragma unroll
-  for (int i = 0; i < OpTile<OUTER, NT>::GLDS; ++i) stage_one<KCONTIG, OUTER, NT>(g, ld, o0, k0, lds, wave, lane, i);
+  for (int i = 0; i < OpTile<OUTER, NT>::GLDS; ++i)
+    stage_one<KCONTIG, OUTER, NT, EDGE>(g, ld, o0, k0, lds, wave, lane, i, o_lim, k_lim);
 }
 
 template <bool KCONTIG>
@@ -251,16 +268,16 @@ __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict_
 // encodes the bias segment of the [W | b] bucket (its 16-column group is lanes 0..15).
 template <int NJ, int WTN, int EPI, bool SPLIT>
 __device__ __forceinline__ void colsum_finish(float (&cs)[NJ], int lane, int col0, float* __restrict__ out,
-                                              const WireOut& wo) {
+                                              const WireOut& wo, int N) {
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     float v = cs[j];
     v += __shfl_xor(v, 16);
     v += __shfl_xor(v, 32);
     const int col = col0 + j * 16 + (lane & 15);
-    if (lane < 16) out[col] = v;
+    if (lane < 16 && col < N) out[col] = v;
     if constexpr (EPI == kEpiWire && !SPLIT) {
-      if (wo.bias_off > 0) {
+      if (wo.bias_off > 0 && col0 + j * 16 < N) {  // N % 16 == 0: the 16-column group is wholly in range
         uint32_t mx = __float_as_uint(v) & 0x7FFFFFFFu;
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
@@ -284,7 +301,7 @@ template <int MI, int NJ, int WTN, int EPI, typename TC, bool ACCUM, bool SPLIT>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* smem, int wave, int lane, int row0,
                                            int col0, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                            const TC* __restrict__ aux, int64_t ldaux, int M, int N, int ksplit,
-                                           float* __restrict__ ws, const WireOut& wo) {
+                                           float* __restrict__ ws, const WireOut& wo, bool mn_edge = false) {
   constexpr int EW = WTN + 4;  // staged row stride in floats (16-B aligned, breaks bank aliasing)
   float* stg = reinterpret_cast<float*>(smem) + wave * (16 * EW);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
@@ -312,7 +329,8 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
             const float4 q = *reinterpret_cast<const float4*>(stg + rr * EW + cc + u);
             v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
           }
-          wire_epi16(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr, col0 + cc);
+          if (!mn_edge || (row0 + i * 16 + rr < M && col0 + cc < N))
+            wire_epi16(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr, col0 + cc);
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -326,6 +344,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
       float v[4] = {q.x, q.y, q.z, q.w};
       const int row = row0 + i * 16 + rr;
       const int col = col0 + cc;
+      if (mn_edge && (row >= M || col >= N)) continue;  // N % 8 == 0: a 4-column chunk is wholly in or out
       if (SPLIT) {
         float* slab = ws + (int64_t)ksplit * M * N;
         *reinterpret_cast<float4*>(slab + (int64_t)row * N + col) = q;
@@ -355,8 +374,9 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
   static_assert(WM * WN == 8 || WM * WN == 4, "4 or 8 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tiles_n = N / BN;
-  const int tiles = (M / BM) * tiles_n;
+  const int tiles_n = cdiv_i(N, BN);
+  const int tiles_m = cdiv_i(M, BM);
+  const int tiles = tiles_m * tiles_n;
   const int nwg = tiles * split_k;
   const int wg = xcd_remap(blockIdx.x, nwg);
   const int tile = wg % tiles;
@@ -364,16 +384,20 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
   // 2-D grouped order: consecutive tiles (one XCD's contiguous run after xcd_remap) walk GM tile-rows
   // before moving right, so an XCD works on a compact GM x (run/GM) block of C and its L2 holds
   // fewer distinct A/B panel slices per k-step.
-  const int tiles_m = M / BM;
   const int GM = tiles_m >= 4 ? 4 : tiles_m;
   const int grp = tile / (GM * tiles_n);
   const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
   const int in_grp = tile % (GM * tiles_n);
   const int m0 = (grp * GM + in_grp % gm) * BM;
   const int n0 = (in_grp / gm) * BN;
-  const int k_per = K / split_k;
-  const int kbeg = ksplit * k_per;
-  const int nk = k_per / BK;
+  // K-tiles of this split (a ragged K: the last split is shorter, the last K-tile is zero-filled past K)
+  const int nkt = cdiv_i(K, BK);
+  const int kt_per = cdiv_i(nkt, split_k);
+  const int kt0 = ksplit * kt_per;
+  const int nk = max(0, min(nkt, kt0 + kt_per) - kt0);
+  const int kbeg = kt0 * BK;
+  const bool mn_edge = m0 + BM > M || n0 + BN > N;
+  const bool edge = mn_edge || (kt0 + nk) * BK > K;  // uniform: predicated staging for this workgroup
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -392,8 +416,13 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
 
   auto issue_stage = [&](int kt_stage, int buf) {
     char* st = smem + buf * STAGE;
-    stage_tile<AK, BM, NT>(A, lda, m0, kbeg + kt_stage * BK, st, wave, lane);
-    stage_tile<BKC, BN, NT>(B, ldb, n0, kbeg + kt_stage * BK, st + A_BYTES, wave, lane);
+    if (edge) {
+      stage_tile<AK, BM, NT, true>(A, lda, m0, kbeg + kt_stage * BK, st, wave, lane, M, K);
+      stage_tile<BKC, BN, NT, true>(B, ldb, n0, kbeg + kt_stage * BK, st + A_BYTES, wave, lane, N, K);
+    } else {
+      stage_tile<AK, BM, NT>(A, lda, m0, kbeg + kt_stage * BK, st, wave, lane);
+      stage_tile<BKC, BN, NT>(B, ldb, n0, kbeg + kt_stage * BK, st + A_BYTES, wave, lane);
+    }
   };
 
   // Register budget per lane: 4 waves = 1 wave/SIMD (512 VGPR+AGPR), 8 waves = 2 waves/SIMD (256).
@@ -427,12 +456,22 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
       // fragment reads per wave and K-tile) 3-10 % faster; with a K-contiguous A 12-25 % slower, so only the
       // bwd-weight layout uses it (launch_main).
       if (pf && wave < 4) {
-        stage_tile<AK, BM, 256>(A, lda, m0, pk, pst, wave, lane);
-        stage_tile<BKC, BN, 256>(B, ldb, n0, pk, pst + A_BYTES, wave, lane);
+        if (edge) {
+          stage_tile<AK, BM, 256, true>(A, lda, m0, pk, pst, wave, lane, M, K);
+          stage_tile<BKC, BN, 256, true>(B, ldb, n0, pk, pst + A_BYTES, wave, lane, N, K);
+        } else {
+          stage_tile<AK, BM, 256>(A, lda, m0, pk, pst, wave, lane);
+          stage_tile<BKC, BN, 256>(B, ldb, n0, pk, pst + A_BYTES, wave, lane);
+        }
       }
     } else if (pf) {
-      stage_tile<AK, BM, NT>(A, lda, m0, pk, pst, wave, lane);
-      stage_tile<BKC, BN, NT>(B, ldb, n0, pk, pst + A_BYTES, wave, lane);
+      if (edge) {
+        stage_tile<AK, BM, NT, true>(A, lda, m0, pk, pst, wave, lane, M, K);
+        stage_tile<BKC, BN, NT, true>(B, ldb, n0, pk, pst + A_BYTES, wave, lane, N, K);
+      } else {
+        stage_tile<AK, BM, NT>(A, lda, m0, pk, pst, wave, lane);
+        stage_tile<BKC, BN, NT>(B, ldb, n0, pk, pst + A_BYTES, wave, lane);
+      }
     }
     FAN_STAMP(3);
     const char* sa = smem + (kt % S) * STAGE;
@@ -494,10 +533,10 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
 
   if (do_colsum)
     colsum_finish<NJ, WTN, EPI, SPLIT>(cs, lane, n0 + wn * WTN, SPLIT ? ws + (int64_t)split_k * M * N + (int64_t)ksplit * N
-                                                                      : colsum, wo);
+                                                                      : colsum, wo, N);
   __syncthreads();  // all waves done reading the operand ring
   store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
-                                                 aux, ldaux, M, N, ksplit, ws, wo);
+                                                 aux, ldaux, M, N, ksplit, ws, wo, mn_edge);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -684,7 +723,7 @@ __global__ void __launch_bounds__(512, 2)
 
   if (do_colsum)
     colsum_finish<NJ, WTN, EPI, SPLIT>(cs, lane, n0 + wcol, SPLIT ? ws + (int64_t)split_k * M * N + (int64_t)ksplit * N
-                                                                   : colsum, wo);
+                                                                   : colsum, wo, N);
   store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wrow, n0 + wcol, C, ldc, bias, aux,
                                                  ldaux, M, N, ksplit, ws, wo);
 }
@@ -780,9 +819,10 @@ inline bool use_pingpong() { return gemm_pingpong_flag().load(std::memory_order_
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
 void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
-  const int grid = (a.M / BM) * (a.N / BN) * sk;
+  const int grid = cdiv_i(a.M, BM) * cdiv_i(a.N, BN) * sk;
   if constexpr (BM == 256 && BN == 256 && WM * WN == 8) {
-    if (use_pingpong()) {
+    // the staggered loop has no edge path: aligned shapes only
+    if (use_pingpong() && a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto k = gemm_pp_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT>;
       FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));

@@ -81,9 +81,49 @@ static const EnvPlans& env_plans() {
   return ep;
 }
 
+// Shapes that are not multiples of the tile (any M, N, K that are multiples of 8, e.g. the reference workload's
+// 672 or 1344 rows per rank at 8 or 4 ranks): ceil-divided tiles with zero-filled edges. Take the largest tile
+// that still gives one workgroup per CU and pads each dimension by at most ~15 %, else 128x128; split K over
+// the CUs when even 128x128 tiles leave more than half of them idle (ragged splits are allowed).
+static GemmPlan plan_ragged(int M, int N, int K, int split_k, int tile_bm, int tile_bn) {
+  GemmPlan p{0, 0, 1, kDefaultWaves};
+  const int cand[4][2] = {{256, 256}, {128, 256}, {256, 128}, {128, 128}};
+  auto pad_ok = [](int x, int b) { return (int64_t)((x + b - 1) / b) * b * 100 <= (int64_t)x * 115; };
+  int best = 3;
+  for (int c = 0; c < 4; ++c) {
+    const int bm = cand[c][0], bn = cand[c][1];
+    if (tile_bm > 0) {
+      if (bm == tile_bm && bn == tile_bn) best = c;
+      continue;
+    }
+    const int tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    if (tiles >= kNumCU && pad_ok(M, bm) && pad_ok(N, bn)) {
+      best = c;
+      break;
+    }
+  }
+  p.bm = cand[best][0];
+  p.bn = cand[best][1];
+  const int tiles = ((M + p.bm - 1) / p.bm) * ((N + p.bn - 1) / p.bn);
+  const int nkt = (K + BK - 1) / BK;
+  int sk = 1;
+  if (split_k > 0) {
+    sk = split_k;
+    if (sk > nkt) return GemmPlan{0, 0, 1, kDefaultWaves};
+  } else if (tiles * 2 <= kNumCU) {
+    while (tiles * sk < kNumCU && sk < 8 && nkt / (sk * 2) >= 8) sk *= 2;
+  }
+  p.split_k = sk;
+  return p;
+}
+
 GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn, int tile_waves) {
   GemmPlan p{0, 0, 1, 8};
-  if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % BK) return p;
+  if (M <= 0 || N <= 0 || K <= 0 || M % 8 || N % 8 || K % 8) return p;
+  if (tile_bm != 0 && ((tile_bm != 128 && tile_bm != 256) || (tile_bn != 128 && tile_bn != 256))) return p;
+  if (M % 128 || N % 128 || K % BK ||
+      (tile_bm > 0 && (M % tile_bm || N % tile_bn)) || (split_k > 1 && K % (BK * split_k)))
+    return plan_ragged(M, N, K, split_k, tile_bm, tile_bn);
   if (tile_bm == 0 && split_k <= 0) {
     for (const TunedPlan& t : env_plans().plans) {
       if (t.M == M && t.N == N && t.K == K && M % t.bm == 0 && N % t.bn == 0 && K % (BK * t.sk) == 0) {
@@ -167,7 +207,7 @@ bool gemm_bf16_supported(const GemmArgs& a) {
   if (p.split_k > 1 && a.workspace == nullptr) return false;
   if (a.colsum && a.b_kcontig) return false;
   if (a.epilogue == kEpiWire) {
-    if (a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire) return false;
+    if (a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire || a.N % 16) return false;
     if (a.wire_shard <= 0 || a.wire_shard % 256 || a.ldc % 16) return false;
     if (a.wire_codec != kBfpTrunc && a.wire_codec != kBfpRne) return false;
     if ((int64_t)a.M * a.ldc + a.N >= (int64_t(1) << 31)) return false;
@@ -176,7 +216,7 @@ bool gemm_bf16_supported(const GemmArgs& a) {
 }
 
 void launch_gemm_bf16(const GemmArgs& a, hipStream_t s) {
-  FAN_CHECK(gemm_bf16_supported(a), "gemm_bf16: unsupported shape/layout (need M,N % 128 == 0, K % 64 == 0)");
+  FAN_CHECK(gemm_bf16_supported(a), "gemm_bf16: unsupported shape/layout (need M, N, K % 8 == 0)");
   const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn, a.tile_waves);
   if (a.a_kcontig && a.b_kcontig) launch_tile<true, true>(a, p.bm, p.bn, p.waves, p.split_k, s);
   else if (a.a_kcontig && !a.b_kcontig) launch_tile<true, false>(a, p.bm, p.bn, p.waves, p.split_k, s);

@@ -9,6 +9,9 @@
 //     b ^ ((k>>2)&3); a fragment is 4 ds_read_b32 (lanes of the 4 k-row groups hit 4 disjoint bank quarters).
 // Within each 16-wide k chunk lane l feeds k = 4*(l>>4) + i to MFMA i (a consistent permutation of the k order
 // for A and B).
+// Any M, N, K that are multiples of 8: tiles are ceil-divided; a workgroup whose tile crosses an operand edge stages
+// its out-of-range 16-B chunks from a zero page and stores only in-range elements (the reference's libxsmm
+// blocking falls back to whole dimensions, sw/mlp_mpi_example_f32.cpp:498-506, so any MB / C works there).
 #include "gemm/gemm.h"
 #include "gemm/glds.h"
 
@@ -25,22 +28,29 @@ constexpr int LDS_BYTES = 2 * STAGE_BYTES;
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
 
-template <bool KCONTIG>
+static __device__ __attribute__((aligned(256))) uint4 g_f32_zero16[16];  // zero page for edge-tile chunks
+
+// EDGE: 16-B chunks at outer >= o_lim or k >= k_lim (multiples of 4 floats) load the zero page instead.
+template <bool KCONTIG, bool EDGE = false>
 __device__ __forceinline__ void stage(const float* __restrict__ g, int64_t ld, int o0, int k0, char* tile, int wave,
-                                      int lane) {
+                                      int lane, int o_lim = 0, int k_lim = 0) {
   const int t = wave * 64 + lane;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float* src;
+    bool out = false;
     if (KCONTIG) {
       const int row = i * 32 + (t >> 3);
       const int c = (t & 7) ^ swz(row);
       src = g + (int64_t)(o0 + row) * ld + k0 + c * 4;
+      if (EDGE) out = o0 + row >= o_lim || k0 + c * 4 >= k_lim;
     } else {
       const int krow = i * 8 + (t >> 5);
       const int col = ((t & 31) * 4) ^ (((krow >> 2) & 3) << 4);
       src = g + (int64_t)(k0 + krow) * ld + o0 + col;
+      if (EDGE) out = k0 + krow >= k_lim || o0 + col >= o_lim;
     }
+    if (EDGE && out) src = reinterpret_cast<const float*>(g_f32_zero16);
     glds16((const void*)src, __builtin_amdgcn_readfirstlane(lds_addr_of(tile + i * 4096 + wave * 1024)));
   }
 }
@@ -74,14 +84,25 @@ __global__ void __launch_bounds__(NT, 2)
                     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, const float* __restrict__ aux,
                     int64_t ldaux, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tiles_n = N / BN;
-  const int nwg = (M / BM) * tiles_n;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int nwg = ((M + BM - 1) / BM) * tiles_n;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nk = K / BK;
+  const int nk = (K + BK - 1) / BK;
+  const bool mn_edge = m0 + BM > M || n0 + BN > N;
+  const bool edge = mn_edge || K % BK;  // uniform: predicated staging for this workgroup
+  auto stage_ab = [&](int k0, char* dst) {
+    if (edge) {
+      stage<AK, true>(A, lda, m0, k0, dst, wave, lane, M, K);
+      stage<BKC, true>(B, ldb, n0, k0, dst + TILE_BYTES, wave, lane, N, K);
+    } else {
+      stage<AK>(A, lda, m0, k0, dst, wave, lane);
+      stage<BKC>(B, ldb, n0, k0, dst + TILE_BYTES, wave, lane);
+    }
+  };
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -89,8 +110,7 @@ __global__ void __launch_bounds__(NT, 2)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage<AK>(A, lda, m0, 0, smem, wave, lane);
-  stage<BKC>(B, ldb, n0, 0, smem + TILE_BYTES, wave, lane);
+  stage_ab(0, smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
@@ -98,9 +118,7 @@ __global__ void __launch_bounds__(NT, 2)
     char* sa = smem + cur * STAGE_BYTES;
     char* sb = sa + TILE_BYTES;
     if (kt + 1 < nk) {
-      char* na = smem + (cur ^ 1) * STAGE_BYTES;
-      stage<AK>(A, lda, m0, (kt + 1) * BK, na, wave, lane);
-      stage<BKC>(B, ldb, n0, (kt + 1) * BK, na + TILE_BYTES, wave, lane);
+      stage_ab((kt + 1) * BK, smem + (cur ^ 1) * STAGE_BYTES);
     }
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
@@ -124,12 +142,14 @@ __global__ void __launch_bounds__(NT, 2)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + wn * 64 + j * 16 + col_l;
+    if (mn_edge && col >= N) continue;
     const float bv = (EPI == kEpiBias || EPI == kEpiBiasRelu) ? bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * 64 + i * 16 + row_l + r;
+        if (mn_edge && row >= M) continue;
         float v = acc[i][j][r] + bv;
         if (EPI == kEpiBiasRelu) v = fmaxf(v, 0.f);
         if (EPI == kEpiReluMask) v = aux[(int64_t)row * ldaux + col] > 0.f ? v : 0.f;
@@ -142,7 +162,7 @@ __global__ void __launch_bounds__(NT, 2)
 
 template <bool AK, bool BKC>
 void launch_layout(const GemmArgs& a, hipStream_t s) {
-  const int grid = (a.M / BM) * (a.N / BN);
+  const int grid = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
 #define FAN_F32_CASE(E)                                                                                       \
   case E:                                                                                                     \
     if (a.accumulate)                                                                                         \
@@ -168,7 +188,7 @@ void launch_layout(const GemmArgs& a, hipStream_t s) {
 
 bool gemm_f32_supported(const GemmArgs& a) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
-  if (a.M % BM || a.N % BN || a.K % BK) return false;
+  if (a.M % 8 || a.N % 8 || a.K % 8) return false;
   if (a.lda % 4 || a.ldb % 4) return false;
   if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return false;
   if (a.c_bf16 || a.split_k > 1) return false;
@@ -176,7 +196,7 @@ bool gemm_f32_supported(const GemmArgs& a) {
 }
 
 void launch_gemm_f32(const GemmArgs& a, hipStream_t s) {
-  FAN_CHECK(gemm_f32_supported(a), "gemm_f32: unsupported shape/layout (need M,N % 128 == 0, K % 32 == 0)");
+  FAN_CHECK(gemm_f32_supported(a), "gemm_f32: unsupported shape/layout (need M, N, K % 8 == 0)");
   if (a.a_kcontig && a.b_kcontig) launch_layout<true, true>(a, s);
   else if (a.a_kcontig) launch_layout<true, false>(a, s);
   else if (a.b_kcontig) launch_layout<false, true>(a, s);

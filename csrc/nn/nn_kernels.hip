@@ -55,27 +55,41 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// One wave per row; 4 waves per block. C % 8 == 0.
-template <typename TIN, typename TOUT>
+template <typename T>
+__device__ __forceinline__ float ld1(const T* p) {
+  if constexpr (sizeof(T) == 4) return *reinterpret_cast<const float*>(p);
+  else return bf16_to_f32(*reinterpret_cast<const bf16_t*>(p));
+}
+template <typename T>
+__device__ __forceinline__ void st1(T* p, float v) {
+  if constexpr (sizeof(T) == 4) *reinterpret_cast<float*>(p) = v;
+  else *reinterpret_cast<bf16_t*>(p) = f32_to_bf16(v);
+}
+
+// One wave per row; 4 waves per block. VEC: 8 values per lane access (C, ld, ldd % 8 == 0); otherwise one value
+// per lane access (any class count, e.g. a 10-class head).
+template <typename TIN, typename TOUT, bool VEC>
 __global__ void __launch_bounds__(256)
     softmax_xent_kernel(const TIN* __restrict__ logits, int64_t ld, const int32_t* __restrict__ labels,
                         TOUT* __restrict__ dlogits, int64_t ldd, float* __restrict__ loss_rows, int M, int C,
                         float grad_scale) {
+  constexpr int V = VEC ? 8 : 1;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const TIN* x = logits + (int64_t)row * ld;
   float m = -INFINITY, s = 0.f;
-  for (int c = lane * 8; c < C; c += 64 * 8) {
-    float v[8];
-    ld8<TIN>(x + c, v);
+  for (int c = lane * V; c < C; c += 64 * V) {
+    float v[V];
+    if constexpr (VEC) ld8<TIN>(x + c, v);
+    else v[0] = ld1<TIN>(x + c);
     float cm = v[0];
 #pragma unroll
-    for (int j = 1; j < 8; ++j) cm = fmaxf(cm, v[j]);
+    for (int j = 1; j < V; ++j) cm = fmaxf(cm, v[j]);
     const float nm = fmaxf(m, cm);
     float cs = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) cs += __expf(v[j] - nm);
+    for (int j = 0; j < V; ++j) cs += __expf(v[j] - nm);
     s = s * __expf(m - nm) + cs;
     m = nm;
   }
@@ -91,21 +105,24 @@ __global__ void __launch_bounds__(256)
     loss_rows[row] = lse - xl;
   }
   TOUT* d = dlogits + (int64_t)row * ldd;
-  for (int c = lane * 8; c < C; c += 64 * 8) {
-    float v[8];
-    ld8<TIN>(x + c, v);
+  for (int c = lane * V; c < C; c += 64 * V) {
+    float v[V];
+    if constexpr (VEC) ld8<TIN>(x + c, v);
+    else v[0] = ld1<TIN>(x + c);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < V; ++j) {
       const float p = __expf(v[j] - gm) * inv;
       v[j] = (p - (c + j == lab ? 1.f : 0.f)) * grad_scale;
     }
-    st8<TOUT>(d + c, v);
+    if constexpr (VEC) st8<TOUT>(d + c, v);
+    else st1<TOUT>(d + c, v[0]);
   }
 }
 
 // Partial column sums over a chunk of rows: block = 256 threads covers 64 columns (16 thr x 4 cols)
-// and 16 row lanes; grid = (N/64, chunks).
-template <typename T>
+// and 16 row lanes; grid = (ceil(N/64), chunks). VEC: 4-column vector loads (N % 4 == 0, ld % 4 == 0); the
+// scalar form takes any width.
+template <typename T, bool VEC>
 __global__ void __launch_bounds__(256)
     col_sum_partial_kernel(const T* __restrict__ x, int64_t ld, int M, int N, int rows_per_chunk,
                            float* __restrict__ part) {
@@ -115,9 +132,13 @@ __global__ void __launch_bounds__(256)
   const int r0 = blockIdx.y * rows_per_chunk;
   const int r1 = min(M, r0 + rows_per_chunk);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int r = r0 + ty; r < r1; r += 16) {
+  for (int r = r0 + ty; r < r1 && col < N; r += 16) {
     const T* p = x + (int64_t)r * ld + col;
-    if (sizeof(T) == 4) {
+    if (!VEC) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (col + u < N) acc[u] += ld1<T>(p + u);
+    } else if (sizeof(T) == 4) {
       const float4 v = *reinterpret_cast<const float4*>(p);
       acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
     } else {
@@ -131,7 +152,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int u = 0; u < 4; ++u) red[ty][tx * 4 + u] = acc[u];
   __syncthreads();
-  if (threadIdx.x < 64) {
+  if (threadIdx.x < 64 && blockIdx.x * 64 + threadIdx.x < N) {
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
@@ -162,20 +183,26 @@ __global__ void __launch_bounds__(256)
 void launch_softmax_xent(int in_dtype, const void* logits, int64_t ld, const int32_t* labels, int out_dtype,
                          void* dlogits, int64_t ldd, float* loss_rows, int M, int C, float grad_scale,
                          hipStream_t s) {
-  FAN_CHECK(C % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0, "softmax_xent needs C, ld % 8 == 0");
+  FAN_CHECK(C > 0, "softmax_xent needs C > 0");
   const int grid = (M + 3) / 4;
-  if (in_dtype == kF32 && out_dtype == kF32)
-    hipLaunchKernelGGL((softmax_xent_kernel<float, float>), grid, 256, 0, s, (const float*)logits, ld, labels,
-                       (float*)dlogits, ldd, loss_rows, M, C, grad_scale);
-  else if (in_dtype == kF32 && out_dtype == kBF16)
-    hipLaunchKernelGGL((softmax_xent_kernel<float, bf16_t>), grid, 256, 0, s, (const float*)logits, ld, labels,
-                       (bf16_t*)dlogits, ldd, loss_rows, M, C, grad_scale);
-  else if (in_dtype == kBF16 && out_dtype == kBF16)
-    hipLaunchKernelGGL((softmax_xent_kernel<bf16_t, bf16_t>), grid, 256, 0, s, (const bf16_t*)logits, ld, labels,
-                       (bf16_t*)dlogits, ldd, loss_rows, M, C, grad_scale);
-  else
-    hipLaunchKernelGGL((softmax_xent_kernel<bf16_t, float>), grid, 256, 0, s, (const bf16_t*)logits, ld, labels,
-                       (float*)dlogits, ldd, loss_rows, M, C, grad_scale);
+  const bool vec = C % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0;
+#define FAN_SMX(TI, TO)                                                                                         \
+  if (vec)                                                                                                      \
+    hipLaunchKernelGGL((softmax_xent_kernel<TI, TO, true>), grid, 256, 0, s, (const TI*)logits, ld, labels,     \
+                       (TO*)dlogits, ldd, loss_rows, M, C, grad_scale);                                          \
+  else                                                                                                          \
+    hipLaunchKernelGGL((softmax_xent_kernel<TI, TO, false>), grid, 256, 0, s, (const TI*)logits, ld, labels,    \
+                       (TO*)dlogits, ldd, loss_rows, M, C, grad_scale);
+  if (in_dtype == kF32 && out_dtype == kF32) {
+    FAN_SMX(float, float)
+  } else if (in_dtype == kF32 && out_dtype == kBF16) {
+    FAN_SMX(float, bf16_t)
+  } else if (in_dtype == kBF16 && out_dtype == kBF16) {
+    FAN_SMX(bf16_t, bf16_t)
+  } else {
+    FAN_SMX(bf16_t, float)
+  }
+#undef FAN_SMX
   FAN_HIP_CHECK(hipGetLastError());
 }
 
@@ -186,15 +213,22 @@ size_t col_sum_workspace_floats(int M, int N) {
 
 void launch_col_sum(int in_dtype, const void* x, int64_t ld, int M, int N, int out_dtype, void* out, float scale,
                     bool accumulate, float* workspace, hipStream_t s) {
-  FAN_CHECK(N % 64 == 0 && ld % 4 == 0, "col_sum needs N % 64 == 0");
+  FAN_CHECK(N > 0, "col_sum needs N > 0");
   const int rows_per_chunk = 256;
   const int chunks = (M + rows_per_chunk - 1) / rows_per_chunk;
-  dim3 grid(N / 64, chunks);
-  if (in_dtype == kF32)
-    hipLaunchKernelGGL((col_sum_partial_kernel<float>), grid, 256, 0, s, (const float*)x, ld, M, N, rows_per_chunk,
-                       workspace);
+  dim3 grid((N + 63) / 64, chunks);
+  const bool vec = N % 4 == 0 && ld % 4 == 0;
+  if (in_dtype == kF32 && vec)
+    hipLaunchKernelGGL((col_sum_partial_kernel<float, true>), grid, 256, 0, s, (const float*)x, ld, M, N,
+                       rows_per_chunk, workspace);
+  else if (in_dtype == kF32)
+    hipLaunchKernelGGL((col_sum_partial_kernel<float, false>), grid, 256, 0, s, (const float*)x, ld, M, N,
+                       rows_per_chunk, workspace);
+  else if (vec)
+    hipLaunchKernelGGL((col_sum_partial_kernel<bf16_t, true>), grid, 256, 0, s, (const bf16_t*)x, ld, M, N,
+                       rows_per_chunk, workspace);
   else
-    hipLaunchKernelGGL((col_sum_partial_kernel<bf16_t>), grid, 256, 0, s, (const bf16_t*)x, ld, M, N,
+    hipLaunchKernelGGL((col_sum_partial_kernel<bf16_t, false>), grid, 256, 0, s, (const bf16_t*)x, ld, M, N,
                        rows_per_chunk, workspace);
   if (out_dtype == kF32)
     hipLaunchKernelGGL((col_sum_final_kernel<float>), (N + 255) / 256, 256, 0, s, workspace, chunks, N, (float*)out,

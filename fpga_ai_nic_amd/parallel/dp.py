@@ -164,8 +164,9 @@ class DataParallelTrainer:
             with tracing.range(f"bwd{i}"):
                 # the bwd-weight GEMM encodes dW (and the fused bias gradient) straight into the wire buffer;
                 # the zero tail (padding, or the bias segment of a bias-free model) is encoded once
+                # (the wire epilogue encodes whole 16-column groups: output widths that are multiples of 16)
                 tgt = (self.engine.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout)
-                       if self.prepack else None)
+                       if self.prepack and l.cout % 16 == 0 else None)
                 m.backward_weight(i, wire=tgt)
                 h = None
                 if self.engine is not None:

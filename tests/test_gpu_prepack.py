@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("codec", ["bfp_rne", "bfp_trunc"])
 @pytest.mark.parametrize("cin,cout,mb,nsh", [(1024, 4096, 512, 1), (4096, 1024, 256, 3), (512, 768, 384, 8),
-                                              (256, 256, 128, 2)])
+                                              (256, 256, 128, 2), (1000, 2048, 672, 3), (2048, 1008, 200, 2)])
 def test_gemm_wire_epilogue_matches_pack(codec, cin, cout, mb, nsh):
     torch.manual_seed(cin + nsh)
     x = (torch.randn(mb, cin, device="cuda") * 0.5).to(torch.bfloat16)
