@@ -97,6 +97,13 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     launch_gemm_bf16(g, fan_stream());
   } else {
     TORCH_CHECK(A.scalar_type() == at::kFloat, "gemm: A must be bf16 or f32");
+    const int sk = gemm_f32_split(g.M, g.N, g.K, g.split_k);
+    if (sk > 1) {
+      const int64_t need = (int64_t)sk * g.M * g.N;
+      TORCH_CHECK(workspace && workspace->scalar_type() == at::kFloat && workspace->is_contiguous() &&
+                      workspace->numel() >= need,
+                  "gemm_f32: split-K ", sk, " needs an f32 workspace of ", need, " elements");
+    }
     TORCH_CHECK(gemm_f32_supported(g), "gemm_f32: unsupported shape M=", g.M, " N=", g.N, " K=", g.K);
     launch_gemm_f32(g, fan_stream());
   }
@@ -153,6 +160,8 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("wire") = pybind11::none(), pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1,
         pybind11::arg("wire_codec") = 1);
   m.def("gemm_supported", &gemm_supported);
+  m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
+        pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);
   m.def("gemm_set_pingpong", [](bool on) { gemm_pingpong_flag().store(on); },
         "256x256 GEMM tiles: ping-pong main loop (default) or the one-role loop");
   m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {

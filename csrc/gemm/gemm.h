@@ -68,6 +68,8 @@ std::atomic<bool>& gemm_pingpong_flag();
 void gemm_set_stamp_buffer(void* p);
 void* gemm_stamp_buffer();
 
+// f32 GEMM split-K factor for a shape (split_k <= 0: automatic); workspace: split * M * N floats when > 1.
+int gemm_f32_split(int M, int N, int K, int split_k);
 bool gemm_f32_supported(const GemmArgs& a);
 void launch_gemm_f32(const GemmArgs& a, hipStream_t stream);
 

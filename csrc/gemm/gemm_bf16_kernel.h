@@ -357,8 +357,10 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
 }
 
 // 8 waves (2 per SIMD) or 4 waves (1 per SIMD, up to 512 VGPR+AGPR per lane: large per-wave tiles).
+// RAGGED: the shape is not a multiple of the tile (or K of BK * split_k); only then is the edge code compiled in,
+// so aligned shapes run exactly the unpredicated kernel.
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT,
-          bool DMA1 = false>
+          bool DMA1 = false, bool RAGGED = false>
 __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
     gemm_bf16_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                      TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
@@ -396,8 +398,8 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
   const int kt0 = ksplit * kt_per;
   const int nk = max(0, min(nkt, kt0 + kt_per) - kt0);
   const int kbeg = kt0 * BK;
-  const bool mn_edge = m0 + BM > M || n0 + BN > N;
-  const bool edge = mn_edge || (kt0 + nk) * BK > K;  // uniform: predicated staging for this workgroup
+  const bool mn_edge = RAGGED && (m0 + BM > M || n0 + BN > N);
+  const bool edge = RAGGED && (mn_edge || (kt0 + nk) * BK > K);  // uniform: predicated staging for this workgroup
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -837,7 +839,9 @@ void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
   // it from every wave right after the barrier. (Issuing it between the two k-steps' MFMA clusters made fwd1 5 %
   // faster in isolation but the flagship step 3 % slower, same box: profiles/r1_gemm_dma_position_layout_ab.jsonl,
   // r1_gemm_dma_position_flagship_ab.log.)
-  auto k = gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, SPLIT, !AK && !BKC>;
+  const bool ragged = a.M % BM || a.N % BN || a.K % (BK * sk);
+  auto k = ragged ? gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, SPLIT, !AK && !BKC, true>
+                  : gemm_bf16_kernel<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, SPLIT, !AK && !BKC, false>;
   FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
                      a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,

@@ -78,22 +78,30 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + bid / kNumXCD;
 }
 
-template <bool AK, bool BKC, int EPI, bool ACCUM>
+// SPLIT: K split over split_k workgroups per tile (ragged ranges of K-tiles); each writes its raw f32 partial
+// tile to slab ws[ksplit][M][N] and f32_splitk_reduce_kernel sums the slabs in split order (deterministic) and
+// applies the epilogue. Small output grids (the reference workload's 672 / 448-row batches) fill the CUs this way.
+template <bool AK, bool BKC, int EPI, bool ACCUM, bool SPLIT>
 __global__ void __launch_bounds__(NT, 2)
     gemm_f32_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B, int64_t ldb,
                     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias, const float* __restrict__ aux,
-                    int64_t ldaux, int M, int N, int K) {
+                    int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles_n = (N + BN - 1) / BN;
-  const int nwg = ((M + BM - 1) / BM) * tiles_n;
-  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, tiles * split_k);
+  const int tile = wg % tiles, ksplit = wg / tiles;
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nk = (K + BK - 1) / BK;
+  const int nkt = (K + BK - 1) / BK;
+  const int kt_per = (nkt + split_k - 1) / split_k;
+  const int kt0 = ksplit * kt_per;
+  const int nk = max(0, min(nkt, kt0 + kt_per) - kt0);
+  const int kbeg = kt0 * BK;
   const bool mn_edge = m0 + BM > M || n0 + BN > N;
-  const bool edge = mn_edge || K % BK;  // uniform: predicated staging for this workgroup
+  const bool edge = mn_edge || (kt0 + nk) * BK > K;  // uniform: predicated staging for this workgroup
   auto stage_ab = [&](int k0, char* dst) {
     if (edge) {
       stage<AK, true>(A, lda, m0, k0, dst, wave, lane, M, K);
@@ -110,7 +118,7 @@ __global__ void __launch_bounds__(NT, 2)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage_ab(0, smem);
+  if (nk > 0) stage_ab(kbeg, smem);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
@@ -118,7 +126,7 @@ __global__ void __launch_bounds__(NT, 2)
     char* sa = smem + cur * STAGE_BYTES;
     char* sb = sa + TILE_BYTES;
     if (kt + 1 < nk) {
-      stage_ab((kt + 1) * BK, smem + (cur ^ 1) * STAGE_BYTES);
+      stage_ab(kbeg + (kt + 1) * BK, smem + (cur ^ 1) * STAGE_BYTES);
     }
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
@@ -143,13 +151,17 @@ __global__ void __launch_bounds__(NT, 2)
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + wn * 64 + j * 16 + col_l;
     if (mn_edge && col >= N) continue;
-    const float bv = (EPI == kEpiBias || EPI == kEpiBiasRelu) ? bias[col] : 0.f;
+    const float bv = (!SPLIT && (EPI == kEpiBias || EPI == kEpiBiasRelu)) ? bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * 64 + i * 16 + row_l + r;
         if (mn_edge && row >= M) continue;
+        if (SPLIT) {
+          ws[((int64_t)ksplit * M + row) * N + col] = acc[i][j][r];
+          continue;
+        }
         float v = acc[i][j][r] + bv;
         if (EPI == kEpiBiasRelu) v = fmaxf(v, 0.f);
         if (EPI == kEpiReluMask) v = aux[(int64_t)row * ldaux + col] > 0.f ? v : 0.f;
@@ -160,19 +172,49 @@ __global__ void __launch_bounds__(NT, 2)
   }
 }
 
+// Ordered split-K reduction (slabs summed in split order) + the f32 epilogue.
+template <int EPI, bool ACCUM>
+__global__ void __launch_bounds__(256)
+    f32_splitk_reduce_kernel(const float* __restrict__ ws, int split_k, float* __restrict__ C, int64_t ldc,
+                             const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux, int M, int N) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(e / N), col = (int)(e % N);
+    float v = ws[e];
+    for (int k = 1; k < split_k; ++k) v += ws[(int64_t)k * total + e];
+    if (EPI == kEpiBias || EPI == kEpiBiasRelu) v += bias[col];
+    if (EPI == kEpiBiasRelu) v = fmaxf(v, 0.f);
+    if (EPI == kEpiReluMask) v = aux[(int64_t)row * ldaux + col] > 0.f ? v : 0.f;
+    float* p = C + (int64_t)row * ldc + col;
+    if (ACCUM) v += *p;
+    *p = v;
+  }
+}
+
+template <bool AK, bool BKC, int EPI, bool ACCUM>
+void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
+  const int grid = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * sk;
+  if (sk > 1) {
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC, EPI, ACCUM, true>), grid, NT, LDS_BYTES, s, (const float*)a.A, a.lda,
+                       (const float*)a.B, a.ldb, (float*)a.C, a.ldc, (const float*)a.bias, (const float*)a.aux, a.ldaux,
+                       a.M, a.N, a.K, sk, (float*)a.workspace);
+    hipLaunchKernelGGL((f32_splitk_reduce_kernel<EPI, ACCUM>), stream_grid((size_t)a.M * a.N), 256, 0, s,
+                       (const float*)a.workspace, sk, (float*)a.C, a.ldc, (const float*)a.bias, (const float*)a.aux,
+                       a.ldaux, a.M, a.N);
+  } else {
+    hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC, EPI, ACCUM, false>), grid, NT, LDS_BYTES, s, (const float*)a.A,
+                       a.lda, (const float*)a.B, a.ldb, (float*)a.C, a.ldc, (const float*)a.bias, (const float*)a.aux,
+                       a.ldaux, a.M, a.N, a.K, 1, nullptr);
+  }
+}
+
 template <bool AK, bool BKC>
 void launch_layout(const GemmArgs& a, hipStream_t s) {
-  const int grid = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-#define FAN_F32_CASE(E)                                                                                       \
-  case E:                                                                                                     \
-    if (a.accumulate)                                                                                         \
-      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC, E, true>), grid, NT, LDS_BYTES, s, (const float*)a.A, a.lda, \
-                         (const float*)a.B, a.ldb, (float*)a.C, a.ldc, (const float*)a.bias, (const float*)a.aux,    \
-                         a.ldaux, a.M, a.N, a.K);                                                            \
-    else                                                                                                      \
-      hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC, E, false>), grid, NT, LDS_BYTES, s, (const float*)a.A, a.lda, \
-                         (const float*)a.B, a.ldb, (float*)a.C, a.ldc, (const float*)a.bias, (const float*)a.aux,     \
-                         a.ldaux, a.M, a.N, a.K);                                                             \
+  const int sk = gemm_f32_split(a.M, a.N, a.K, a.split_k);
+#define FAN_F32_CASE(E)                                         \
+  case E:                                                       \
+    if (a.accumulate) launch_typed<AK, BKC, E, true>(a, sk, s); \
+    else launch_typed<AK, BKC, E, false>(a, sk, s);             \
     break;
   switch (a.epilogue) {
     FAN_F32_CASE(kEpiNone)
@@ -186,12 +228,23 @@ void launch_layout(const GemmArgs& a, hipStream_t s) {
 
 }  // namespace
 
+int gemm_f32_split(int M, int N, int K, int split_k) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int nkt = (K + BK - 1) / BK;
+  if (split_k > 0) return std::min(split_k, std::max(1, nkt));
+  int sk = 1;  // split K only when the output grid leaves more than half of the CUs idle
+  if (tiles * 2 <= kNumCU)
+    while (tiles * sk < kNumCU && sk < 8 && nkt / (sk * 2) >= 8) sk *= 2;
+  return sk;
+}
+
 bool gemm_f32_supported(const GemmArgs& a) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0) return false;
   if (a.M % 8 || a.N % 8 || a.K % 8) return false;
   if (a.lda % 4 || a.ldb % 4) return false;
   if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return false;
-  if (a.c_bf16 || a.split_k > 1) return false;
+  if (a.c_bf16 || a.epilogue == kEpiWire || a.colsum) return false;
+  if (gemm_f32_split(a.M, a.N, a.K, a.split_k) > 1 && a.workspace == nullptr) return false;
   return true;
 }
 

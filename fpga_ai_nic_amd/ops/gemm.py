@@ -90,7 +90,9 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
             if sk > 1:
                 ws = _workspace(C.device, sk * (M * N + N))
         else:
-            sk = 1
+            sk = Cx.gemm_f32_split(M, N, K, sk)
+            if sk > 1:
+                ws = _workspace(C.device, sk * M * N)
         Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, tbm, tbn, colsum, tw)
         return C
     # CPU reference path

@@ -47,7 +47,7 @@ def test_ragged_all_layouts(C, dt, M):
                 for b_t in (False, True):
                     Ain = A.t().contiguous() if a_t else A
                     Bin = B.t().contiguous() if b_t else B
-                    splits = (None, 1, 3) if dt == torch.bfloat16 else (None,)
+                    splits = (None, 1, 3)
                     for sk in splits:
                         Cout = torch.full((M, N), float("nan"), device=DEV)
                         G.gemm(Ain, a_t, Bin, b_t, Cout, split_k=sk)
