@@ -31,6 +31,7 @@ void register_engine(pybind11::module_& m) {
       .def("comm", [](std::shared_ptr<LoopbackFabric> f, int rank) { return new LoopbackComm(f, rank); });
   pybind11::class_<LoopbackComm, Comm>(m, "LoopbackComm")
       .def("drop_after", &LoopbackComm::drop_after)
+      .def("lose_round", &LoopbackComm::lose_round)
       .def_property_readonly("collectives", &LoopbackComm::collectives);
   pybind11::class_<P2PComm, Comm>(m, "P2PComm")
       .def(pybind11::init<int, int, int, size_t>(), pybind11::arg("rank"), pybind11::arg("world"),
@@ -45,6 +46,7 @@ void register_engine(pybind11::module_& m) {
       .def_static("connect_local", &P2PComm::connect_local)
       .def_property_readonly("slot_bytes", &P2PComm::slot_bytes)
       .def_property_readonly("sequence", &P2PComm::sequence)
+      .def_property_readonly("uncached", &P2PComm::uncached)
       .def("all_to_all",
            [](P2PComm& c, const at::Tensor& send, at::Tensor& recv) {
              TORCH_CHECK(bytes_of(send) == bytes_of(recv) && bytes_of(send) % c.world() == 0, "all_to_all sizes");
@@ -105,7 +107,7 @@ void register_engine(pybind11::module_& m) {
   namespace py = pybind11;
   py::class_<AllReduceEngine>(m, "AllReduceEngine")
       .def(py::init([](Comm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
-                       bool compat, double timeout_s, int priority, bool force_comm, int device) {
+                       bool compat, double timeout_s, int priority, bool force_comm, int device, int verify) {
              EngineConfig c;
              c.codec = codec;
              c.algo = algo;
@@ -115,11 +117,13 @@ void register_engine(pybind11::module_& m) {
              c.timeout_s = timeout_s;
              c.stream_priority = priority;
              c.force_comm = force_comm;
+             c.verify = verify;
              return new AllReduceEngine(comm, rank, world, c, device);
            }),
            py::keep_alive<1, 2>(), py::arg("comm").none(true), py::arg("rank"), py::arg("world"), py::arg("codec"),
            py::arg("algo"), py::arg("rings"), py::arg("max_slice_elems"), py::arg("compat_owner_fp32"),
-           py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"))
+           py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"),
+           py::arg("verify") = -1)
       .def("layout",
            [](AllReduceEngine& e, int64_t n) {
              const EngineLayout L = e.layout(n);
@@ -236,6 +240,10 @@ void register_engine(pybind11::module_& m) {
       .def("latency_ms", &AllReduceEngine::latency_ms, py::call_guard<py::gil_scoped_release>())
       .def("set_timing", &AllReduceEngine::set_timing)
       .def("diagnostics", &AllReduceEngine::diagnostics)
+      .def_property_readonly("verify", &AllReduceEngine::verify)
+      .def("check_verify", &AllReduceEngine::check_verify,
+           "verify mode: raise if any message so far failed its checksum / sequence check")
+      .def("set_fault", &AllReduceEngine::set_fault, "test-only fault injection rules (FAN_FAULT grammar)")
       .def("counters",
            [](const AllReduceEngine& e) {
              const EngineCounters& c = e.counters();
@@ -249,6 +257,7 @@ void register_engine(pybind11::module_& m) {
              d["device_ms"] = c.device_ms;
              d["timed_requests"] = c.timed_requests;
              d["forced_commits"] = c.forced_commits;
+             d["verified_rows"] = c.verified_rows;
              return d;
            },
            "perf counters (the NIC's latency / host-stall registers): requests, bytes, host wait, device time")

@@ -3,6 +3,8 @@
 
 #include <chrono>
 #include <cstdlib>
+
+#include "common/roctx.h"
 #include <functional>
 #include <sstream>
 #include <thread>
@@ -43,6 +45,15 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     if (!std::strcmp(f, "system")) evf |= hipEventReleaseToSystem;
     else if (!std::strcmp(f, "device")) evf |= hipEventReleaseToDevice;
   }
+  const char* ve = std::getenv("FAN_VERIFY");
+  verify_ = cfg.verify >= 0 ? cfg.verify > 0 : (ve && ve[0] == '1');
+  if (verify_) {
+    FAN_HIP_CHECK(hipMalloc(&tags_, (size_t)5 * kTagRows * 16));
+    FAN_HIP_CHECK(hipMalloc(&verr_dev_, sizeof(VerifyError)));
+    FAN_HIP_CHECK(hipMemset(verr_dev_, 0, sizeof(VerifyError)));
+    FAN_HIP_CHECK(hipHostMalloc(&verr_host_, sizeof(VerifyError), hipHostMallocDefault));
+    std::memset(verr_host_, 0, sizeof(VerifyError));
+  }
   for (auto& s : slots_) {
     FAN_HIP_CHECK(hipEventCreateWithFlags(&s.ready, evf));
     FAN_HIP_CHECK(hipEventCreateWithFlags(&s.update, evf));
@@ -68,6 +79,9 @@ AllReduceEngine::~AllReduceEngine() {
     for (auto& e : t.ev) hipEventDestroy(e);
   for (auto& kv : scratch_) hipFree(kv.second.first);
   if (flags_host_) hipHostFree((void*)flags_host_);
+  if (tags_) hipFree(tags_);
+  if (verr_dev_) hipFree(verr_dev_);
+  if (verr_host_) hipHostFree(verr_host_);
   hipStreamDestroy(stream_);
 }
 
@@ -166,18 +180,40 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
   const uint8_t* P = prepacked ? prepacked : g;
   const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
   if (!zero_copy && !prepacked) {
+    RoctxRange rr("fan/mesh/pack");
     uint8_t* Pb = scratch("mesh_P" + std::to_string(sb * N), sb * N);
     launch_wire_pack(c, gdt, g, Pb, (size_t)s, N, st);
     P = Pb;
   }
   mark(kTpPacked);
   uint8_t* R = scratch("mesh_R" + std::to_string(sb * N), sb * N);
-  comm_->all_to_all(P, R, sb, st);
+  {
+    RoctxRange rr("fan/mesh/all_to_all");
+    if (verify_) launch_msg_tags(P, sb, sb, N, req_seq_, tag_region(0), st);
+    fault_.maybe_corrupt("mesh_pack", const_cast<uint8_t*>(P), sb * N, st);  // in flight: after the tags
+    comm_->all_to_all(P, R, sb, st);
+    if (verify_) {
+      comm_->all_to_all(tag_region(0), tag_region(1), 16, st);
+      verify_rows(R, sb, N, tag_region(1), 1, 0, st);
+    }
+  }
   mark(kTpExchanged);
-  launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
+  {
+    RoctxRange rr("fan/mesh/reduce");
+    launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
+  }
   mark(kTpReduced);
   uint8_t* G = epi_scratch("mesh_G" + std::to_string(sb * N), sb * N);
-  comm_->all_gather(S, G, sb, st);
+  {
+    RoctxRange rr("fan/mesh/all_gather");
+    if (verify_) launch_msg_tags(S, sb, sb, 1, req_seq_, tag_region(3), st);
+    fault_.maybe_corrupt("mesh_reduce", S, sb, st);
+    comm_->all_gather(S, G, sb, st);
+    if (verify_) {
+      comm_->all_gather(tag_region(3), tag_region(4), 16, st);
+      verify_rows(G, sb, N, tag_region(4), 2, 0, st);
+    }
+  }
   const int64_t n_pad = L.n_pad;
   return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
 }
@@ -229,7 +265,9 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
     else rounds.push_back({j});
   }
   auto local = [&](const RingState& rs, int64_t x) { return g + (size_t)(rs.off + x * S) * esize(gdt); };
+  uint32_t round_id = 0;
   for (const auto& rnd : rounds) {
+    RoctxRange rr("fan/ring/round");
     std::vector<P2POp> sends, recvs;
     for (size_t j : rnd) {
       for (auto& rs : rings) {
@@ -259,7 +297,24 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
         }
       }
     }
-    if (N > 1) comm_->sendrecv(sends, recvs, st);
+    if (N > 1) {
+      const size_t nd = sends.size(), nr = recvs.size();
+      if (verify_) {  // one tag per message, sent after all of the round's payloads (per-peer order is kept)
+        FAN_CHECK(nd <= (size_t)kTagRows && nr <= (size_t)kTagRows, "verify: too many messages in a ring round");
+        for (size_t q = 0; q < nd; ++q) {
+          launch_msg_tags(static_cast<const uint8_t*>(sends[q].ptr), sb, sb, 1, req_seq_, tag_region(0) + q * 4, st);
+          sends.push_back({tag_region(0) + q * 4, 16, sends[q].peer});
+        }
+        for (size_t q = 0; q < nr; ++q) recvs.push_back({tag_region(1) + q * 4, 16, recvs[q].peer});
+      }
+      for (size_t q = 0; q < nd; ++q) fault_.maybe_corrupt("ring_send", static_cast<uint8_t*>(sends[q].ptr), sb, st);
+      comm_->sendrecv(sends, recvs, st);
+      if (verify_)
+        for (size_t q = 0; q < nr; ++q)
+          verify_rows(static_cast<const uint8_t*>(recvs[q].ptr), sb, 1, tag_region(1) + q * 4, 3,
+                      round_id * kTagRows + (uint32_t)q, st);
+    }
+    ++round_id;
   }
   std::vector<EpiThunk> thunks;
   for (auto& rs : rings) {
@@ -288,7 +343,9 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
 int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
                             SgdParams sgd, hipStream_t producer, bool defer, bool update, float* out_sum,
                             const uint8_t* prepacked, int64_t prepacked_elems) {
+  RoctxRange rr("fan/allreduce/submit");
   FAN_HIP_CHECK(hipSetDevice(device_));
+  req_seq_ = seq_ + 1;  // the sequence number this request will get (its messages' tags carry it)
   const int slot = next_slot_;
   next_slot_ = (slot + 1) % kSlots;
   Slot& sl = slots_[slot];
@@ -339,6 +396,8 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   // phases this schedule does not have (ring hops, the world-1 local path) collapse onto the end of comm
   for (int tp = kTpPacked; tp <= kTpCommEnd; ++tp)
     if (!(trace_marked_ & (1u << tp))) mark(tp);
+  // verify mode: the device error block's host mirror, refreshed after every request's communication phase
+  if (verify_) FAN_HIP_CHECK(hipMemcpyAsync(verr_host_, verr_dev_, sizeof(VerifyError), hipMemcpyDeviceToHost, run_stream_));
   cur_trace_ = -1;
   // end of this request's communication phase: what an epilogue on the producer stream waits for
   if (!inline_) FAN_HIP_CHECK(hipEventRecord(sl.comm_done, stream_));
@@ -357,6 +416,7 @@ void AllReduceEngine::commit(int slot, bool after_producer, hipStream_t producer
 
 void AllReduceEngine::commit_slot(Slot& sl, int slot, bool after_producer, hipStream_t producer) {
   if (!sl.pending) return;
+  RoctxRange rr("fan/allreduce/epilogue");
   sl.epi_stream = sl.stream;
   if (epi_on_producer_ && !inline_ && after_producer && producer != sl.stream) {
     // Epilogue on the producer (compute) stream: it waits for the request's communication phase, then the
@@ -486,6 +546,24 @@ void AllReduceEngine::synchronize(int slot, double timeout_s, uint32_t seq) {
       }
     }
   }
+  check_verify();  // verify mode: surface a mismatch recorded while this request ran
+}
+
+void AllReduceEngine::verify_rows(const uint8_t* rows, size_t row_bytes, int nrows, const uint32_t* recv_tags,
+                                  uint32_t site, uint32_t row_base, hipStream_t st) {
+  launch_msg_verify(rows, row_bytes, row_bytes, nrows, recv_tags, req_seq_, tag_region(2), verr_dev_, site, row_base, st);
+  counters_.verified_rows += (uint64_t)nrows;
+}
+
+void AllReduceEngine::check_verify() {
+  if (!verify_ || verr_host_->flag == 0) return;
+  static const char* sites[] = {"?", "mesh all_to_all", "mesh all_gather", "ring round"};
+  const VerifyError e = *verr_host_;
+  std::ostringstream os;
+  os << "verify: message " << (e.kind == 1 ? "corrupted" : "out of sequence (dropped or reordered)") << " in "
+     << sites[e.site < 4 ? e.site : 0] << " row " << e.row << " (checksum " << e.got_s1 << " vs tag " << e.exp_s1
+     << ", request " << e.got_seq << " vs expected " << e.exp_seq << ") [rank=" << rank_ << " world=" << world_ << "]";
+  throw std::runtime_error(os.str());
 }
 
 float AllReduceEngine::latency_ms(int slot) {

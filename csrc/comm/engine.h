@@ -23,6 +23,7 @@
 #include "bfp/bfp_format.h"
 #include "comm/native_comm.h"
 #include "comm/planner.h"
+#include "comm/verify.h"
 
 namespace fan {
 
@@ -35,6 +36,7 @@ struct EngineConfig {
   double timeout_s = 600.0;
   int stream_priority = -1;
   bool force_comm = false;  // world 1 still runs the collectives (exercises the multi-rank path)
+  int verify = -1;          // debug verify mode (message tags + sequence numbers); -1: from FAN_VERIFY
 };
 
 struct EngineLayout {
@@ -59,6 +61,7 @@ struct EngineCounters {
   double device_ms = 0.0;      // summed device time of timed requests (lpbk_latency analogue)
   uint64_t timed_requests = 0;
   uint64_t forced_commits = 0;  // deferred epilogues committed because their slot was needed (> kSlots deferred)
+  uint64_t verified_rows = 0;   // verify mode: message rows whose tags were checked on arrival
 };
 
 // Device-side request trace: GPU timestamps (timing events) at the phase boundaries of each request, the MI355X
@@ -135,6 +138,11 @@ class AllReduceEngine {
   void set_epilogue_on_producer(bool on) { epi_on_producer_ = on; }
   bool epilogue_on_producer() const { return epi_on_producer_; }
   std::string diagnostics(int slot) const;
+  bool verify() const { return verify_; }
+  // verify mode: raise (with site, row, checksums, sequence numbers) if any message so far failed its check
+  void check_verify();
+  // test-only fault injection (FAN_FAULT grammar, see verify.h); replaces the rules taken from the environment
+  void set_fault(const std::string& spec) { fault_ = FaultInjector(spec); }
   uint64_t requests() const { return seq_; }
   const EngineCounters& counters() const { return counters_; }
   void reset_counters() { counters_ = EngineCounters{}; }
@@ -195,6 +203,17 @@ class AllReduceEngine {
   size_t trace_used_ = 0;
   uint64_t trace_dropped_ = 0;
   int cur_trace_ = -1;  // trace of the request being built
+  // verify mode / fault injection (verify.h): tag buffers (device), first-error block (device) + its host mirror
+  bool verify_ = false;
+  FaultInjector fault_;
+  uint32_t* tags_ = nullptr;  // [kTagRows][4] x 5 regions: send, recv, scratch, gather-send, gather-recv
+  VerifyError* verr_dev_ = nullptr;
+  VerifyError* verr_host_ = nullptr;
+  uint32_t req_seq_ = 0;  // sequence number of the request being built (what its tags carry)
+  static constexpr int kTagRows = 64;
+  uint32_t* tag_region(int r) { return tags_ + (size_t)r * kTagRows * 4; }
+  void verify_rows(const uint8_t* rows, size_t row_bytes, int nrows, const uint32_t* recv_tags, uint32_t site,
+                   uint32_t row_base, hipStream_t st);
   unsigned trace_marked_ = 0;  // trace points the schedule of the request being built has recorded
   // Scratch that a deferred epilogue reads: per request slot, so a later request of the same size cannot
   // overwrite it before this request commits (the trainer commits every request at the end of backward).

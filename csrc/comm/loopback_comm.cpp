@@ -7,7 +7,7 @@
 namespace fan {
 
 LoopbackFabric::LoopbackFabric(int world, double timeout_s)
-    : post(world, nullptr), sends(world), world_(world), timeout_s_(timeout_s) {
+    : post(world, nullptr), sends(world), lost(world, 0), world_(world), timeout_s_(timeout_s) {
   FAN_CHECK(world >= 1, "loopback world must be >= 1");
 }
 
@@ -67,6 +67,7 @@ void LoopbackComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P
   const int N = world();
   FAN_HIP_CHECK(hipStreamSynchronize(s));
   f_->sends[rank_] = sends;
+  f_->lost[rank_] = rounds_++ == lose_round_;
   f_->barrier(rank_);
   std::vector<int> taken(N, 0);
   for (const P2POp& r : recvs) {
@@ -81,7 +82,7 @@ void LoopbackComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P
       }
     FAN_CHECK(match != nullptr, "loopback sendrecv: no matching send from peer");
     FAN_CHECK(match->bytes == r.bytes, "loopback sendrecv: size mismatch between send and recv");
-    FAN_HIP_CHECK(hipMemcpyAsync(r.ptr, match->ptr, r.bytes, hipMemcpyDeviceToDevice, s));
+    if (!f_->lost[r.peer]) FAN_HIP_CHECK(hipMemcpyAsync(r.ptr, match->ptr, r.bytes, hipMemcpyDeviceToDevice, s));
   }
   FAN_HIP_CHECK(hipStreamSynchronize(s));
   f_->barrier(rank_);

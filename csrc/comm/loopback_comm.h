@@ -25,6 +25,7 @@ class LoopbackFabric {
   void barrier(int rank);
   std::vector<const void*> post;                // per rank: the buffer published for this collective
   std::vector<std::vector<P2POp>> sends;        // per rank: sends published for this round
+  std::vector<char> lost;                       // per rank: this round's sends are lost in flight (fault injection)
   bool aborted = false;
 
  private:
@@ -47,13 +48,17 @@ class LoopbackComm : public Comm {
   std::string async_error() override { return f_->aborted ? "loopback fabric aborted" : ""; }
   void abort() override { f_->aborted = true; }
   void drop_after(int64_t k) { drop_after_ = k; }
+  // fault injection: the messages of this rank's k-th sendrecv round (0-based, counted over sendrecv calls) are lost
+  // in flight — the receivers' buffers keep their stale contents, the schedule goes on (a silent loss, what
+  // verify mode must catch)
+  void lose_round(int64_t k) { lose_round_ = k; }
   int64_t collectives() const { return ops_; }
 
  private:
   bool dropped();
   std::shared_ptr<LoopbackFabric> f_;
   int rank_;
-  int64_t ops_ = 0, drop_after_ = -1;
+  int64_t ops_ = 0, drop_after_ = -1, lose_round_ = -1, rounds_ = 0;
 };
 
 }  // namespace fan

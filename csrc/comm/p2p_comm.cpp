@@ -19,12 +19,24 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
   FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
   FAN_CHECK(slot_ > 0, "slot_bytes must be > 0");
   FAN_HIP_CHECK(hipSetDevice(device));
-  FAN_HIP_CHECK(hipMalloc(&arena_, (size_t)world * 2 * slot_));
+  // Arena and flags UNCACHED (see the memory-ordering argument in p2p_comm.h): peers write them over xGMI, so no
+  // line of them may sit in this GPU's (per-XCD, non-coherent) L2 when the reader consumes a new message.
+  // Fallback to coarse-grained memory only if the allocator refuses the flag (the ordering then rests on the
+  // kernel-boundary L2 invalidate of the reading kernel, which reads each arena byte once per message).
+  uncached_ = hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * 2 * slot_,
+                                    hipDeviceMallocUncached) == hipSuccess;
+  if (!uncached_) {
+    (void)hipGetLastError();
+    FAN_HIP_CHECK(hipMalloc(&arena_, (size_t)world * 2 * slot_));
+  }
   // flags are polled by the command processor (hipStreamWaitValue64) and written by peers' command
-  // processors (hipStreamWriteValue64); plain device memory supports both and HIP IPC export (probed on
+  // processors (hipStreamWriteValue64); device memory supports both and HIP IPC export (probed on
   // MI355X: tools/probes/stream_wait_probe.cpp)
   void* f = nullptr;
-  FAN_HIP_CHECK(hipMalloc(&f, (size_t)2 * world * sizeof(uint64_t)));
+  if (hipExtMallocWithFlags(&f, (size_t)2 * world * sizeof(uint64_t), hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    FAN_HIP_CHECK(hipMalloc(&f, (size_t)2 * world * sizeof(uint64_t)));
+  }
   flags_ = reinterpret_cast<uint64_t*>(f);
   FAN_HIP_CHECK(hipMemset(flags_, 0, (size_t)2 * world * sizeof(uint64_t)));
   FAN_HIP_CHECK(hipDeviceSynchronize());
@@ -35,6 +47,22 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
   peer_flags_[rank] = flags_;
   last_sent_[0].assign(world, 0);
   last_sent_[1].assign(world, 0);
+}
+
+void P2PComm::abort() {
+  if (aborted_) return;
+  aborted_ = true;
+  // Release every GPU waiter parked on this rank's flag block (a ready-wait for a dead sender, an ack-wait for a
+  // dead receiver): overwrite all ready / ack words with a poison value above any sequence number, from a stream of
+  // its own (the parked stream cannot run it). The released streams then copy stale arena bytes; the aborted_
+  // state makes every later call and the engine's synchronize() raise, so nothing trusts them.
+  hipSetDevice(device_);
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+    hipMemsetAsync(flags_, 0x7F, (size_t)2 * world_ * sizeof(uint64_t), s);
+    hipStreamSynchronize(s);
+    hipStreamDestroy(s);
+  }
 }
 
 P2PComm::~P2PComm() {

@@ -11,6 +11,23 @@
 // stalls when it is two messages ahead of a receiver. Flags: ready[world] + ack[world] (uint64 each).
 // Reference analogue: the NIC's Ethernet link + credit flow control (hw/all_reduce.sv:468-483) and the
 // done-flag writes (hw/all_reduce.sv:1368-1375); here sequence numbers play the role of both.
+//
+// Memory ordering (why a reader never sees a stale payload, across GPUs whose per-XCD L2s are not coherent):
+//   1. writer: the copy kernel stores the payload into the peer's arena (stores over xGMI land in the peer's HBM;
+//      the writer's own L2 does not keep remote lines), then __threadfence_system() and kernel end (release at
+//      system scope) — every payload store is performed before the kernel's completion is signalled;
+//   2. the flag write (hipStreamWriteValue64) is stream-ordered after that completion, so it becomes visible to the
+//      peer only after the payload;
+//   3. reader: its stream's hipStreamWaitValue64 (the command processor polls the flag in memory, not a cache)
+//      releases the copy-out kernel only once the flag carries the message's sequence number;
+//   4. arena and flags are allocated UNCACHED (hipDeviceMallocUncached): the reader's loads bypass L2, so no stale
+//      line from the previous message in that slot can be hit — the acquire side needs no invalidate. (If the
+//      allocator refuses the flag, coarse-grained memory is used and the reader's kernel-start L2 invalidate does
+//      that job; uncached() reports which.)
+//   5. WAR: a sender reuses a parity slot only after the receiver's ack (written after its copy-out kernel
+//      completed) shows the previous message in it was consumed.
+// abort() releases every stream parked on this rank's flags (poison value) so a dead peer cannot hang the GPU;
+// the communicator then refuses further calls.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -46,8 +63,9 @@ class P2PComm : public Comm {
   void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s) override;
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override;
   std::string async_error() override { return aborted_ ? "p2p transport aborted" : ""; }
-  void abort() override { aborted_ = true; }
+  void abort() override;
   uint64_t sequence() const { return seq_; }
+  bool uncached() const { return uncached_; }
 
  private:
   void copy(const std::vector<P2PCopy>& segs, hipStream_t s);
@@ -62,6 +80,7 @@ class P2PComm : public Comm {
   std::vector<uint64_t> last_sent_[2];  // per parity: sequence of the last message sent to each peer
   uint64_t seq_ = 0;
   bool aborted_ = false;
+  bool uncached_ = false;
 };
 
 }  // namespace fan

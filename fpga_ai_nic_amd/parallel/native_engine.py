@@ -23,7 +23,7 @@ import torch
 
 from .. import _ext
 from ..ops import wire
-from .allreduce import NUM_SLOTS, BucketLayout, CommTimeoutError
+from .allreduce import NUM_SLOTS, BucketLayout, ChecksumError, CommTimeoutError
 from .transport import NativeTransport, Transport
 
 _ALGOS = {"mesh": 0, "ring": 1}
@@ -78,10 +78,16 @@ class NativeHandle:
     def synchronize(self, timeout: float | None = None):
         self.commit_after_current()
         if self.done():
+            try:
+                self.engine.C.check_verify()
+            except RuntimeError as e:
+                raise ChecksumError(f"all-reduce '{self.name}': {e}") from e
             return
         try:
             self.engine.C.synchronize(self.slot, -1.0 if timeout is None else float(timeout), self.seq)
         except RuntimeError as e:
+            if "verify:" in str(e):
+                raise ChecksumError(f"all-reduce '{self.name}': {e}") from e
             raise CommTimeoutError(f"all-reduce '{self.name}': {e}") from e
 
     def latency_ms(self) -> float | None:
@@ -97,10 +103,13 @@ class NativeAllReduce:
     def __init__(self, transport: Transport | None, *, codec: str = "bfp_rne", algo: str = "mesh", rings: int = 1,
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
                  timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None,
-                 side_stream: bool = False):
+                 side_stream: bool = False, verify: bool | None = None, fault: str | None = None):
         """``comm``: an explicit ``_C.Comm`` (e.g. ``_C.LoopbackFabric(N).comm(r)`` for virtual ranks on one
         GPU); otherwise the engine's own RCCL communicator is created from ``transport``. ``side_stream``
-        (world 1): run requests on the engine's comm stream instead of inline (overlap measurements)."""
+        (world 1): run requests on the engine's comm stream instead of inline (overlap measurements).
+        ``verify`` (default: env FAN_VERIFY): debug mode — every message carries a GPU-computed checksum + the
+        request sequence number, checked on arrival (csrc/comm/verify.h); ``fault``: test-only fault injection
+        rules (FAN_FAULT grammar, default from the environment)."""
         if algo not in _ALGOS:
             raise ValueError(f"unknown algo {algo!r}")
         C = _ext.require()
@@ -121,7 +130,10 @@ class NativeAllReduce:
         self.timeout_s = timeout_s
         self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
                                    compat_owner_fp32, timeout_s, stream_priority, force_comm or side_stream,
-                                   self.device.index)
+                                   self.device.index, -1 if verify is None else int(bool(verify)))
+        if fault is not None:
+            self.C.set_fault(fault)
+        self.verify = bool(self.C.verify)
         self.orders = [list(o) for o in self.C.orders]
         self.rings = len(self.orders)
         self.inline = bool(self.C.inline)

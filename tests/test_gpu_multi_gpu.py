@@ -24,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("transport", ["torch", "native"])
+@pytest.mark.parametrize("transport", ["torch", "native", "p2p"])
 def test_rccl_probe_all_gpus(transport):
     n = torch.cuda.device_count()
     if n < 2:

@@ -161,3 +161,18 @@ def test_p2p_data_parallel_trainer_two_ranks():
     assert np.array_equal(res[0]["w"], res[1]["w"]), "replicas diverged"
     for r in range(WORLD):
         assert np.all(np.isfinite(res[r]["losses"])) and res[r]["losses"][-1] < res[r]["losses"][0]
+
+
+def test_abort_releases_a_parked_stream():
+    """A stream parked on an unsatisfied P2P flag (the peer died) is released by P2PComm.abort() within seconds —
+    it does not hang the GPU or the destructor — and the communicator refuses further rounds. Runs in a child
+    process under a timeout (the probe's own watchdog exits if the stream stays parked)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "probes", "p2p_abort_probe.py")], cwd=root,
+                       capture_output=True, text=True, timeout=120)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "parked=True" in r.stdout and "UNBLOCKED" in r.stdout and "raises after abort" in r.stdout, out[-3000:]

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Multi-rank probe of the RCCL data path on whatever GPUs exist (ranks may share one GPU).
 
-Run: torchrun --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/dist_probe.py [--transport torch|native]
+Run: torchrun --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/dist_probe.py [--transport torch|native|p2p]
 Checks the engine (mesh / ring / multi-ring, BFP) against the spec simulator and the DP trainer's replica
 consistency over the real torch.distributed "nccl" (RCCL) backend. Prints one PASS/FAIL line per check.
 """
@@ -21,7 +21,7 @@ from fpga_ai_nic_amd.models.mlp import MLP  # noqa: E402
 from fpga_ai_nic_amd.parallel import sim  # noqa: E402
 from fpga_ai_nic_amd.parallel.allreduce import CompressedAllReduce  # noqa: E402
 from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine  # noqa: E402
-from fpga_ai_nic_amd.parallel.transport import NativeTransport, TorchDistTransport  # noqa: E402
+from fpga_ai_nic_amd.parallel.transport import NativeTransport, P2PTransport, TorchDistTransport  # noqa: E402
 
 
 def main():
@@ -33,7 +33,8 @@ def main():
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % ndev)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-    t = NativeTransport() if a.transport == "native" else TorchDistTransport()
+    # p2p: the Python engine's byte transport AND the C++ engine's communicator are the direct HIP-IPC peer transport
+    t = {"native": NativeTransport, "torch": TorchDistTransport, "p2p": P2PTransport}[a.transport]()
     ok_all = True
     n = 100_000
     rng = np.random.default_rng(11)
@@ -58,10 +59,11 @@ def main():
     from fpga_ai_nic_amd.ops import bfp_oracle as O
 
     nt = t if isinstance(t, NativeTransport) else NativeTransport()
+    comm = t.comm if isinstance(t, P2PTransport) else None  # C++ engine over the P2P communicator
     w0 = rng.standard_normal(n).astype(np.float32)
     for codec in ("bfp_rne", "bfp_trunc"):
         for algo, rings in (("mesh", 1), ("ring", 1), ("ring", min(7, max(1, world - 1)))):
-            eng = NativeAllReduce(nt, codec=codec, algo=algo, rings=rings, max_slice_elems=8192)
+            eng = NativeAllReduce(nt, codec=codec, algo=algo, rings=rings, max_slice_elems=8192, comm=comm)
             L = eng.layout(n)
             g = torch.zeros(L.n_pad, device=dev)
             g[:n] = torch.from_numpy(grads[rank]).to(dev)
@@ -89,7 +91,7 @@ def main():
             print(f"[rank {rank}] {'PASS' if ok else 'FAIL'} native engine codec={codec} algo={algo} rings={eng.rings} "
                   f"sum-bitexact + sgd<=1ulp ({ulp}) + replicas-identical={same} ({time.time() - t0:.2f}s)", flush=True)
     # uncompressed f32 wire over the C++ ring == RCCL's own all-reduce within fp32 reassociation
-    eng = NativeAllReduce(nt, codec="raw_f32", algo="ring", rings=1, max_slice_elems=8192)
+    eng = NativeAllReduce(nt, codec="raw_f32", algo="ring", rings=1, max_slice_elems=8192, comm=comm)
     L = eng.layout(n)
     g = torch.zeros(L.n_pad, device=dev)
     g[:n] = torch.from_numpy(grads[rank]).to(dev)
@@ -103,7 +105,7 @@ def main():
     ok_all &= ok
     print(f"[rank {rank}] {'PASS' if ok else 'FAIL'} raw f32 ring vs RCCL all_reduce max|diff|={err:.2e}", flush=True)
     # DP trainer replicas stay identical (C++ engine; bwd-weight GEMM encodes straight into the wire)
-    eng = make_engine(nt, "bfp", impl="native")
+    eng = make_engine(nt, "bfp", impl="native", comm=comm)
     sizes = [256, 512, 512, 256]
     model = MLP(sizes, dtype=torch.bfloat16, device=dev, pad_fn=lambda k: eng.layout(k).n_pad, seed=1)
     for l in model.layers:
