@@ -107,7 +107,8 @@ void register_engine(pybind11::module_& m) {
   namespace py = pybind11;
   py::class_<AllReduceEngine>(m, "AllReduceEngine")
       .def(py::init([](Comm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
-                       bool compat, double timeout_s, int priority, bool force_comm, int device, int verify) {
+                       bool compat, double timeout_s, int priority, bool force_comm, int device, int verify,
+                       int64_t chunk_elems) {
              EngineConfig c;
              c.codec = codec;
              c.algo = algo;
@@ -118,18 +119,19 @@ void register_engine(pybind11::module_& m) {
              c.stream_priority = priority;
              c.force_comm = force_comm;
              c.verify = verify;
+             c.chunk_elems = chunk_elems;
              return new AllReduceEngine(comm, rank, world, c, device);
            }),
            py::keep_alive<1, 2>(), py::arg("comm").none(true), py::arg("rank"), py::arg("world"), py::arg("codec"),
            py::arg("algo"), py::arg("rings"), py::arg("max_slice_elems"), py::arg("compat_owner_fp32"),
            py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"),
-           py::arg("verify") = -1)
+           py::arg("verify") = -1, py::arg("chunk_elems") = 0)
       .def("layout",
            [](AllReduceEngine& e, int64_t n) {
              const EngineLayout L = e.layout(n);
              return py::dict(py::arg("n") = L.n, py::arg("n_pad") = L.n_pad, py::arg("algo") = L.algo,
                              py::arg("shard") = L.shard, py::arg("slice") = L.slice, py::arg("blocks") = L.blocks,
-                             py::arg("rings") = L.rings, py::arg("part") = L.part);
+                             py::arg("rings") = L.rings, py::arg("part") = L.part, py::arg("chunks") = L.chunks);
            })
       .def("wire_bytes", [](AllReduceEngine& e, int64_t n) { return e.wire_bytes(e.layout(n)); })
       .def_property_readonly("orders", &AllReduceEngine::orders)
@@ -262,6 +264,7 @@ void register_engine(pybind11::module_& m) {
            },
            "perf counters (the NIC's latency / host-stall registers): requests, bytes, host wait, device time")
       .def("reset_counters", &AllReduceEngine::reset_counters)
+      .def_property_readonly("scratch_bytes", &AllReduceEngine::scratch_bytes)
       .def_property_readonly("requests", &AllReduceEngine::requests);
 }
 

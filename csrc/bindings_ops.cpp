@@ -29,7 +29,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux, bool accumulate,
           int64_t split_k, const c10::optional<at::Tensor>& workspace, int64_t tile_bm, int64_t tile_bn,
           const c10::optional<at::Tensor>& colsum, int64_t tile_waves, const c10::optional<at::Tensor>& wire,
-          int64_t wire_shard, int64_t wire_own, int64_t wire_codec) {
+          int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "A and B dtype mismatch");
   GemmArgs g{};
@@ -81,6 +81,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     g.wire = wire->data_ptr<uint8_t>();
     g.wire_shard = wire_shard;
     g.wire_own = (int)wire_own;
+    g.wire_period = (int)wire_period;
     g.wire_codec = (int)wire_codec;
   }
   if (A.scalar_type() == at::kBFloat16) {
@@ -158,7 +159,7 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("workspace") = pybind11::none(), pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0,
         pybind11::arg("colsum") = pybind11::none(), pybind11::arg("tile_waves") = 0,
         pybind11::arg("wire") = pybind11::none(), pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1,
-        pybind11::arg("wire_codec") = 1);
+        pybind11::arg("wire_codec") = 1, pybind11::arg("wire_period") = 0);
   m.def("gemm_supported", &gemm_supported);
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);

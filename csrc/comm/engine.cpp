@@ -29,7 +29,15 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     for (int i = 0; i < world; ++i) orders_[0][i] = i;
   }
   inline_ = world == 1 && !cfg.force_comm;
+  if (cfg_.chunk_elems <= 0) {
+    const char* ce = std::getenv("FAN_CHUNK_ELEMS");
+    cfg_.chunk_elems = ce ? std::atoll(ce) : (int64_t(1) << 25);
+  }
+  FAN_CHECK(cfg_.chunk_elems >= 256, "chunk_elems must be >= 256");
   FAN_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, cfg.stream_priority));
+  FAN_HIP_CHECK(hipStreamCreateWithPriority(&aux_stream_, hipStreamNonBlocking, cfg.stream_priority));
+  for (auto& row : cev_)
+    for (auto& e : row) FAN_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   run_stream_ = stream_;
   void* h = nullptr;
   FAN_HIP_CHECK(hipHostMalloc(&h, kSlots * 64, hipHostMallocMapped));
@@ -66,6 +74,9 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
 
 AllReduceEngine::~AllReduceEngine() {
   hipStreamSynchronize(stream_);
+  hipStreamSynchronize(aux_stream_);
+  for (auto& row : cev_)
+    for (auto& e : row) hipEventDestroy(e);
   for (auto& s : slots_) {
     hipEventSynchronize(s.done);  // epilogues may have run on a producer stream and still read the scratch
     hipEventDestroy(s.ready);
@@ -82,6 +93,7 @@ AllReduceEngine::~AllReduceEngine() {
   if (tags_) hipFree(tags_);
   if (verr_dev_) hipFree(verr_dev_);
   if (verr_host_) hipHostFree(verr_host_);
+  hipStreamDestroy(aux_stream_);
   hipStreamDestroy(stream_);
 }
 
@@ -91,8 +103,12 @@ EngineLayout AllReduceEngine::layout(int64_t n) const {
   L.algo = cfg_.algo;
   const int N = world_;
   if (cfg_.algo == 0) {
-    L.shard = round_up(std::max<int64_t>(cdiv(n, N), 1), 256);
-    L.n_pad = L.shard * N;
+    // buckets above chunk_elems stream through the collectives in balanced chunks of N shards (multi-rank path
+    // only: the inline world-1 engine has no collectives to pipeline)
+    const bool local = N == 1 && !cfg_.force_comm;
+    L.chunks = local ? 1 : std::max<int64_t>(1, cdiv(n, cfg_.chunk_elems));
+    L.shard = round_up(std::max<int64_t>(cdiv(n, N * L.chunks), 1), 256);
+    L.n_pad = L.shard * N * L.chunks;
     return L;
   }
   const int R = (int)orders_.size();
@@ -109,7 +125,7 @@ EngineLayout AllReduceEngine::layout(int64_t n) const {
 int64_t AllReduceEngine::wire_bytes(const EngineLayout& L) const {
   const int N = world_;
   if (N == 1) return 0;
-  if (L.algo == 0) return 2 * (N - 1) * (int64_t)wire_shard_bytes(cfg_.codec, L.shard);
+  if (L.algo == 0) return 2 * (N - 1) * L.chunks * (int64_t)wire_shard_bytes(cfg_.codec, L.shard);
   return (int64_t)L.rings * L.blocks * 2 * (N - 1) * (int64_t)wire_shard_bytes(cfg_.codec, L.slice);
 }
 
@@ -151,7 +167,8 @@ std::array<int64_t, 3> AllReduceEngine::prepack_shape(int64_t n) const {
   if (cfg_.algo != 0 || (cfg_.codec != kBfpTrunc && cfg_.codec != kBfpRne)) return {0, 0, -1};
   const EngineLayout L = layout(n);
   const bool local = (world_ == 1 && !cfg_.force_comm) || comm_ == nullptr;
-  return {L.shard, world_, local ? -1 : rank_};
+  // chunked buckets: the owner shard of chunk c is wire shard c*N + rank (owner = shard index mod N)
+  return {L.shard, world_ * L.chunks, local ? -1 : rank_};
 }
 
 std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const void* grad, int gdt,
@@ -176,6 +193,8 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     launch_wire_reduce(c, gdt, S, sb, 1, 0, g, S, nullptr, (size_t)s, st);
     return {[=](hipStream_t es) { epilogue(c, es, S, s, 1, 0, s, master, lp, mom, n_valid, p, update, out_sum); }};
   }
+  if (L.chunks > 1)
+    return run_mesh_chunked(L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked, cur_defer_);
   uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
   const uint8_t* P = prepacked ? prepacked : g;
   const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
@@ -216,6 +235,97 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
   }
   const int64_t n_pad = L.n_pad;
   return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
+}
+
+// Chunked mesh (buckets above chunk_elems): the reference's block pipeline (hw/all_reduce.sv:330, 423-464,
+// 1033-1061) re-expressed over two streams. Chunk c = N shards of L.shard elements (wire shards c*N .. c*N+N-1).
+//   comm stream (every collective, in one order on every rank): pack(c), all_to_all(c), all_gather(c-1), ...
+//   aux stream: owner reduce(c) [after all_to_all(c)], per-chunk decode+SGD epilogue(c-1) [after all_gather(c-1)]
+// so chunk c's reduce / chunk c-1's epilogue run while the links carry chunk c's / c+1's exchange. Pack, receive
+// and reduce buffers are double-buffered by chunk parity, so scratch is bounded by two chunks whatever the bucket
+// size — except the gathered wire of a DEFERRED request, which its epilogue reads at commit (per slot, whole
+// bucket: 17 B per 16 values). Buffer reuse is ordered by the stream order plus one wait each way:
+//   P[c%2], R[c%2] rewritten by pack/all_to_all(c+2) after reduce(c) (comm waits reduce(c) before all_to_all(c+2))
+//   S[c%2] rewritten by reduce(c+2) after all_gather(c): all_gather(c) precedes all_to_all(c+2) on the comm stream
+//   G[c%2] rewritten by all_gather(c+2) after epilogue(c): reduce(c+2), which all_gather(c+2) waits for, follows
+//   epilogue(c) on the aux stream.
+std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, const void* grad, int gdt,
+                                                        float* master, bf16_t* lp, float* mom, int64_t n_valid,
+                                                        SgdParams p, bool update, float* out_sum,
+                                                        const uint8_t* prepacked, bool defer) {
+  const int N = world_, r = rank_, c = cfg_.codec;
+  const int64_t s = L.shard, C = L.chunks;
+  const size_t sb = wire_shard_bytes(c, s), cb = sb * N;  // one shard / one chunk of wire
+  const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
+  hipStream_t A = run_stream_, B = aux_stream_;
+  const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
+  const std::string k = std::to_string(sb);
+  uint8_t *Pb[2] = {nullptr, nullptr}, *R[2], *S[2], *Gc[2] = {nullptr, nullptr};
+  for (int q = 0; q < 2; ++q) {
+    if (!zero_copy && !prepacked) Pb[q] = scratch("meshc_P" + std::to_string(q) + "_" + k, cb);
+    R[q] = scratch("meshc_R" + std::to_string(q) + "_" + k, cb);
+    S[q] = scratch("meshc_S" + std::to_string(q) + "_" + k, sb);
+    if (!defer) Gc[q] = scratch("meshc_G" + std::to_string(q) + "_" + k, cb);
+  }
+  uint8_t* Gall = defer ? epi_scratch("meshc_Gall_" + k + "_" + std::to_string(C), cb * C) : nullptr;
+  auto gath = [&](int64_t ch) { return defer ? Gall + ch * cb : Gc[ch % 2]; };
+  auto gather = [&](int64_t ch) {  // comm stream: all-gather of chunk ch's reduced owner shard
+    RoctxRange rr("fan/mesh/all_gather");
+    FAN_HIP_CHECK(hipStreamWaitEvent(A, cev_[1][ch % 2], 0));
+    if (verify_) launch_msg_tags(S[ch % 2], sb, sb, 1, req_seq_, tag_region(3), A);
+    fault_.maybe_corrupt("mesh_reduce", S[ch % 2], sb, A);
+    comm_->all_gather(S[ch % 2], gath(ch), sb, A);
+    if (verify_) {
+      comm_->all_gather(tag_region(3), tag_region(4), 16, A);
+      verify_rows(gath(ch), sb, N, tag_region(4), 2, (uint32_t)(ch * N), A);
+    }
+    if (!defer) {  // per-chunk epilogue on the aux stream
+      FAN_HIP_CHECK(hipEventRecord(cev_[2][ch % 2], A));
+      FAN_HIP_CHECK(hipStreamWaitEvent(B, cev_[2][ch % 2], 0));
+      RoctxRange re("fan/mesh/epilogue");
+      epilogue(c, B, gath(ch), s, N, ch * N * s, N * s, master, lp, mom, n_valid, p, update, out_sum);
+    }
+  };
+  for (int64_t ch = 0; ch < C; ++ch) {
+    const uint8_t* P;
+    if (prepacked) {
+      P = prepacked + ch * cb;
+    } else if (zero_copy) {
+      P = g + (size_t)ch * N * s * esize(gdt);
+    } else {
+      RoctxRange rr("fan/mesh/pack");
+      launch_wire_pack(c, gdt, g + (size_t)ch * N * s * esize(gdt), Pb[ch % 2], (size_t)s, N, A);
+      P = Pb[ch % 2];
+    }
+    {
+      RoctxRange rr("fan/mesh/all_to_all");
+      if (ch >= 2) FAN_HIP_CHECK(hipStreamWaitEvent(A, cev_[1][ch % 2], 0));  // reduce(ch-2) done with R, P
+      if (verify_) launch_msg_tags(P, sb, sb, N, req_seq_, tag_region(0), A);
+      fault_.maybe_corrupt("mesh_pack", const_cast<uint8_t*>(P), cb, A);
+      comm_->all_to_all(P, R[ch % 2], sb, A);
+      if (verify_) {
+        comm_->all_to_all(tag_region(0), tag_region(1), 16, A);
+        verify_rows(R[ch % 2], sb, N, tag_region(1), 1, (uint32_t)(ch * N), A);
+      }
+      FAN_HIP_CHECK(hipEventRecord(cev_[0][ch % 2], A));
+    }
+    {
+      RoctxRange rr("fan/mesh/reduce");
+      FAN_HIP_CHECK(hipStreamWaitEvent(B, cev_[0][ch % 2], 0));
+      launch_wire_reduce(c, gdt, R[ch % 2], sb, N, r, g + ((size_t)ch * N + r) * s * esize(gdt), S[ch % 2], nullptr,
+                         (size_t)s, B);
+      FAN_HIP_CHECK(hipEventRecord(cev_[1][ch % 2], B));
+    }
+    if (ch >= 1) gather(ch - 1);
+  }
+  gather(C - 1);
+  // the request's completion on the comm stream covers the aux stream's last reduce / epilogue
+  FAN_HIP_CHECK(hipEventRecord(cev_[3][1], B));
+  FAN_HIP_CHECK(hipStreamWaitEvent(A, cev_[3][1], 0));
+  if (!defer) return {};
+  const int64_t n_pad = L.n_pad, shards = C * N;
+  uint8_t* G = Gall;
+  return {[=](hipStream_t es) { epilogue(c, es, G, s, (int)shards, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
 }
 
 std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const void* grad, int gdt,
@@ -388,6 +498,7 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   // buffers the deferred epilogue reads are per slot: a later request of the same size must not overwrite
   // them before this one commits (the trainer commits every request at the end of backward)
   epi_slot_ = slot;
+  cur_defer_ = defer;
   trace_marked_ = 1u << kTpStart;
   sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum,
                                         prepacked, prepacked_elems)

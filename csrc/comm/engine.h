@@ -37,12 +37,16 @@ struct EngineConfig {
   int stream_priority = -1;
   bool force_comm = false;  // world 1 still runs the collectives (exercises the multi-rank path)
   int verify = -1;          // debug verify mode (message tags + sequence numbers); -1: from FAN_VERIFY
+  // mesh: buckets above this many elements stream through the collectives in chunks (block pipeline, bounded
+  // scratch); 0: from FAN_CHUNK_ELEMS, default 32 Mi elements (128 MB of f32 gradient)
+  int64_t chunk_elems = 0;
 };
 
 struct EngineLayout {
   int64_t n = 0, n_pad = 0;
   int algo = 0;
-  int64_t shard = 0;        // mesh
+  int64_t shard = 0;        // mesh (per chunk)
+  int64_t chunks = 1;       // mesh: chunks of N shards each (shard-major: shard s of chunk c is wire shard c*N+s)
   int64_t slice = 0;        // ring
   int64_t blocks = 0;       // ring
   int rings = 1;
@@ -147,6 +151,12 @@ class AllReduceEngine {
   const EngineCounters& counters() const { return counters_; }
   void reset_counters() { counters_ = EngineCounters{}; }
   int64_t wire_bytes(const EngineLayout& L) const;
+  // device scratch the engine holds (wire staging buffers; per-slot gathered wire of deferred requests)
+  size_t scratch_bytes() const {
+    size_t t = 0;
+    for (const auto& kv : scratch_) t += kv.second.second;
+    return t;
+  }
 
  private:
   struct Slot {
@@ -175,6 +185,9 @@ class AllReduceEngine {
   std::vector<EpiThunk> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                               float* out_sum, const uint8_t* prepacked, int64_t prepacked_elems);
+  std::vector<EpiThunk> run_mesh_chunked(const EngineLayout& L, const void* grad, int gdt, float* master,
+                                         bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
+                                         float* out_sum, const uint8_t* prepacked, bool defer);
   std::vector<EpiThunk> run_ring(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                               float* out_sum);
@@ -184,6 +197,8 @@ class AllReduceEngine {
   EngineConfig cfg_;
   std::vector<std::vector<int>> orders_;
   hipStream_t stream_ = nullptr;
+  hipStream_t aux_stream_ = nullptr;  // chunked mesh: owner reduces + per-chunk epilogues beside the collectives
+  hipEvent_t cev_[4][2] = {};         // chunked mesh pipeline events: [all-to-all, reduce, all-gather, epilogue][parity]
   bool epi_on_producer_ = false;
   // world 1 without forced collectives: nothing to overlap, so requests run inline on the producer's
   // stream (no cross-stream event packets); run_stream_ is the stream of the request being issued.
@@ -198,6 +213,7 @@ class AllReduceEngine {
   EngineCounters counters_;
   std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
   int epi_slot_ = 0;  // slot of the request being built
+  bool cur_defer_ = false;  // the request being built defers its epilogue
   bool tracing_ = false;
   std::vector<RequestTrace> trace_pool_;
   size_t trace_used_ = 0;

@@ -48,6 +48,7 @@ struct GemmArgs {
   uint8_t* wire = nullptr;
   int64_t wire_shard = 0;
   int wire_own = -1;
+  int wire_period = 0;  // > 0: every shard s with s % wire_period == wire_own is owned (chunked mesh buckets)
   int wire_codec = 1;  // kBfpTrunc or kBfpRne
 };
 

@@ -209,6 +209,7 @@ struct WireOut {
   uint8_t* p;
   int64_t shard;  // elements per shard (multiple of 256)
   int own;        // shard also written to C in f32 (-1: none)
+  int period;     // > 0: shards s with s % period == own are all written (chunked buckets: one owner shard per chunk)
   int codec;      // kBfpTrunc / kBfpRne
   float inv_shard;  // 1 / shard (shard index without a 64-bit integer division)
   int bias_off;     // > 0: flat offset of the bias segment, encoded from the fused column sum
@@ -256,7 +257,8 @@ __device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const
 __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
                                            int row, int col) {
   const uint32_t f = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
-  if (wire_store16(v, f, wo) == wo.own) {
+  const int sh = wire_store16(v, f, wo);
+  if ((wo.period > 0 ? sh % wo.period : sh) == wo.own) {
 #pragma unroll
     for (int u = 0; u < 16; u += 4)
       *reinterpret_cast<float4*>(C + f + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
@@ -850,7 +852,7 @@ void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
 void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
-  const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_codec,
+  const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_period, a.wire_codec,
                    a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
                    a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0
 #ifdef FAN_GEMM_STAMPS

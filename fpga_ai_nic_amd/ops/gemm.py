@@ -49,15 +49,17 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
     ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only).
     ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N]).
-    ``wire=(buf_u8, shard_elems, own_shard, codec_id)``: BFP-encode the f32 result straight into all-reduce
-    wire shards (flat index m*ldc + n; shard ``own_shard`` is also written to C) — bf16 bwd-weight only."""
+    ``wire=(buf_u8, shard_elems, own_shard, codec_id[, period])``: BFP-encode the f32 result straight into all-reduce
+    wire shards (flat index m*ldc + n; shard ``own_shard`` — with ``period``, every shard s with s % period ==
+    own_shard — is also written to C) — bf16 bwd-weight only."""
     if wire is not None:
         if not C.is_cuda or A.dtype != torch.bfloat16 or not a_t or b_t:
             raise ValueError("wire epilogue: bf16 GPU bwd-weight layout only")
         Cx = _ext.require()
         M, K, N = A.shape[1], A.shape[0], B.shape[1]
         tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
-        buf, shard, own, codec = wire
+        buf, shard, own, codec = wire[:4]
+        period = int(wire[4]) if len(wire) > 4 else 0
         sk = 0 if split_k is None else int(split_k)
         bm, bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
         if bm == 0:
@@ -65,7 +67,7 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
         tbm, tbn = bm, bn  # launch exactly the planned tile (re-planning with an explicit split_k differs)
         ws = _workspace(C.device, sk * (M * N + N)) if sk > 1 else None
         Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, tbm, tbn, colsum, tw, buf, int(shard),
-                int(own), int(codec))
+                int(own), int(codec), period)
         return C
     if C.is_cuda:
         Cx = _ext.require()

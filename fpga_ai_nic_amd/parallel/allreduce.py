@@ -120,6 +120,7 @@ class BucketLayout:
     blocks: int = 0         # ring: blocks per ring part
     rings: int = 1
     part: int = 0           # ring: padded elements per ring part
+    chunks: int = 1         # mesh (C++ engine): chunks of `world` shards streamed through the collectives
 
     @property
     def key(self):

@@ -103,13 +103,16 @@ class NativeAllReduce:
     def __init__(self, transport: Transport | None, *, codec: str = "bfp_rne", algo: str = "mesh", rings: int = 1,
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
                  timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None,
-                 side_stream: bool = False, verify: bool | None = None, fault: str | None = None):
+                 side_stream: bool = False, verify: bool | None = None, fault: str | None = None,
+                 chunk_elems: int = 0):
         """``comm``: an explicit ``_C.Comm`` (e.g. ``_C.LoopbackFabric(N).comm(r)`` for virtual ranks on one
         GPU); otherwise the engine's own RCCL communicator is created from ``transport``. ``side_stream``
         (world 1): run requests on the engine's comm stream instead of inline (overlap measurements).
         ``verify`` (default: env FAN_VERIFY): debug mode — every message carries a GPU-computed checksum + the
         request sequence number, checked on arrival (csrc/comm/verify.h); ``fault``: test-only fault injection
-        rules (FAN_FAULT grammar, default from the environment)."""
+        rules (FAN_FAULT grammar, default from the environment). ``chunk_elems`` (mesh, multi-rank): buckets above it
+        stream through the collectives in chunks — all-to-all / owner reduce / all-gather / epilogue pipelined over
+        two streams with scratch bounded by two chunks (0: env FAN_CHUNK_ELEMS, default 32 Mi elements)."""
         if algo not in _ALGOS:
             raise ValueError(f"unknown algo {algo!r}")
         C = _ext.require()
@@ -130,7 +133,7 @@ class NativeAllReduce:
         self.timeout_s = timeout_s
         self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
                                    compat_owner_fp32, timeout_s, stream_priority, force_comm or side_stream,
-                                   self.device.index, -1 if verify is None else int(bool(verify)))
+                                   self.device.index, -1 if verify is None else int(bool(verify)), int(chunk_elems))
         if fault is not None:
             self.C.set_fault(fault)
         self.verify = bool(self.C.verify)
@@ -177,14 +180,15 @@ class NativeAllReduce:
     def layout(self, n: int) -> BucketLayout:
         d = self.C.layout(int(n))
         return BucketLayout(n=d["n"], n_pad=d["n_pad"], algo=self.algo, world=self.world, shard=d["shard"],
-                            slice_elems=d["slice"], blocks=d["blocks"], rings=d["rings"], part=d["part"])
+                            slice_elems=d["slice"], blocks=d["blocks"], rings=d["rings"], part=d["part"],
+                            chunks=d["chunks"])
 
     def wire_bytes(self, L: BucketLayout) -> int:
         return int(self.C.wire_bytes(L.n))
 
     def prepack_target(self, grad: torch.Tensor, n: int, static_from: int | None = None):
         """Wire target for a producer that encodes the gradient itself (GEMM ``kEpiWire`` epilogue):
-        ``(wire_u8, shard_elems, own_shard, codec_id)`` — one persistent buffer per gradient bucket — or None
+        ``(wire_u8, shard_elems, own_shard, codec_id, period)`` — one persistent buffer per gradient bucket — or None
         when this configuration (ring / raw codec) cannot take prepacked input.
 
         ``static_from``: flat elements [static_from, padded end) are always zero (padding, or a bias segment
@@ -204,7 +208,7 @@ class NativeAllReduce:
                 _ext.require().wire_pack_range(torch.zeros(total, device=self.device), buf, shard, static_from,
                                                total, self.codec_id)
             self._prepack_bufs[key] = buf
-        return buf, shard, own, self.codec_id
+        return buf, shard, own, self.codec_id, self.world  # owner shard period: one owner shard per chunk
 
     def allreduce_sgd(self, grad: torch.Tensor, master: torch.Tensor, lp: torch.Tensor | None = None,
                       mom: torch.Tensor | None = None, *, n_valid: int | None = None, lr: float,

@@ -134,3 +134,53 @@ def test_loopback_fault_drop_raises_not_hangs():
     assert all(e is not None for e in errs)
     assert "fault injection" in str(errs[1])
     assert any("timed out" in str(e) or "aborted" in str(e) for e in (errs[0], errs[2]))
+
+
+@pytest.mark.parametrize("N", [2, 3])
+def test_chunked_mesh_bitexact_and_bounded(N):
+    """Buckets above chunk_elems stream through the collectives chunk by chunk (two-stream block pipeline): every
+    chunk is its own N-shard mesh all-reduce, so the result is bit-exact vs the spec simulator applied per chunk,
+    for the immediate (per-chunk epilogue on the aux stream) and the deferred epilogue; the engine's scratch stays
+    bounded by two chunks for immediate requests."""
+    C = _ext.require()
+    fabric = C.LoopbackFabric(N, 60.0)
+    n, chunk = 50_000, 8_192
+    rng = np.random.default_rng(N + 40)
+    grads = [rng.standard_normal(n).astype(np.float32) * (1 + r) for r in range(N)]
+    w0 = rng.standard_normal(n).astype(np.float32)
+    engines = [NativeAllReduce(None, codec="bfp_rne", comm=fabric.comm(r), chunk_elems=chunk) for r in range(N)]
+    L = engines[0].layout(n)
+    assert L.chunks == -(-n // chunk) and L.n_pad == L.shard * N * L.chunks
+
+    def fn(r):
+        eng = engines[r]
+        g = torch.zeros(L.n_pad, device="cuda")
+        g[:n] = torch.from_numpy(grads[r]).cuda()
+        out = torch.zeros(L.n_pad, device="cuda")
+        w = torch.zeros(L.n_pad, device="cuda")
+        w[:n] = torch.from_numpy(w0).cuda()
+        w2 = w.clone()
+        torch.cuda.synchronize()
+        eng.allreduce(g, out, n_valid=n).synchronize(60)
+        eng.allreduce_sgd(g, w, None, n_valid=n, lr=0.5).synchronize(60)  # immediate: per-chunk epilogues
+        h = eng.allreduce_sgd(g, w2, None, n_valid=n, lr=0.5, defer=True)  # deferred: one epilogue at commit
+        h.commit_after_current()
+        h.synchronize(60)
+        torch.cuda.synchronize()
+        return out.cpu().numpy(), w.cpu().numpy(), w2.cpu().numpy()
+
+    res, errs = _threads(N, fn)
+    for e in errs:
+        if e is not None:
+            raise e
+    cw = L.shard * N
+    gin = [np.pad(x, (0, L.n_pad - n)) for x in grads]
+    exp = np.concatenate([sim.mesh_allreduce([x[c * cw:(c + 1) * cw] for x in gin], L.shard, "bfp_rne")
+                          for c in range(L.chunks)])
+    ref_w, _ = O.sgd(w0, exp[:n], 0.5)
+    for r in range(N):
+        assert np.array_equal(res[r][0][:n], exp[:n]), f"rank {r}: chunked sum mismatch"
+        for w in (res[r][1], res[r][2]):
+            ulp = np.abs(w[:n].view(np.int32).astype(np.int64) - ref_w.view(np.int32).astype(np.int64))
+            assert ulp.max() <= 1
+        assert np.array_equal(res[r][1], res[0][1]) and np.array_equal(res[r][2], res[r][1])
