@@ -108,7 +108,7 @@ void register_engine(pybind11::module_& m) {
   py::class_<AllReduceEngine>(m, "AllReduceEngine")
       .def(py::init([](Comm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
                        bool compat, double timeout_s, int priority, bool force_comm, int device, int verify,
-                       int64_t chunk_elems) {
+                       int64_t chunk_elems, c10::optional<std::vector<std::vector<int>>> links) {
              EngineConfig c;
              c.codec = codec;
              c.algo = algo;
@@ -120,12 +120,20 @@ void register_engine(pybind11::module_& m) {
              c.force_comm = force_comm;
              c.verify = verify;
              c.chunk_elems = chunk_elems;
+             if (links) {
+               TORCH_CHECK((int)links->size() == world, "links: world x world expected");
+               c.links.assign((size_t)world * world, 0);
+               for (int a = 0; a < world; ++a) {
+                 TORCH_CHECK((int)(*links)[a].size() == world, "links: world x world expected");
+                 for (int b = 0; b < world; ++b) c.links[(size_t)a * world + b] = (*links)[a][b] != 0;
+               }
+             }
              return new AllReduceEngine(comm, rank, world, c, device);
            }),
            py::keep_alive<1, 2>(), py::arg("comm").none(true), py::arg("rank"), py::arg("world"), py::arg("codec"),
            py::arg("algo"), py::arg("rings"), py::arg("max_slice_elems"), py::arg("compat_owner_fp32"),
            py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"),
-           py::arg("verify") = -1, py::arg("chunk_elems") = 0)
+           py::arg("verify") = -1, py::arg("chunk_elems") = 0, py::arg("links") = py::none())
       .def("layout",
            [](AllReduceEngine& e, int64_t n) {
              const EngineLayout L = e.layout(n);

@@ -197,7 +197,20 @@ void register_planner(pybind11::module_& m) {
     for (auto& r : rounds) out.push_back({r.send_slice, r.send_src, r.recv_slice, r.recv_full, r.owned});
     return out;
   });
-  m.def("ring_orders", &ring_orders, pybind11::arg("world"), pybind11::arg("max_rings"));
+  m.def(
+      "ring_orders",
+      [](int world, int max_rings, c10::optional<std::vector<std::vector<int>>> links) {
+        if (!links) return ring_orders(world, max_rings);
+        std::vector<char> l((size_t)world * world, 0);
+        TORCH_CHECK((int)links->size() == world, "links: world rows expected");
+        for (int a = 0; a < world; ++a) {
+          TORCH_CHECK((int)(*links)[a].size() == world, "links: world columns expected");
+          for (int b = 0; b < world; ++b) l[(size_t)a * world + b] = (*links)[a][b] != 0;
+        }
+        return ring_orders(world, max_rings, &l);
+      },
+      pybind11::arg("world"), pybind11::arg("max_rings"), pybind11::arg("links") = pybind11::none(),
+      "arc-disjoint directed Hamiltonian rings over the (optional) link matrix links[a][b]: a can send to b");
 }
 
 }  // namespace fan

@@ -23,7 +23,8 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
   FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
   FAN_CHECK(world == 1 || comm != nullptr, "world > 1 needs a communicator");
   FAN_HIP_CHECK(hipSetDevice(device));
-  orders_ = cfg.algo == 1 ? ring_orders(world, cfg.rings) : std::vector<std::vector<int>>{{}};
+  orders_ = cfg.algo == 1 ? ring_orders(world, cfg.rings, cfg.links.empty() ? nullptr : &cfg.links)
+                          : std::vector<std::vector<int>>{{}};
   if (cfg.algo != 1) {
     orders_[0].resize(world);
     for (int i = 0; i < world; ++i) orders_[0][i] = i;

@@ -40,6 +40,8 @@ struct EngineConfig {
   // mesh: buckets above this many elements stream through the collectives in chunks (block pipeline, bounded
   // scratch); 0: from FAN_CHUNK_ELEMS, default 32 Mi elements (128 MB of f32 gradient)
   int64_t chunk_elems = 0;
+  // ring: direct links (row-major world x world, links[a*world+b]: a can send to b); empty = fully connected
+  std::vector<char> links;
 };
 
 struct EngineLayout {

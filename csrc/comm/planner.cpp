@@ -45,14 +45,19 @@ std::vector<RingRound> ring_plan(int N, int p, int64_t blocks) {
   return out;
 }
 
-std::vector<std::vector<int>> ring_orders(int N, int max_rings) {
+std::vector<std::vector<int>> ring_orders(int N, int max_rings, const std::vector<char>* links) {
   std::vector<std::vector<int>> best;
   if (N <= 1) return {{0}};
+  if (links && (int64_t)links->size() != (int64_t)N * N)
+    throw std::invalid_argument("ring_orders: links must be world x world");
+  // path arc u -> v carries data v -> u (position p sends to p - 1): it needs the link v -> u
+  auto link = [&](int u, int v) { return links == nullptr || (*links)[(size_t)v * N + u] != 0; };
   if (N == 2) return {{0, 1}};
   const int limit = std::max(1, std::min(max_rings, N - 1));
   for (int R = limit; R >= 1; --R) {
     std::vector<std::vector<char>> used(N, std::vector<char>(N, 0));
-    for (int i = 0; i < N; ++i) used[i][i] = 1;
+    for (int i = 0; i < N; ++i)
+      for (int j = 0; j < N; ++j) used[i][j] = i == j || !link(i, j);
     std::vector<std::vector<int>> cycles;
     long budget = 2000000;  // bounded search (N <= 16 in practice)
     std::function<bool(int)> find_cycle = [&](int k) -> bool {

@@ -39,8 +39,12 @@ struct RingGeometry {
 RingGeometry ring_geometry(int64_t n, int world, int64_t max_slice_elems);
 std::vector<RingRound> ring_plan(int world, int position, int64_t blocks);
 
-// Arc-disjoint directed Hamiltonian cycles of the complete digraph on `world` vertices
-// (up to world-1 rings; fewer when no decomposition exists, e.g. world 4 and 6).
-std::vector<std::vector<int>> ring_orders(int world, int max_rings);
+// Arc-disjoint directed Hamiltonian cycles of the link digraph on `world` vertices (up to world-1 rings; fewer
+// when no decomposition exists, e.g. world 4 and 6 on a complete graph). `links` (row-major world x world,
+// links[a * world + b] != 0: rank a can send to rank b over a direct link; nullptr: complete graph, the 8-GPU
+// fully connected xGMI node) restricts the rings to physical links — the reference builds its single ring from
+// the physical Ethernet wiring the same way (sw/setup_route.sh:12-40). With no Hamiltonian cycle over the links
+// the identity order is returned (the transport then routes the missing hops).
+std::vector<std::vector<int>> ring_orders(int world, int max_rings, const std::vector<char>* links = nullptr);
 
 }  // namespace fan

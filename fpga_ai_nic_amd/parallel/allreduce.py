@@ -102,10 +102,13 @@ def _py_ring_plan(N, p, blocks):  # identical to csrc/comm/planner.cpp (used onl
     return out
 
 
-def ring_orders(world: int, max_rings: int):
+def ring_orders(world: int, max_rings: int, links=None):
+    """Arc-disjoint directed Hamiltonian rings (native planner); ``links[a][b]`` truthy: rank a has a direct link
+    to rank b (None: fully connected)."""
     C = _ext.load()
     if C is not None:
-        return [list(o) for o in C.ring_orders(int(world), int(max_rings))]
+        lk = None if links is None else [[int(bool(x)) for x in row] for row in links]
+        return [list(o) for o in C.ring_orders(int(world), int(max_rings), lk)]
     return [list(range(world))]
 
 

@@ -104,7 +104,7 @@ class NativeAllReduce:
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
                  timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None,
                  side_stream: bool = False, verify: bool | None = None, fault: str | None = None,
-                 chunk_elems: int = 0):
+                 chunk_elems: int = 0, links="auto"):
         """``comm``: an explicit ``_C.Comm`` (e.g. ``_C.LoopbackFabric(N).comm(r)`` for virtual ranks on one
         GPU); otherwise the engine's own RCCL communicator is created from ``transport``. ``side_stream``
         (world 1): run requests on the engine's comm stream instead of inline (overlap measurements).
@@ -112,7 +112,9 @@ class NativeAllReduce:
         request sequence number, checked on arrival (csrc/comm/verify.h); ``fault``: test-only fault injection
         rules (FAN_FAULT grammar, default from the environment). ``chunk_elems`` (mesh, multi-rank): buckets above it
         stream through the collectives in chunks — all-to-all / owner reduce / all-gather / epilogue pipelined over
-        two streams with scratch bounded by two chunks (0: env FAN_CHUNK_ELEMS, default 32 Mi elements)."""
+        two streams with scratch bounded by two chunks (0: env FAN_CHUNK_ELEMS, default 32 Mi elements).
+        ``links`` (ring): direct-link matrix the rings must follow (``"auto"``: this node's xGMI links from
+        :func:`~fpga_ai_nic_amd.utils.topology.link_matrix`; None: fully connected)."""
         if algo not in _ALGOS:
             raise ValueError(f"unknown algo {algo!r}")
         C = _ext.require()
@@ -131,9 +133,17 @@ class NativeAllReduce:
             comm = transport.comm
         self.codec, self.codec_id, self.algo = codec, wire.codec_id(codec), algo
         self.timeout_s = timeout_s
+        if isinstance(links, str):
+            links = None
+            if algo == "ring" and self.world > 1 and not isinstance(comm, C.LoopbackComm):
+                from ..utils import topology
+
+                links = topology.link_matrix(self.world)
+        self.links = links
         self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
                                    compat_owner_fp32, timeout_s, stream_priority, force_comm or side_stream,
-                                   self.device.index, -1 if verify is None else int(bool(verify)), int(chunk_elems))
+                                   self.device.index, -1 if verify is None else int(bool(verify)), int(chunk_elems),
+                                   links)
         if fault is not None:
             self.C.set_fault(fault)
         self.verify = bool(self.C.verify)

@@ -53,16 +53,34 @@ def rocm_smi_links():
     return links
 
 
-def ring_orders(world: int, max_rings: int | None = None):
+def link_matrix(world: int):
+    """Direct-link matrix of the first ``world`` GPUs (rank r = device r, one process per GPU on one node):
+    links[a][b] = 1 when a reaches b over xGMI — rocm-smi's link type when it reports one (XGMI), else HIP peer
+    access. None when the devices are not all visible (the planner then assumes a fully connected node)."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < world:
+        return None
+    peer = peer_matrix()
+    types = rocm_smi_links()
+    out = [[0] * world for _ in range(world)]
+    for a in range(world):
+        for b in range(world):
+            if a == b:
+                continue
+            t = types.get((a, b))
+            out[a][b] = int(t.upper() == "XGMI") if t else int(peer[a][b])
+    return out
+
+
+def ring_orders(world: int, max_rings: int | None = None, links=None):
     from ..parallel.allreduce import ring_orders as _ro
 
-    return _ro(world, world - 1 if max_rings is None else max_rings)
+    return _ro(world, world - 1 if max_rings is None else max_rings, links)
 
 
 def report(world: int | None = None) -> dict:
     devs = device_info()
     n = world or max(1, len(devs))
-    rings = ring_orders(n)
+    rings = ring_orders(n, links=link_matrix(n))
     return {"devices": devs, "peer_access": peer_matrix(), "links": {f"{k[0]}-{k[1]}": v for k, v in
                                                                      rocm_smi_links().items()},
             "world": n, "rings": rings,

@@ -115,3 +115,34 @@ def test_gemm_plan_env_override():
     env["FAN_GEMM_PLAN"] = "8192x4096x1024=96,256,1"
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "FAN_GEMM_PLAN" in r.stderr
+
+
+def _check_rings(orders, N, links=None):
+    arcs = set()
+    for o in orders:
+        assert sorted(o) == list(range(N))
+        for p in range(N):
+            src, dst = o[p], o[(p - 1) % N]  # position p sends to p-1
+            assert (src, dst) not in arcs, "rings must be arc-disjoint"
+            arcs.add((src, dst))
+            if links is not None:
+                assert links[src][dst], f"ring uses the missing link {src}->{dst}"
+
+
+def test_ring_orders_follow_the_link_matrix():
+    """Topology-aware rings (the reference wires its ring from the physical links, sw/setup_route.sh:12-40): a
+    ring-wired node (each GPU linked to its two neighbours) gets exactly the physical ring; a full node with one
+    GPU pair unlinked still gets arc-disjoint rings that avoid that pair; no Hamiltonian cycle -> identity."""
+    N = 8
+    ring_links = [[int(b in ((a + 1) % N, (a - 1) % N)) for b in range(N)] for a in range(N)]
+    orders = A.ring_orders(N, 7, ring_links)
+    assert len(orders) == 2  # the physical ring, one per direction
+    _check_rings(orders, N, ring_links)
+    holes = [[int(a != b and {a, b} != {0, 1}) for b in range(N)] for a in range(N)]
+    orders = A.ring_orders(N, 7, holes)
+    assert len(orders) >= 5
+    _check_rings(orders, N, holes)
+    two_islands = [[int(a != b and a // 4 == b // 4) for b in range(N)] for a in range(N)]
+    assert A.ring_orders(N, 7, two_islands) == [list(range(N))]
+    full = [[int(a != b) for b in range(N)] for a in range(N)]
+    assert A.ring_orders(N, 7, full) == A.ring_orders(N, 7)
