@@ -145,10 +145,11 @@ uint8_t* AllReduceEngine::scratch(const std::string& key, size_t bytes) {
 }
 
 uint8_t* AllReduceEngine::epi_scratch(const std::string& base, size_t bytes) {
-  // one buffer per request slot; on a key's first use all kSlots are allocated at once, so the slot rotation
-  // never allocates later (inside a timed loop)
+  // one buffer per request slot; for ordinary buckets all kSlots are allocated on a key's first use, so the slot
+  // rotation never allocates later (inside a timed loop); buckets above 64 MB allocate per slot on first use
+  // (8 copies of a multi-GB gathered wire would be pure waste for a request stream that rarely defers them)
   const std::string key = base + "_s" + std::to_string(epi_slot_);
-  if (scratch_.find(key) == scratch_.end())
+  if (scratch_.find(key) == scratch_.end() && bytes <= (size_t(64) << 20))
     for (int s = 0; s < kSlots; ++s) scratch(base + "_s" + std::to_string(s), bytes);
   return scratch(key, bytes);
 }

@@ -229,10 +229,13 @@ class NativeAllReduce:
         (from :meth:`prepack_target`); the engine encodes the rest and skips its pack pass."""
         n_valid = int(n_valid if n_valid is not None else master.numel())
         pre, pre_n = (None, 0) if prepacked is None else prepacked
+        # an immediate request (no ordering after the producer's later work) is committed by the engine itself, so
+        # a chunked bucket runs its per-chunk epilogues inside the pipeline (bounded scratch)
+        eng_defer = defer or update_after is not None
         slot = self.C.submit(grad.view(-1), master.view(-1), None if lp is None else lp.view(-1),
                              None if mom is None else mom.view(-1), n_valid, lr, grad_scale, weight_decay, momentum,
-                             nesterov, True, True, None, pre, int(pre_n))
-        h = NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=True)
+                             nesterov, eng_defer, True, None, pre, int(pre_n))
+        h = NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=eng_defer)
         self._account(n_valid)
         return h if defer else h.commit(update_after)
 
