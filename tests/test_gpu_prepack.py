@@ -122,7 +122,7 @@ def _engine_case(N, prepack, force=False, n=20000, codec="bfp_rne"):
         w[:n] = torch.from_numpy(w0)
         kw = {}
         if prepack:
-            buf, shard, own, cid = eng.prepack_target(g, n)
+            buf, shard, own, cid = eng.prepack_target(g, n)[:4]
             full = torch.zeros(shard * eng.world, device="cuda")
             full[:n] = g[:n]
             _ext.require().wire_pack_range(full, buf, shard, 0, w_elems, cid)  # the "producer"
