@@ -32,7 +32,7 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
   inline_ = world == 1 && !cfg.force_comm;
   if (cfg_.chunk_elems <= 0) {
     const char* ce = std::getenv("FAN_CHUNK_ELEMS");
-    cfg_.chunk_elems = ce ? std::atoll(ce) : (int64_t(1) << 25);
+    cfg_.chunk_elems = ce ? std::atoll(ce) : (int64_t(1) << 26);
   }
   FAN_CHECK(cfg_.chunk_elems >= 256, "chunk_elems must be >= 256");
   FAN_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, cfg.stream_priority));

@@ -38,7 +38,8 @@ struct EngineConfig {
   bool force_comm = false;  // world 1 still runs the collectives (exercises the multi-rank path)
   int verify = -1;          // debug verify mode (message tags + sequence numbers); -1: from FAN_VERIFY
   // mesh: buckets above this many elements stream through the collectives in chunks (block pipeline, bounded
-  // scratch); 0: from FAN_CHUNK_ELEMS, default 32 Mi elements (128 MB of f32 gradient)
+  // scratch); 0: from FAN_CHUNK_ELEMS, default 64 Mi elements (256 MB of f32 gradient: at world 1 the chunked
+  // pipeline measured 29 % slower on a 256 MB request, profiles/r2_allreduce_bw_1gpu_chunked8M.jsonl)
   int64_t chunk_elems = 0;
   // ring: direct links (row-major world x world, links[a*world+b]: a can send to b); empty = fully connected
   std::vector<char> links;

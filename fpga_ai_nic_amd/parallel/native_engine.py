@@ -112,7 +112,7 @@ class NativeAllReduce:
         request sequence number, checked on arrival (csrc/comm/verify.h); ``fault``: test-only fault injection
         rules (FAN_FAULT grammar, default from the environment). ``chunk_elems`` (mesh, multi-rank): buckets above it
         stream through the collectives in chunks — all-to-all / owner reduce / all-gather / epilogue pipelined over
-        two streams with scratch bounded by two chunks (0: env FAN_CHUNK_ELEMS, default 32 Mi elements).
+        two streams with scratch bounded by two chunks (0: env FAN_CHUNK_ELEMS, default 64 Mi elements).
         ``links`` (ring): direct-link matrix the rings must follow (``"auto"``: this node's xGMI links from
         :func:`~fpga_ai_nic_amd.utils.topology.link_matrix`; None: fully connected)."""
         if algo not in _ALGOS:

@@ -296,7 +296,7 @@ def test_one_gib_allreduce_streams_through_bounded_scratch():
     16-value group is its BFP quantisation, checked against the oracle-verified pack/unpack kernels)."""
     from fpga_ai_nic_amd.ops import wire
 
-    eng = NativeAllReduce(_native_transport(), codec="bfp_rne", force_comm=True)
+    eng = NativeAllReduce(_native_transport(), codec="bfp_rne", force_comm=True, chunk_elems=1 << 25)
     n = 1 << 28
     L = eng.layout(n)
     assert L.chunks == 8
