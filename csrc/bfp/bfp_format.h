@@ -174,6 +174,13 @@ struct DenseLane<bf16_t> {
 };
 
 // ---------------------------------------------------------------- host launchers
+// Destination table of a kernel that stores its output straight into several buffers (the direct peer-to-peer
+// transport: one entry per rank, each an IPC-mapped slot of that peer's receive arena; nullptr entries skipped).
+constexpr int kMaxPeers = 16;
+struct WirePtrs {
+  uint8_t* p[kMaxPeers];
+};
+
 void launch_wire_pack(int codec, int in_dtype, const void* in, void* out, size_t n_s, int n_shards,
                       hipStream_t stream);
 void launch_wire_unpack(int codec, int out_dtype, const void* in, void* out, size_t n_s, int n_shards,
@@ -187,7 +194,21 @@ void launch_wire_reduce(int codec, int local_dtype, const void* slots, size_t sl
                         hipStream_t stream);
 // Fused all-gather epilogue: decode + SGD in place (master f32, optional bf16 copy, optional momentum).
 // Shards s with (s % skip_period) == skip_shard are left untouched (skip_shard < 0: none).
+// shard_stride: bytes between consecutive shards of `wire` (0: packed, wire_shard_bytes(codec, n_s)) — a gathered
+// wire read in place from a receive arena has its shards one arena slot pair apart.
 void launch_wire_sgd(int codec, const void* wire, size_t n_s, int n_shards, int skip_shard, int skip_period,
-                     float* master, bf16_t* lp, float* mom, SgdParams p, size_t n_valid, hipStream_t stream);
+                     float* master, bf16_t* lp, float* mom, SgdParams p, size_t n_valid, hipStream_t stream,
+                     size_t shard_stride = 0);
+// Decode to f32/bf16 from a strided wire (as launch_wire_sgd's shard_stride).
+void launch_wire_unpack_strided(int codec, int out_dtype, const void* in, size_t shard_stride, void* out, size_t n_s,
+                                int n_shards, hipStream_t stream);
+// Pack shards 0..n_shards-1 of `in`, shard s stored at dst.p[s] (skipped when nullptr); ends with a system-scope
+// release so a peer may read the stores once the (stream-ordered) ready flag is set.
+void launch_wire_pack_to(int codec, int in_dtype, const void* in, const WirePtrs& dst, size_t n_s, int n_shards,
+                         hipStream_t stream);
+// launch_wire_reduce whose encoded output is stored to every non-null dst.p[i] (i < n_dst), with a system-scope
+// release at the end (the owner's reduced shard goes straight into every peer's receive slot).
+void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots, int self_pos,
+                           const void* local, const WirePtrs& dst, int n_dst, size_t n_s, hipStream_t stream);
 
 }  // namespace fan

@@ -111,14 +111,74 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
+// Direct-transport variants: pack / reduce store their encoded output into a table of destinations (peers'
+// receive slots over xGMI), then release at system scope before the kernel retires.
+template <typename TIN, int C>
+__global__ void __launch_bounds__(kBlock) wire_pack_to_kernel(const TIN* __restrict__ in, WirePtrs dst, size_t n_s,
+                                                             int n_shards) {
+  const size_t tasks = n_s >> 3;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (int s = 0; s < n_shards; ++s) {
+    uint8_t* d = dst.p[s];
+    if (d == nullptr) continue;
+    const TIN* src = in + (size_t)s * n_s;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+      float v[8];
+      DenseLane<TIN>::load8(src, t << 3, v);
+      WireLane<C>::store8(d, n_s, t << 3, v);
+    }
+  }
+  __threadfence_system();
+}
+
+template <typename TL, int C>
+__global__ void __launch_bounds__(kBlock)
+    wire_reduce_to_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
+                          const TL* __restrict__ local, WirePtrs dst, int n_dst, size_t n_s) {
+  const size_t tasks = n_s >> 3;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+    const size_t le = t << 3;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.0f;
+    for (int r = 0; r < n_slots; ++r) {
+      float v[8];
+      if (r == self_pos) DenseLane<TL>::load8(local, le, v);
+      else WireLane<C>::load8(slots + (size_t)r * slot_stride, n_s, le, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    for (int i = 0; i < n_dst; ++i)
+      if (dst.p[i] != nullptr) WireLane<C>::store8(dst.p[i], n_s, le, acc);
+  }
+  __threadfence_system();
+}
+
+template <typename TOUT, int C>
+__global__ void __launch_bounds__(kBlock) wire_unpack_strided_kernel(const uint8_t* __restrict__ in,
+                                                                    size_t shard_stride, TOUT* __restrict__ out,
+                                                                    size_t n_s, int n_shards) {
+  const size_t tasks = n_s >> 3;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (int s = 0; s < n_shards; ++s) {
+    const uint8_t* src = in + (size_t)s * shard_stride;
+    TOUT* dst = out + (size_t)s * n_s;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+      float v[8];
+      WireLane<C>::load8(src, n_s, t << 3, v);
+      DenseLane<TOUT>::store8(dst, t << 3, v);
+    }
+  }
+}
+
 template <int C, bool HAS_LP, bool HAS_MOM>
 __global__ void __launch_bounds__(kBlock)
     wire_sgd_kernel(const uint8_t* __restrict__ wire, size_t n_s, int n_shards, int skip_shard, int skip_period,
                     float* __restrict__ master, bf16_t* __restrict__ lp, float* __restrict__ mom, SgdParams p,
-                    size_t n_valid) {
+                    size_t n_valid, size_t sb) {
   const size_t tasks = n_s >> 3;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  const size_t sb = wire_shard_bytes(C, n_s);
   for (int s = 0; s < n_shards; ++s) {
     if (skip_shard >= 0 && (s % skip_period) == skip_shard) continue;
     const uint8_t* src = wire + (size_t)s * sb;
@@ -260,25 +320,77 @@ void launch_wire_reduce(int codec, int local_dtype, const void* slots, size_t sl
 }
 
 void launch_wire_sgd(int codec, const void* wire, size_t n_s, int n_shards, int skip_shard, int skip_period,
-                     float* master, bf16_t* lp, float* mom, SgdParams p, size_t n_valid, hipStream_t stream) {
+                     float* master, bf16_t* lp, float* mom, SgdParams p, size_t n_valid, hipStream_t stream,
+                     size_t shard_stride) {
   if (skip_period < 1) skip_period = 1 << 30;
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
   const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
   const uint8_t* w = (const uint8_t*)wire;
   FAN_CODEC_SWITCH(codec, {
+    const size_t sb = shard_stride ? shard_stride : wire_shard_bytes(C, n_s);
     if (lp && mom)
       hipLaunchKernelGGL((wire_sgd_kernel<C, true, true>), grid, kBlock, 0, stream, w, n_s, n_shards, skip_shard, skip_period,
-                         master, lp, mom, p, n_valid);
+                         master, lp, mom, p, n_valid, sb);
     else if (lp)
       hipLaunchKernelGGL((wire_sgd_kernel<C, true, false>), grid, kBlock, 0, stream, w, n_s, n_shards,
-                         skip_shard, skip_period, master, lp, mom, p, n_valid);
+                         skip_shard, skip_period, master, lp, mom, p, n_valid, sb);
     else if (mom)
       hipLaunchKernelGGL((wire_sgd_kernel<C, false, true>), grid, kBlock, 0, stream, w, n_s, n_shards,
-                         skip_shard, skip_period, master, lp, mom, p, n_valid);
+                         skip_shard, skip_period, master, lp, mom, p, n_valid, sb);
     else
       hipLaunchKernelGGL((wire_sgd_kernel<C, false, false>), grid, kBlock, 0, stream, w, n_s, n_shards,
-                         skip_shard, skip_period, master, lp, mom, p, n_valid);
+                         skip_shard, skip_period, master, lp, mom, p, n_valid, sb);
+  });
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+void launch_wire_unpack_strided(int codec, int out_dtype, const void* in, size_t shard_stride, void* out, size_t n_s,
+                                int n_shards, hipStream_t stream) {
+  check_ns(n_s);
+  if (n_s == 0 || n_shards == 0) return;
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  FAN_CODEC_SWITCH(codec, {
+    if (out_dtype == kF32)
+      hipLaunchKernelGGL((wire_unpack_strided_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)in,
+                         shard_stride, (float*)out, n_s, n_shards);
+    else
+      hipLaunchKernelGGL((wire_unpack_strided_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const uint8_t*)in,
+                         shard_stride, (bf16_t*)out, n_s, n_shards);
+  });
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+void launch_wire_pack_to(int codec, int in_dtype, const void* in, const WirePtrs& dst, size_t n_s, int n_shards,
+                         hipStream_t stream) {
+  check_ns(n_s);
+  FAN_CHECK(n_shards <= kMaxPeers, "pack_to: at most 16 destinations");
+  if (n_s == 0 || n_shards == 0) return;
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  FAN_CODEC_SWITCH(codec, {
+    if (in_dtype == kF32)
+      hipLaunchKernelGGL((wire_pack_to_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in, dst, n_s,
+                         n_shards);
+    else
+      hipLaunchKernelGGL((wire_pack_to_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const bf16_t*)in, dst, n_s,
+                         n_shards);
+  });
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots, int self_pos,
+                           const void* local, const WirePtrs& dst, int n_dst, size_t n_s, hipStream_t stream) {
+  check_ns(n_s);
+  FAN_CHECK(n_dst <= kMaxPeers && local != nullptr, "reduce_to: local operand and at most 16 destinations");
+  if (n_s == 0) return;
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  FAN_CODEC_SWITCH(codec, {
+    if (local_dtype == kF32)
+      hipLaunchKernelGGL((wire_reduce_to_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,
+                         slot_stride, n_slots, self_pos, (const float*)local, dst, n_dst, n_s);
+    else
+      hipLaunchKernelGGL((wire_reduce_to_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,
+                         slot_stride, n_slots, self_pos, (const bf16_t*)local, dst, n_dst, n_s);
   });
   FAN_HIP_CHECK(hipGetLastError());
 }

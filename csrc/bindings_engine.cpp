@@ -268,6 +268,7 @@ void register_engine(pybind11::module_& m) {
              d["timed_requests"] = c.timed_requests;
              d["forced_commits"] = c.forced_commits;
              d["verified_rows"] = c.verified_rows;
+             d["direct_rounds"] = c.direct_rounds;
              return d;
            },
            "perf counters (the NIC's latency / host-stall registers): requests, bytes, host wait, device time")

@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cstdlib>
 
+#include "comm/p2p_comm.h"
 #include "common/roctx.h"
 #include <functional>
 #include <sstream>
@@ -197,6 +198,8 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
   }
   if (L.chunks > 1)
     return run_mesh_chunked(L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked, cur_defer_);
+  if (P2PComm* d = comm_->direct(); d && N <= kMaxPeers && !verify_ && !fault_.active())
+    return run_mesh_direct(d, L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked, cur_defer_);
   uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
   const uint8_t* P = prepacked ? prepacked : g;
   const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
@@ -237,6 +240,82 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
   }
   const int64_t n_pad = L.n_pad;
   return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
+}
+
+// Mesh over the direct P2P transport: the encoder is the sender (the NIC streams its sums
+// from send_fifo through the BFP TX framing onto the link, hw/all_reduce.sv:1155-1166, hw/bfp_adapter.sv:279-379).
+//   round 1: the pack kernel stores shard p straight into peer p's receive slot (a prepacked bucket is copied
+//            there); ready flags; the owner reduce reads the N-1 received shards IN PLACE from this rank's arena
+//            (plus its own f32 shard) and stores the re-encoded owner shard straight into every peer's round-2
+//            slot and its own; the round-1 slots are acknowledged;
+//   round 2: ready flags; an immediate request decodes + applies SGD reading the gathered shards in place, then
+//            acknowledges; a deferred one (epilogue at commit, after the producer's remaining GEMMs) first moves
+//            them into per-slot scratch, since the slots are reused two rounds later.
+// No staging buffer and no copy kernel on either side of a link (verify mode / fault injection use the copying
+// path). Memory ordering: p2p_comm.h.
+std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineLayout& L, const void* grad, int gdt,
+                                                       float* master, bf16_t* lp, float* mom, int64_t n_valid,
+                                                       SgdParams p, bool update, float* out_sum,
+                                                       const uint8_t* prepacked, bool defer) {
+  const int N = world_, r = rank_, c = cfg_.codec;
+  const int64_t s = L.shard;
+  const size_t sb = wire_shard_bytes(c, s);
+  FAN_CHECK(sb <= d->slot_bytes(), "p2p: shard larger than the arena slot (raise slot_bytes)");
+  const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
+  hipStream_t st = run_stream_;
+  const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
+  P2PComm::Round r1 = d->begin(st);
+  {
+    RoctxRange rr("fan/mesh/direct_send");
+    WirePtrs to{};
+    std::vector<P2PCopy> segs;
+    for (int q = 0; q < N; ++q) {
+      if (q == r) continue;
+      to.p[q] = d->dst(r1, q);
+      if (prepacked) segs.push_back({prepacked + (size_t)q * sb, to.p[q], sb});
+      else if (zero_copy) segs.push_back({g + (size_t)q * s * esize(gdt), to.p[q], sb});
+    }
+    if (prepacked || zero_copy) launch_multi_copy(segs, st);
+    else launch_wire_pack_to(c, gdt, g, to, (size_t)s, N, st);
+  }
+  mark(kTpPacked);
+  d->publish(r1, st);
+  d->wait(r1, st);
+  mark(kTpExchanged);
+  P2PComm::Round r2 = d->begin(st);
+  {
+    RoctxRange rr("fan/mesh/direct_reduce");
+    WirePtrs out{};
+    for (int q = 0; q < N; ++q) out.p[q] = d->dst(r2, q);  // q == r: this rank's own copy (its own slot)
+    launch_wire_reduce_to(c, gdt, d->src_base(r1), d->src_stride(), N, r, g + (size_t)r * s * esize(gdt), out, N,
+                          (size_t)s, st);
+    d->release(r1, st);
+  }
+  mark(kTpReduced);
+  d->publish(r2, st);
+  d->wait(r2, st);
+  counters_.direct_rounds += 2;
+  const uint8_t* Gv = d->src_base(r2);
+  const size_t gstride = d->src_stride();
+  const int64_t n_pad = L.n_pad;
+  if (defer) {
+    uint8_t* G = epi_scratch("mesh_G" + std::to_string(sb * N), sb * N);
+    std::vector<P2PCopy> segs;
+    for (int q = 0; q < N; ++q) segs.push_back({Gv + (size_t)q * gstride, G + (size_t)q * sb, sb});
+    launch_multi_copy(segs, st);
+    d->release(r2, st);
+    return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
+  }
+  mark(kTpCommEnd);
+  {
+    RoctxRange rr("fan/mesh/direct_epilogue");
+    const int64_t nv = std::max<int64_t>(0, std::min<int64_t>(n_valid, n_pad));
+    if (update && nv > 0)
+      launch_wire_sgd(c, Gv, (size_t)s, N, -1, 0, master, lp, mom, p, (size_t)nv, st, gstride);
+    if (out_sum) launch_wire_unpack_strided(c, kF32, Gv, gstride, out_sum, (size_t)s, N, st);
+  }
+  d->release(r2, st);
+  return {};
 }
 
 // Chunked mesh (buckets above chunk_elems): the reference's block pipeline (hw/all_reduce.sv:330, 423-464,

@@ -69,6 +69,7 @@ struct EngineCounters {
   uint64_t timed_requests = 0;
   uint64_t forced_commits = 0;  // deferred epilogues committed because their slot was needed (> kSlots deferred)
   uint64_t verified_rows = 0;   // verify mode: message rows whose tags were checked on arrival
+  uint64_t direct_rounds = 0;   // direct P2P rounds (kernels stored into / read from peer receive slots in place)
 };
 
 // Device-side request trace: GPU timestamps (timing events) at the phase boundaries of each request, the MI355X
@@ -188,6 +189,9 @@ class AllReduceEngine {
   std::vector<EpiThunk> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                               float* out_sum, const uint8_t* prepacked, int64_t prepacked_elems);
+  std::vector<EpiThunk> run_mesh_direct(P2PComm* d, const EngineLayout& L, const void* grad, int gdt, float* master,
+                                        bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
+                                        float* out_sum, const uint8_t* prepacked, bool defer);
   std::vector<EpiThunk> run_mesh_chunked(const EngineLayout& L, const void* grad, int gdt, float* master,
                                          bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
                                          float* out_sum, const uint8_t* prepacked, bool defer);

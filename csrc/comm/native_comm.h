@@ -32,6 +32,8 @@ struct P2POp {
 // What the all-reduce engine needs from a communicator. Implemented by NativeComm (RCCL over xGMI) and by
 // LoopbackComm (virtual ranks on one GPU, csrc/comm/loopback_comm.h) so the engine's multi-rank schedules are
 // testable on a single device.
+class P2PComm;
+
 class Comm {
  public:
   virtual ~Comm() = default;
@@ -45,6 +47,8 @@ class Comm {
   // Returns an empty string when healthy, else the async error text.
   virtual std::string async_error() = 0;
   virtual void abort() = 0;
+  // Transports whose receive buffers the engine's kernels may write and read in place (direct peer stores):
+  virtual P2PComm* direct() { return nullptr; }
 };
 
 class NativeComm : public Comm {

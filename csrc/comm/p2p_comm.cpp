@@ -167,6 +167,38 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
   for (int src : srcs) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[src] + world_ + rank_, q, 0));
 }
 
+P2PComm::Round P2PComm::begin(hipStream_t s) {
+  FAN_CHECK(!aborted_, "p2p transport aborted");
+  Round r{++seq_};
+  const int par = (int)(r.seq & 1);
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
+    const uint64_t prev = last_sent_[par][p];
+    if (prev) FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + world_ + p, prev, hipStreamWaitValueGte));
+  }
+  return r;
+}
+
+void P2PComm::publish(const Round& r, hipStream_t s) {
+  const int par = (int)(r.seq & 1);
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, r.seq, 0));  // "ready from rank_" at p
+    last_sent_[par][p] = r.seq;
+  }
+}
+
+void P2PComm::wait(const Round& r, hipStream_t s) {
+  for (int p = 0; p < world_; ++p)
+    if (p != rank_) FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + p, r.seq, hipStreamWaitValueGte));
+}
+
+void P2PComm::release(const Round& r, hipStream_t s) {
+  for (int p = 0; p < world_; ++p)
+    if (p != rank_) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + world_ + rank_, r.seq, 0));
+}
+
 void P2PComm::copy(const std::vector<P2PCopy>& segs, hipStream_t s) {
   bool aligned = true;
   for (const P2PCopy& c : segs)

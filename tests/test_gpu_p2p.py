@@ -78,6 +78,31 @@ def _worker(rank, world, port, q):
             ref = sim.mesh_allreduce(gin, L.shard) if algo == "mesh" else \
                 sim.ring_allreduce(gin, eng.orders, L.slice_elems, L.blocks)[0]
             ok[f"engine_{algo}"] = bool(np.array_equal(out.cpu().numpy()[:m], ref[:m]))
+            if algo != "mesh":
+                continue
+            # the mesh ran the DIRECT path (pack / reduce kernels stored into the peer's slots, reduce and epilogue
+            # read this rank's slots in place); fused SGD immediate and deferred, and the copying path (verify
+            # mode) bit-identical to it
+            from fpga_ai_nic_amd.ops import bfp_oracle as O
+
+            ok["direct_rounds"] = eng.counters()["direct_rounds"] >= 2
+            w0 = rng.standard_normal(m).astype(np.float32)
+            ref_w, _ = O.sgd(w0, ref[:m], 0.5)
+            for defer in (False, True):
+                w = torch.zeros(L.n_pad, device="cuda")
+                w[:m] = torch.from_numpy(w0).cuda()
+                h = eng.allreduce_sgd(g, w, n_valid=m, lr=0.5, defer=defer)
+                h.commit_after_current()
+                h.synchronize(30)
+                torch.cuda.synchronize()
+                got = w.cpu().numpy()[:m]
+                ulp = np.abs(got.view(np.int32).astype(np.int64) - ref_w.view(np.int32).astype(np.int64)).max()
+                ok[f"direct_sgd_defer{int(defer)}"] = bool(ulp <= 1)
+            ev = NativeAllReduce(None, codec="bfp_rne", algo="mesh", comm=comm, verify=True)
+            out2 = torch.zeros(L.n_pad, device="cuda")
+            ev.allreduce(g, out2, n_valid=m).synchronize(30)
+            torch.cuda.synchronize()
+            ok["copy_path_equals_direct"] = bool(torch.equal(out2, out)) and ev.counters()["direct_rounds"] == 0
         q.put((rank, ok, comm.sequence))
     except Exception as e:  # noqa: BLE001
         q.put((rank, {"error": repr(e)}, -1))
