@@ -47,6 +47,13 @@ void register_engine(pybind11::module_& m) {
       .def_property_readonly("slot_bytes", &P2PComm::slot_bytes)
       .def_property_readonly("sequence", &P2PComm::sequence)
       .def_property_readonly("uncached", &P2PComm::uncached)
+      .def_property_readonly("arena_memory", &P2PComm::arena_memory)
+      .def("arena_view",
+           [](P2PComm& c) {
+             return at::from_blob(c.arena(), {(int64_t)c.arena_bytes()},
+                                  at::TensorOptions().dtype(at::kByte).device(at::kCUDA, at::cuda::current_device()));
+           },
+           "diagnostics: this rank's receive arena as a uint8 tensor (no copy)")
       .def("all_to_all",
            [](P2PComm& c, const at::Tensor& send, at::Tensor& recv) {
              TORCH_CHECK(bytes_of(send) == bytes_of(recv) && bytes_of(send) % c.world() == 0, "all_to_all sizes");

@@ -1,6 +1,7 @@
 // Direct peer-to-peer transport. See p2p_comm.h.
 #include "comm/p2p_comm.h"
 
+#include <cstdlib>
 #include <cstring>
 
 namespace fan {
@@ -23,12 +24,21 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
   // line of them may sit in this GPU's (per-XCD, non-coherent) L2 when the reader consumes a new message.
   // Fallback to coarse-grained memory only if the allocator refuses the flag (the ordering then rests on the
   // kernel-boundary L2 invalidate of the reading kernel, which reads each arena byte once per message).
-  uncached_ = hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * 2 * slot_,
-                                    hipDeviceMallocUncached) == hipSuccess;
+  // FAN_P2P_MEM=uncached (default) | fine | coarse: memory type of the arena (A/B; the flags stay uncached)
+  const char* me = std::getenv("FAN_P2P_MEM");
+  const std::string mem = me ? me : "uncached";
+  unsigned aflag = mem == "fine" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
+  uncached_ = mem != "coarse" && mem != "fine" &&
+              hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * 2 * slot_, aflag) == hipSuccess;
   if (!uncached_) {
     (void)hipGetLastError();
-    FAN_HIP_CHECK(hipMalloc(&arena_, (size_t)world * 2 * slot_));
+    if (mem == "fine") {
+      FAN_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * 2 * slot_, aflag));
+    } else {
+      FAN_HIP_CHECK(hipMalloc(&arena_, (size_t)world * 2 * slot_));
+    }
   }
+  arena_mem_ = uncached_ ? "uncached" : mem == "fine" ? "fine" : "coarse";
   // flags are polled by the command processor (hipStreamWaitValue64) and written by peers' command
   // processors (hipStreamWriteValue64); device memory supports both and HIP IPC export (probed on
   // MI355X: tools/probes/stream_wait_probe.cpp)

@@ -89,6 +89,9 @@ class P2PComm : public Comm {
   void abort() override;
   uint64_t sequence() const { return seq_; }
   bool uncached() const { return uncached_; }
+  const std::string& arena_memory() const { return arena_mem_; }
+  uint8_t* arena() const { return arena_; }
+  size_t arena_bytes() const { return (size_t)world_ * 2 * slot_; }
 
  private:
   void copy(const std::vector<P2PCopy>& segs, hipStream_t s);
@@ -104,6 +107,7 @@ class P2PComm : public Comm {
   uint64_t seq_ = 0;
   bool aborted_ = false;
   bool uncached_ = false;
+  std::string arena_mem_;
 };
 
 }  // namespace fan
