@@ -16,7 +16,7 @@ _enabled = os.environ.get("FAN_ROCTX", "0") == "1"
 def _roctx():
     global _lib, _enabled
     if _lib is None and _enabled:
-        for name in ("libroctx64.so.4", "libroctx64.so"):
+        for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4", "libroctx64.so"):
             try:
                 _lib = ctypes.CDLL(name)
                 _lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
