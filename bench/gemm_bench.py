@@ -90,7 +90,8 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
     ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
     ap.add_argument("--set", default="mlp", choices=["mlp", "bert", "ref", "ragged"])
-    ap.add_argument("--ab", action="store_true", help="also time the one-role main loop (ping-pong off)")
+    ap.add_argument("--loops", default="",
+                    help="also time these 256x256 main loops (0 one-role, 1 staggered, 2 pipelined), e.g. 0,2")
     ap.add_argument("--epi-arms", action="store_true",
                     help="bwd-weight shapes: also time the fused bias-gradient (colsum) and BFP wire epilogues")
     a = ap.parse_args()
@@ -152,8 +153,11 @@ def main():
                               "auto_plan": G._ext.require().gemm_plan(M, N, K)}), flush=True)
         mine(); ref(); torch.cuda.synchronize()
         err = (C.float() - (ref().float() * ((aux > 0) if epi == G.EPI_RELU_MASK else 1))).abs().max().item()
-        tm, tr, tmm, tone = [], [], [], []
+        tm, tr, tmm = [], [], []
         Cx = G._ext.require()
+        loops = [int(x) for x in a.loops.split(",") if x]
+        tloop = {m: [] for m in loops}
+        mode0 = Cx.gemm_main_loop()
         arms = {}
         if a.epi_arms and a_t and not b_t and dt == torch.bfloat16:
             from fpga_ai_nic_amd.ops import wire as W
@@ -169,10 +173,10 @@ def main():
         for _ in range(a.rounds):
             for k, fn in arms.items():
                 tarm[k].append(time_fn(fn, a.iters))
-            if a.ab:  # same plan with the one-role main loop (256x256 tiles only differ)
-                Cx.gemm_set_pingpong(False)
-                tone.append(time_fn(mine, a.iters))
-                Cx.gemm_set_pingpong(True)
+            for mode in loops:  # same plan, other main loop (256x256 tiles only differ)
+                Cx.gemm_set_main_loop(mode)
+                tloop[mode].append(time_fn(mine, a.iters))
+                Cx.gemm_set_main_loop(mode0)
             tm.append(time_fn(mine, a.iters))
             tr.append(time_fn(ref, a.iters))
             tmm.append(time_fn(ref_mm_only, a.iters))
@@ -185,7 +189,8 @@ def main():
                           "torch_fused_us": round(r, 2), "torch_matmul_only_us": round(rm, 2),
                           "torch_matmul_tflops": round(flop / rm / 1e6, 1), "speedup_vs_torch_fused": round(r / m, 3),
                           "max_abs_err": err,
-                          **({"oneloop_us": round(statistics.median(tone), 2)} if tone else {}),
+                          **({"loop_us": {str(k): round(statistics.median(v), 2) for k, v in tloop.items()}}
+                             if loops else {}),
                           **({"epi_arms_us": {k: round(statistics.median(v), 2) for k, v in tarm.items()}}
                              if arms else {})}), flush=True)
 

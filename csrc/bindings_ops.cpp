@@ -87,11 +87,14 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
   if (A.scalar_type() == at::kBFloat16) {
     TORCH_CHECK(bias ? bias->scalar_type() == at::kBFloat16 : true, "bias must be bf16");
     const GemmPlan p = gemm_bf16_plan(g.M, g.N, g.K, g.split_k, g.tile_bm, g.tile_bn, g.tile_waves);
-    if (p.split_k > 1) {
-      const int64_t need = (int64_t)p.split_k * ((int64_t)g.M * g.N + (g.colsum ? g.N : 0));
+    // split-K slabs, then bias-gradient partials (at most split_k per tile row)
+    const int64_t need = (p.split_k > 1 ? (int64_t)p.split_k * g.M * g.N : 0) +
+                         (g.colsum && p.bm > 0 ? (int64_t)p.split_k * ((g.M + p.bm - 1) / p.bm) * g.N : 0);
+    if (need > 0 || p.split_k > 1) {
       TORCH_CHECK(workspace && workspace->scalar_type() == at::kFloat && workspace->is_contiguous() &&
                       workspace->numel() >= need,
-                  "gemm: split-K ", p.split_k, " needs an f32 workspace of ", need, " elements");
+                  "gemm: split-K ", p.split_k, (g.colsum ? " with colsum" : ""), " needs an f32 workspace of ", need,
+                  " elements");
     }
     TORCH_CHECK(gemm_bf16_supported(g), "gemm_bf16: unsupported shape M=", g.M, " N=", g.N, " K=", g.K,
                 " split_k=", g.split_k);
@@ -163,8 +166,11 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_supported", &gemm_supported);
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);
-  m.def("gemm_set_pingpong", [](bool on) { gemm_pingpong_flag().store(on); },
-        "256x256 GEMM tiles: ping-pong main loop (default) or the one-role loop");
+  m.def("gemm_set_pingpong", [](bool on) { gemm_main_loop_flag().store(on ? 1 : 0); },
+        "256x256 GEMM tiles: staggered 4-phase main loop (true) or the one-role loop (false)");
+  m.def("gemm_set_main_loop", [](int mode) { gemm_main_loop_flag().store(mode); },
+        "256x256 GEMM tiles: 0 one-role loop, 1 staggered 4-phase loop, 2 software-pipelined loop (K-contiguous A)");
+  m.def("gemm_main_loop", []() { return gemm_main_loop_flag().load(); });
   m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {
           gemm_set_stamp_buffer(t ? t->data_ptr() : nullptr);
         },

@@ -64,7 +64,7 @@ bool gemm_bf16_supported(const GemmArgs& a);
 void launch_gemm_bf16(const GemmArgs& a, hipStream_t stream);
 
 // 256x256 tiles: staggered 4-phase main loop (true; env FAN_GEMM_PP=1 starts with true) or the one-role loop.
-std::atomic<bool>& gemm_pingpong_flag();
+std::atomic<int>& gemm_main_loop_flag();
 // diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
 void gemm_set_stamp_buffer(void* p);
 void* gemm_stamp_buffer();

@@ -26,6 +26,9 @@
 //     (global_load_lds has no predicate, so the lane reads zeros instead), so the MFMAs accumulate exact zeros
 //     there, and its epilogue stores only in-range elements. Interior tiles run the unpredicated path.
 #pragma once
+#include <cstdlib>
+#include <type_traits>
+
 #include "bfp/bfp_format.h"
 #include "gemm/gemm.h"
 #include "gemm/glds.h"
@@ -45,8 +48,9 @@ constexpr int kDefaultWaves = 8;
 
 #ifdef FAN_GEMM_STAMPS
 // Diagnostic build only (FAN_EXTRA_CFLAGS=-DFAN_GEMM_STAMPS): s_memtime stamps of the one-role loop for the first
-// kStampWG workgroups, [wg][wave][kt][point] with points 0 loop top, 1 after vmcnt, 2 after barrier, 3 after the
-// DMA issue, 4 after the fragment reads are issued. Never in a production build.
+// kStampWG workgroups, [wg][wave][kt][point]. One-role loop: 0 loop top, 1 after vmcnt, 2 after barrier, 3 after the
+// DMA issue, 4 after the fragment reads are issued. Pipelined loop: 0 K-tile top, 1 k-step-0 block issued, 2 after
+// the vmcnt/lgkmcnt wait, 3 after the barrier, 4 k-step-1 block issued. Never in a production build.
 constexpr int kStampWG = 8, kStampKT = 64, kStampPts = 5;
 #define FAN_STAMP(pt)                                                                                        \
   if (wo.stamps && blockIdx.x < kStampWG && kt < kStampKT && lane == 0)                                       \
@@ -732,6 +736,213 @@ __global__ void __launch_bounds__(512, 2)
                                                  ldaux, M, N, ksplit, ws, wo);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Software-pipelined 256x256 kernel (8 waves, 2x4, 128x64 per wave) for the K-contiguous-A layouts.
+//
+// The one-role loop runs each K-tile as barrier -> DMA burst -> fragment reads -> MFMAs, with every wave in the same
+// phase (one workgroup-wide barrier), so the MFMA pipes idle through the first three (r1 stamps: DMA issue ~1000,
+// reads 500-800, MFMAs ~1300 of ~4000 cycles). Here every load hides under MFMAs:
+//   * k-step 0 of K-tile t: 32 MFMAs on registers read earlier; under them the fragments of k-step (t, 1) are read
+//     (A fragments rolling: A_i of the next k-step is read right after row i's MFMAs; B fragments double-buffered);
+//   * then this wave's DMA of K-tile t+1 and its reads of (t, 1) retire (vmcnt(0), lgkmcnt(0)) and ONE barrier;
+//   * k-step 1: 32 MFMAs; under them the fragments of (t+1, 0) are read from the other stage (complete for every
+//     wave after the barrier) and the DMA of K-tile t+2 goes into stage t & 1 (nobody reads it any more: every wave
+//     retired its reads of it before the barrier), one piece per 4 MFMAs.
+// The DMA of a K-tile thus has two k-steps of MFMAs to land. LDS: 2 stages x 64 KiB. Glds with SGPR bases + 32-bit
+// lane offsets computed once. Aligned shapes only (M, N % 256, K % (64 * split_k)); every layout and epilogue.
+__device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_addr)
+      : "memory");
+}
+
+// Byte offset (from the operand's K-tile origin) of this lane's chunk of glds instruction i: stage_one's address
+// math without the base pointer.
+template <bool KCONTIG, int OUTER, int NT>
+__device__ __forceinline__ uint32_t piece_off(int64_t ld, int o0, int wave, int lane, int i) {
+  using T = OpTile<OUTER, NT>;
+  const int t = wave * 64 + lane;
+  if (KCONTIG) {
+    const int row = i * (T::IB / 128) + (t >> 3);
+    const int c = (t & 7) ^ ((row >> 1) & 7);
+    return (uint32_t)(((int64_t)(o0 + row) * ld + c * 8) * 2);
+  } else {
+    const int half = i / T::PER_HALF;
+    const int krow = (i % T::PER_HALF) * (T::IB / 256) + (t >> 4);
+    const int cs = t & 15;
+    const int blk = (cs >> 1) ^ mn_swz(krow);
+    return (uint32_t)(((int64_t)krow * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8) * 2);
+  }
+}
+
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false>
+__global__ void __launch_bounds__(512, 2)
+    gemm_pl_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
+                   TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
+                   int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
+                   float* __restrict__ colsum, WireOut wo) {
+  constexpr int BM = 256, BN = 256, NT = 512;
+  constexpr int A_BYTES = OpTile<BM, NT>::BYTES;
+  constexpr int STAGE = A_BYTES + OpTile<BN, NT>::BYTES;
+  constexpr int GA = OpTile<BM, NT>::GLDS, G = GA + OpTile<BN, NT>::GLDS;  // 4 + 4 pieces per wave and K-tile
+  constexpr int WTM = 128, WTN = 64, MI = 8, NJ = 4;
+  static_assert(G == 8, "8 glds pieces per wave and K-tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, tiles * split_k);
+  const int tile = wg % tiles, ksplit = wg / tiles;
+  const int GM = tiles_m >= 4 ? 4 : tiles_m;
+  const int grp = tile / (GM * tiles_n);
+  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
+  const int in_grp = tile % (GM * tiles_n);
+  const int m0 = (grp * GM + in_grp % gm) * BM;
+  const int n0 = (in_grp / gm) * BN;
+  const int k_per = K / split_k;
+  const int kbeg = ksplit * k_per;
+  const int nk = k_per / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / 4, wn = wave % 4;
+  // fused bias gradient (COLSUM: MN-contiguous B), waves wm == 0 sum the B fragments they use. Without split-K the
+  // work is spread over the tile rows so no tile runs long (one round of tiles: the slowest sets the time): tile row
+  // im sums K-tiles [cs0, cs1) into partial slab im of ws[]; with split-K (one partial per split, tile row 0) the
+  // partials ride along with the slab reduce. An ordered reduce over the partials follows (launch_typed).
+  const int im = SPLIT ? 0 : m0 / BM;
+  const int cs0 = SPLIT ? (m0 == 0 ? 0 : nk) : im * nk / tiles_m;
+  const int cs1 = SPLIT ? nk : (im + 1) * nk / tiles_m;
+  const bool do_colsum = COLSUM && wm == 0;
+  float cs[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 fa[MI], fb[2][NJ];
+
+  uint32_t off[G];
+#pragma unroll
+  for (int p = 0; p < GA; ++p) off[p] = piece_off<AK, BM, NT>(lda, m0, wave, lane, p);
+#pragma unroll
+  for (int p = GA; p < G; ++p) off[p] = piece_off<BKC, BN, NT>(ldb, n0, wave, lane, p - GA);
+  const int64_t a_step = AK ? (int64_t)BK * 2 : (int64_t)BK * lda * 2;
+  const int64_t b_step = BKC ? (int64_t)BK * 2 : (int64_t)BK * ldb * 2;
+  const char* a_k0 = reinterpret_cast<const char*>(A) + (AK ? (int64_t)kbeg * 2 : (int64_t)kbeg * lda * 2);
+  const char* b_k0 = reinterpret_cast<const char*>(B) + (BKC ? (int64_t)kbeg * 2 : (int64_t)kbeg * ldb * 2);
+  const uint32_t lds0 = lds_addr_of(smem);
+
+  auto piece = [&](int kt, int p) {  // glds piece p (0..7) of K-tile kt into stage kt & 1
+    const uint32_t st = lds0 + (kt & 1) * STAGE + wave * 1024;
+    if (p < GA) glds16_s(a_k0 + kt * a_step, off[p], st + p * OpTile<BM, NT>::IB);
+    else glds16_s(b_k0 + kt * b_step, off[p], st + A_BYTES + (p - GA) * OpTile<BN, NT>::IB);
+  };
+  auto read_a = [&](const char* st, int ks, int i) { fa[i] = read_frag<AK>(st, wm * WTM + i * 16, ks, lane); };
+  auto read_b = [&](const char* st, int ks, int set, int j) {
+    fb[set][j] = read_frag<BKC>(st + A_BYTES, wn * WTN + j * 16, ks, lane);
+  };
+  // One k-step: 32 MFMAs (rows i of 4) on B set `cur`. READ: the next k-step's fragments (stage rd_st, k-step rd_ks)
+  // are read under them — B_j into the other set during rows 0-1, A_i right after row i. DMA: one glds piece of
+  // K-tile dma_kt per 4 MFMAs. Compile-time flags: no branches inside the MFMA stream.
+  auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int rd_ks, int dma_kt, bool csk) {
+    constexpr int cur = decltype(cur_c)::value;
+    constexpr bool READ = decltype(read_c)::value, DMA = decltype(dma_c)::value;
+    if (COLSUM && csk) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) cs[j] += frag_sum(fb[cur][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (READ && i < 2 && (j & 1) == 0) read_b(rd_st, rd_ks, cur ^ 1, i * 2 + (j >> 1));
+        if (DMA && j == 2) piece(dma_kt, i);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                            __builtin_bit_cast(bf16x8, fb[cur][j]), acc[i][j], 0, 0, 0);
+      }
+      if (READ) read_a(rd_st, rd_ks, i);
+    }
+    // keep the source order: the scheduler otherwise clusters the LDS reads at the end of the MFMA stream, where
+    // the barrier's lgkmcnt(0) then waits on all of them
+    if constexpr (READ) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        if (i < 2) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  // prologue: K-tiles 0 and 1 in flight; retire 0 (this wave), barrier (every wave), read k-step (0, 0)
+#pragma unroll
+  for (int p = 0; p < G; ++p) piece(0, p);
+  if (nk > 1) {
+#pragma unroll
+    for (int p = 0; p < G; ++p) piece(1, p);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) read_b(smem, 0, 0, j);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) read_a(smem, 0, i);
+
+  auto ktile = [&](int kt, auto more_c, auto more2_c) {
+    const char* st = smem + (kt & 1) * STAGE;
+    const bool csk = do_colsum && kt >= cs0 && kt < cs1;
+    FAN_STAMP(0);
+    __builtin_amdgcn_s_setprio(1);
+    block(I0{}, T_{}, F_{}, st, 1, 0, csk);
+    __builtin_amdgcn_s_setprio(0);
+    FAN_STAMP(1);
+    // this wave's DMA of K-tile kt+1 and its reads of (kt, 1) retired; after the barrier, every wave's
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    FAN_STAMP(2);
+    __builtin_amdgcn_s_barrier();
+    FAN_STAMP(3);
+    __builtin_amdgcn_s_setprio(1);
+    block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk);
+    __builtin_amdgcn_s_setprio(0);
+    FAN_STAMP(4);
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) ktile(kt, T_{}, T_{});
+  if (kt + 1 < nk) ktile(kt++, T_{}, F_{});
+  if (kt < nk) ktile(kt, F_{}, F_{});
+
+  if (COLSUM && do_colsum && (!SPLIT || m0 == 0))
+    colsum_finish<NJ, WTN, kEpiNone, true>(
+        cs, lane, n0 + wn * WTN, ws + (SPLIT ? (int64_t)split_k * M * N + (int64_t)ksplit * N : (int64_t)im * N), wo,
+        N);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every operand read retired before the epilogue reuses the LDS
+  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
+                                                 aux, ldaux, M, N, ksplit, ws, wo);
+}
+
 // Ordered split-K reduction + epilogue (deterministic: slabs summed in split order).
 template <int EPI, typename TC, bool ACCUM>
 __global__ void __launch_bounds__(256)
@@ -751,20 +962,10 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Ordered reduction of the per-split bias-gradient partial sums (written after the slabs: ws[split_k*M*N + k*N]).
-template <int kUnused = 0>  // template: the header is included by several translation units
-__global__ void __launch_bounds__(256)
-    splitk_colsum_kernel(const float* __restrict__ part, int split_k, float* __restrict__ colsum, int N) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = part[n];
-  for (int k = 1; k < split_k; ++k) s += part[(int64_t)k * N + n];
-  colsum[n] = s;
-}
-
 // Split-K reduction for the wire epilogue: one thread per 16-column group sums the slabs in split order and
 // encodes the group into the all-reduce wire (owner shard also in f32). With colsum, the threads past the
-// M*N/16 groups reduce the bias partial sums, write colsum[] and encode the bias segment of the [W | b] bucket.
+// M*N/16 groups reduce the split_k bias partial sums (ws[split_k * M * N + k * N]), write colsum[] and encode the
+// bias segment of the [W | b] bucket.
 template <int kUnused = 0>
 __global__ void __launch_bounds__(256)
     splitk_reduce_wire_kernel(const float* __restrict__ ws, int split_k, float* __restrict__ C, int64_t ldc, int M,
@@ -774,21 +975,12 @@ __global__ void __launch_bounds__(256)
   const int64_t total = groups + (colsum ? gpr : 0);
   const int64_t slab = (int64_t)M * N;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const bool bias = g >= groups;
+    const int row = bias ? -1 : (int)(g / gpr);
+    const int col = (int)((bias ? g - groups : g % gpr) * 16);
+    const float* p = bias ? ws + (int64_t)split_k * slab + col : ws + (int64_t)row * N + col;
+    const int64_t stride = bias ? N : slab;
     float v[16];
-    const float* p;
-    int64_t stride;
-    int row, col;
-    if (g < groups) {
-      row = (int)(g / gpr);
-      col = (int)(g % gpr) * 16;
-      p = ws + (int64_t)row * N + col;
-      stride = slab;
-    } else {
-      row = -1;
-      col = (int)(g - groups) * 16;
-      p = ws + (int64_t)split_k * slab + col;
-      stride = N;
-    }
 #pragma unroll
     for (int u = 0; u < 16; u += 4) {
       const float4 q = *reinterpret_cast<const float4*>(p + u);
@@ -801,12 +993,52 @@ __global__ void __launch_bounds__(256)
         v[u] += q.x; v[u + 1] += q.y; v[u + 2] += q.z; v[u + 3] += q.w;
       }
     }
-    if (row >= 0) {
+    if (!bias) {
       wire_epi16(v, C, ldc, wo, row, col);
     } else {
 #pragma unroll
       for (int u = 0; u < 16; ++u) colsum[col + u] = v[u];
       if (wo.bias_off > 0) wire_store16(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
+    }
+  }
+}
+
+// Ordered reduce of bias-gradient partial slabs part[p * N + n], p < parts, into colsum[n]; WIRE: also encodes the
+// bias segment of the [W | b] bucket (flat wo.bias_off + n). One block per 64 columns: 16 lanes x float4 columns by
+// 16 part classes (p % 16), each summed in p order, then the classes summed in class order (deterministic).
+template <bool WIRE>
+__global__ void __launch_bounds__(256)
+    colsum_reduce_kernel(const float* __restrict__ part, int parts, float* __restrict__ colsum, int N, WireOut wo) {
+  __shared__ float4 red[16][16];
+  __shared__ float fin[64];
+  const int t = threadIdx.x, cg = t & 15, pc = t >> 4;
+  const int col = blockIdx.x * 64 + cg * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < N) {
+    for (int p = pc; p < parts; p += 16) {
+      const float4 q = *reinterpret_cast<const float4*>(part + (int64_t)p * N + col);
+      acc.x += q.x; acc.y += q.y; acc.z += q.z; acc.w += q.w;
+    }
+  }
+  red[pc][cg] = acc;
+  __syncthreads();
+  if (t < 16) {
+    float4 s = red[0][t];
+    for (int c = 1; c < 16; ++c) {
+      const float4 q = red[c][t];
+      s.x += q.x; s.y += q.y; s.z += q.z; s.w += q.w;
+    }
+    fin[t * 4] = s.x; fin[t * 4 + 1] = s.y; fin[t * 4 + 2] = s.z; fin[t * 4 + 3] = s.w;
+    if (col < N) *reinterpret_cast<float4*>(colsum + col) = s;
+  }
+  if constexpr (WIRE) {
+    __syncthreads();
+    const int c16 = blockIdx.x * 64 + t * 16;
+    if (t < 4 && c16 < N && wo.bias_off > 0) {  // N % 16 == 0
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = fin[t * 16 + u];
+      wire_store16(v, (uint32_t)wo.bias_off + (uint32_t)c16, wo);
     }
   }
 }
@@ -817,23 +1049,44 @@ constexpr int lds_bytes() {
   return ((3 * st <= 160 * 1024) ? 3 : 2) * st;
 }
 
-// Ping-pong main loop for 256x256 tiles (default); FAN_GEMM_PP=0 or gemm_set_pingpong(false) selects the
-// one-role loop (A/B comparisons in one process).
-inline bool use_pingpong() { return gemm_pingpong_flag().load(std::memory_order_relaxed); }
+// 256x256 main loop selection (gemm_main_loop_flag(): 0 one-role, 1 staggered, 2 pipelined), read per launch so
+// A/B comparisons run in one process.
+inline int main_loop_mode() { return gemm_main_loop_flag().load(std::memory_order_relaxed); }
 
+// Launches the main loop; returns the number of bias-gradient partial slabs it left in the workspace for an ordered
+// reduce (split_k with split-K; without: the pipelined loop's tile rows, 0 = colsum written by the kernel).
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
-void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
+int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
   const int grid = cdiv_i(a.M, BM) * cdiv_i(a.N, BN) * sk;
   if constexpr (BM == 256 && BN == 256 && WM * WN == 8) {
-    // the staggered loop has no edge path: aligned shapes only
-    if (use_pingpong() && a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0) {
+    // the staggered and pipelined loops have no edge path: aligned shapes only
+    const int mode = main_loop_mode();
+    const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
+    if (mode == 2 && aligned && (!a.colsum || a.workspace)) {
+      constexpr int lds = 2 * (BM + BN) * BK * 2;
+      auto launch = [&](auto k) {
+        FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        hipLaunchKernelGGL(k, grid, 512, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
+                           a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
+                           (float*)a.workspace, a.colsum, wo);
+      };
+      if constexpr (!BKC) {
+        if (a.colsum) {
+          launch(gemm_pl_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>);
+          return SPLIT ? sk : a.M / BM;
+        }
+      }
+      launch(gemm_pl_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>);
+      return 0;
+    }
+    if (mode == 1 && aligned) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto k = gemm_pp_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT>;
       FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
       hipLaunchKernelGGL(k, grid, 512, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
                          (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
                          a.colsum, wo);
-      return;
+      return SPLIT && a.colsum ? sk : 0;
     }
   }
   constexpr int lds = lds_bytes<BM, BN>();
@@ -848,6 +1101,12 @@ void launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
   hipLaunchKernelGGL(k, grid, WM * WN * 64, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
                      a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
                      a.colsum, wo);
+  return SPLIT && a.colsum ? sk : 0;
+}
+
+template <bool WIRE>
+void launch_colsum_reduce(const float* part, int parts, const GemmArgs& a, const WireOut& wo, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_reduce_kernel<WIRE>, cdiv_i(a.N, 64), 256, 0, s, part, parts, a.colsum, a.N, wo);
 }
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
@@ -860,9 +1119,9 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
 #endif
   };
   if (sk > 1) {
-    // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + k*N]), then an ordered reduce that
+    // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + p*N]), then an ordered reduce that
     // applies the epilogue (deterministic: slabs summed in split order)
-    launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, true>(a, sk, wo, s);
+    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, true>(a, sk, wo, s);
     if constexpr (EPI == kEpiWire) {
       const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
       hipLaunchKernelGGL(splitk_reduce_wire_kernel<0>, stream_grid(items), 256, 0, s, (const float*)a.workspace, sk,
@@ -872,11 +1131,12 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
                          (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
                          a.ldaux, a.M, a.N);
       if (a.colsum)
-        hipLaunchKernelGGL(splitk_colsum_kernel<0>, (a.N + 255) / 256, 256, 0, s,
-                           (const float*)a.workspace + (size_t)sk * a.M * a.N, sk, a.colsum, a.N);
+        launch_colsum_reduce<false>((const float*)a.workspace + (size_t)sk * a.M * a.N, parts, a, wo, s);
     }
   } else {
-    launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>(a, sk, wo, s);
+    // bias-gradient partials at ws[p * N] (pipelined loop): ordered reduce (+ the bias segment's wire encode)
+    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>(a, sk, wo, s);
+    if (parts > 0) launch_colsum_reduce<EPI == kEpiWire>((const float*)a.workspace, parts, a, wo, s);
   }
 }
 

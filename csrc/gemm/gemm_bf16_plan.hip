@@ -29,11 +29,14 @@ extern template void launch_tile<true, false>(const GemmArgs&, int, int, int, in
 extern template void launch_tile<true, true>(const GemmArgs&, int, int, int, int, hipStream_t);
 }  // namespace gemm_detail
 
-std::atomic<bool>& gemm_pingpong_flag() {
-  // Off by default until it measures faster than the one-role loop (FAN_GEMM_PP=1 / gemm_set_pingpong(true)).
-  static std::atomic<bool> flag{[] {
+std::atomic<int>& gemm_main_loop_flag() {
+  // 256x256 main loop (aligned shapes): 2 software-pipelined (default), 0 one-role loop (FAN_GEMM_PL=0), 1
+  // staggered 4-phase (FAN_GEMM_PP=1). The others stay selectable for in-process A/B (gemm_set_main_loop).
+  static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_PP");
-    return e && e[0] == '1';
+    if (e && e[0] == '1') return 1;
+    const char* pl = getenv("FAN_GEMM_PL");
+    return pl && pl[0] == '0' ? 0 : 2;
   }()};
   return flag;
 }

@@ -30,6 +30,11 @@ def _workspace(device, numel):
     return t
 
 
+def _bf16_ws_floats(M: int, N: int, sk: int, bm: int, colsum) -> int:
+    """f32 workspace of a bf16 GEMM plan: split-K slabs, then bias-gradient partials (split_k per tile row)."""
+    return (sk * M * N if sk > 1 else 0) + (sk * (-(-M // bm)) * N if colsum is not None else 0)
+
+
 def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
     """Split K so small output grids still fill the 256 CUs (ordered, deterministic slab reduce)."""
     tiles = (M // 128) * (N // 128)
@@ -65,7 +70,8 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
         if bm == 0:
             raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
         tbm, tbn = bm, bn  # launch exactly the planned tile (re-planning with an explicit split_k differs)
-        ws = _workspace(C.device, sk * (M * N + N)) if sk > 1 else None
+        need = _bf16_ws_floats(M, N, sk, bm, colsum)
+        ws = _workspace(C.device, need) if need else None
         Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, tbm, tbn, colsum, tw, buf, int(shard),
                 int(own), int(codec), period)
         return C
@@ -89,8 +95,9 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
             if bm == 0:
                 raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
             tbm, tbn = bm, bn  # launch exactly the planned tile (re-planning with an explicit split_k differs)
-            if sk > 1:
-                ws = _workspace(C.device, sk * (M * N + N))
+            need = _bf16_ws_floats(M, N, sk, bm, colsum)
+            if need:
+                ws = _workspace(C.device, need)
         else:
             sk = Cx.gemm_f32_split(M, N, K, sk)
             if sk > 1:

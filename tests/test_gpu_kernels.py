@@ -212,13 +212,15 @@ def test_gemm_fused_bias_grad(C, M, N, K, sk, tile):
     assert (db - dZ.float().sum(0)).abs().max().item() < 1e-2 * K ** 0.5
 
 
-@pytest.fixture(params=[False, True], ids=["oneloop", "staggered"])
+@pytest.fixture(params=[0, 1, 2], ids=["oneloop", "staggered", "pipelined"])
 def main_loop(request, C):
-    """Both 256x256 main loops: the one-role loop and the staggered 4-phase loop (gemm_set_pingpong)."""
+    """Every 256x256 main loop: one-role, staggered 4-phase and software-pipelined (gemm_set_main_loop; the
+    pipelined loop serves the K-contiguous-A layouts, the others fall back to the default loop)."""
     Cx = G._ext.require()
-    Cx.gemm_set_pingpong(request.param)
+    mode0 = Cx.gemm_main_loop()
+    Cx.gemm_set_main_loop(request.param)
     yield request.param
-    Cx.gemm_set_pingpong(False)
+    Cx.gemm_set_main_loop(mode0)
 
 
 @pytest.mark.parametrize("K", [64, 128, 192, 1024, 4096])
