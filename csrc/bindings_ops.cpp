@@ -169,7 +169,8 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_set_pingpong", [](bool on) { gemm_main_loop_flag().store(on ? 1 : 0); },
         "256x256 GEMM tiles: staggered 4-phase main loop (true) or the one-role loop (false)");
   m.def("gemm_set_main_loop", [](int mode) { gemm_main_loop_flag().store(mode); },
-        "256x256 GEMM tiles: 0 one-role loop, 1 staggered 4-phase loop, 2 software-pipelined loop (K-contiguous A)");
+        "256x256 GEMM tiles: 0 one-role, 1 staggered 4-phase, 2 pipelined (4 or 8 waves by layout / K), "
+        "3 pipelined 4-wave, 5 pipelined 8-wave");
   m.def("gemm_main_loop", []() { return gemm_main_loop_flag().load(); });
   m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {
           gemm_set_stamp_buffer(t ? t->data_ptr() : nullptr);

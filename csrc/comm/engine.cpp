@@ -31,6 +31,11 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     for (int i = 0; i < world; ++i) orders_[0][i] = i;
   }
   inline_ = world == 1 && !cfg.force_comm;
+  if (inline_) {
+    const char* se = std::getenv("FAN_SIDE_EPI");
+    side_epi_ = cfg.side_epilogue >= 0 ? cfg.side_epilogue > 0 : (se && se[0] == '1');
+    if (side_epi_) FAN_HIP_CHECK(hipStreamCreateWithPriority(&epi_stream_, hipStreamNonBlocking, 0));
+  }
   if (cfg_.chunk_elems <= 0) {
     const char* ce = std::getenv("FAN_CHUNK_ELEMS");
     cfg_.chunk_elems = ce ? std::atoll(ce) : (int64_t(1) << 26);
@@ -96,6 +101,7 @@ AllReduceEngine::~AllReduceEngine() {
   if (verr_dev_) hipFree(verr_dev_);
   if (verr_host_) hipHostFree(verr_host_);
   hipStreamDestroy(aux_stream_);
+  if (epi_stream_) hipStreamDestroy(epi_stream_);
   hipStreamDestroy(stream_);
 }
 
@@ -616,6 +622,12 @@ void AllReduceEngine::commit_slot(Slot& sl, int slot, bool after_producer, hipSt
     // the producer's GEMMs (a side-stream epilogue takes CU slots from their tiles).
     FAN_HIP_CHECK(hipStreamWaitEvent(producer, sl.comm_done, 0));
     sl.epi_stream = producer;
+  } else if (side_epi_ && after_producer) {
+    // world 1: the request has no communication phase (it ran in the producer's order); its decode + SGD runs on
+    // the side stream after everything the producer has enqueued so far, beside the producer's next GEMMs
+    FAN_HIP_CHECK(hipEventRecord(sl.update, producer));
+    FAN_HIP_CHECK(hipStreamWaitEvent(epi_stream_, sl.update, 0));
+    sl.epi_stream = epi_stream_;
   } else if (after_producer && producer != sl.stream) {
     // inline requests already run on the producer's stream: stream order is the dependency
     FAN_HIP_CHECK(hipEventRecord(sl.update, producer));

@@ -43,6 +43,9 @@ struct EngineConfig {
   int64_t chunk_elems = 0;
   // ring: direct links (row-major world x world, links[a*world+b]: a can send to b); empty = fully connected
   std::vector<char> links;
+  // world 1 (inline, no communication phase): run each committed epilogue (decode + SGD) on an engine stream
+  // beside the producer's next kernels instead of in the producer's stream order; -1: from FAN_SIDE_EPI
+  int side_epilogue = -1;
 };
 
 struct EngineLayout {
@@ -145,6 +148,7 @@ class AllReduceEngine {
   // phase) instead of on the comm stream.
   void set_epilogue_on_producer(bool on) { epi_on_producer_ = on; }
   bool epilogue_on_producer() const { return epi_on_producer_; }
+  bool side_epilogue() const { return side_epi_; }
   std::string diagnostics(int slot) const;
   bool verify() const { return verify_; }
   // verify mode: raise (with site, row, checksums, sequence numbers) if any message so far failed its check
@@ -205,6 +209,8 @@ class AllReduceEngine {
   std::vector<std::vector<int>> orders_;
   hipStream_t stream_ = nullptr;
   hipStream_t aux_stream_ = nullptr;  // chunked mesh: owner reduces + per-chunk epilogues beside the collectives
+  hipStream_t epi_stream_ = nullptr;  // world-1 side epilogues (normal priority: the producer's GEMMs keep theirs)
+  bool side_epi_ = false;
   hipEvent_t cev_[4][2] = {};         // chunked mesh pipeline events: [all-to-all, reduce, all-gather, epilogue][parity]
   bool epi_on_producer_ = false;
   // world 1 without forced collectives: nothing to overlap, so requests run inline on the producer's

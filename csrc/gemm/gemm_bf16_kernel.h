@@ -28,6 +28,7 @@
 #pragma once
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "bfp/bfp_format.h"
 #include "gemm/gemm.h"
@@ -943,6 +944,170 @@ __global__ void __launch_bounds__(512, 2)
                                                  aux, ldaux, M, N, ksplit, ws, wo);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Software-pipelined 256x256 kernel with 4 waves (2x2, one per SIMD, 128x128 per wave) and the accumulators in
+// AGPRs: a 128x128 wave tile reads (128 + 128) x K fragments per 128x128 outputs where the 8-wave kernel's 128x64
+// tiles read (128 + 64) per 128x64, so the CU's LDS read traffic per K-tile drops by a third (the hipBLASLt
+// choice for these shapes, profiles/r1_gemm_experiments.md round 2). The MFMAs are inline asm with "+a"
+// accumulator operands: 256 accumulators then stay in the AGPR file (hipcc's allocator otherwise rotates them
+// through VGPRs); volatile asm also pins the issue order of the reads, DMA and MFMAs to the source order. Both
+// fragment sets are double-buffered (VGPRs are free here), so a read never overwrites a register an MFMA of the
+// same k-step still reads. Same K-tile schedule as gemm_pl_kernel: k-step 0 reads (t, 1); wait + barrier; k-step 1
+// reads (t + 1, 0) and issues the DMA of K-tile t + 2 (16 pieces per wave, one per 4 MFMAs; one per 2 measured no
+// faster).
+
+// compile-time loop: f(integral_constant<int, 0..N-1>) in order (indices stay constants: no dynamic array access)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false>
+__global__ void __launch_bounds__(256, 1)
+    gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
+                    TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
+                    int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
+                    float* __restrict__ colsum, WireOut wo) {
+  constexpr int BM = 256, BN = 256, NT = 256;
+  constexpr int A_BYTES = OpTile<BM, NT>::BYTES;
+  constexpr int STAGE = A_BYTES + OpTile<BN, NT>::BYTES;
+  constexpr int GA = OpTile<BM, NT>::GLDS, G = GA + OpTile<BN, NT>::GLDS;  // 8 + 8 pieces per wave and K-tile
+  constexpr int WTM = 128, WTN = 128, MI = 8, NJ = 8;
+  static_assert(G == 16, "16 glds pieces per wave and K-tile");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
+  const int wg = xcd_remap(blockIdx.x, tiles * split_k);
+  const int tile = wg % tiles, ksplit = wg / tiles;
+  const int GM = tiles_m >= 4 ? 4 : tiles_m;
+  const int grp = tile / (GM * tiles_n);
+  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
+  const int in_grp = tile % (GM * tiles_n);
+  const int m0 = (grp * GM + in_grp % gm) * BM;
+  const int n0 = (in_grp / gm) * BN;
+  const int k_per = K / split_k;
+  const int kbeg = ksplit * k_per;
+  const int nk = k_per / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / 2, wn = wave % 2;
+  // fused bias gradient: as gemm_pl_kernel (waves wm == 0; spread over the tile rows without split-K)
+  const int im = SPLIT ? 0 : m0 / BM;
+  const int cs0 = SPLIT ? (m0 == 0 ? 0 : nk) : im * nk / tiles_m;
+  const int cs1 = SPLIT ? nk : (im + 1) * nk / tiles_m;
+  const bool do_colsum = COLSUM && wm == 0;
+  float cs[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 fa[2][MI], fb[2][NJ];
+
+  uint32_t off[G];
+#pragma unroll
+  for (int p = 0; p < GA; ++p) off[p] = piece_off<AK, BM, NT>(lda, m0, wave, lane, p);
+#pragma unroll
+  for (int p = GA; p < G; ++p) off[p] = piece_off<BKC, BN, NT>(ldb, n0, wave, lane, p - GA);
+  const int64_t a_step = AK ? (int64_t)BK * 2 : (int64_t)BK * lda * 2;
+  const int64_t b_step = BKC ? (int64_t)BK * 2 : (int64_t)BK * ldb * 2;
+  const char* a_k0 = reinterpret_cast<const char*>(A) + (AK ? (int64_t)kbeg * 2 : (int64_t)kbeg * lda * 2);
+  const char* b_k0 = reinterpret_cast<const char*>(B) + (BKC ? (int64_t)kbeg * 2 : (int64_t)kbeg * ldb * 2);
+  const uint32_t lds0 = lds_addr_of(smem);
+
+  // glds piece p (0..15) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
+  // the accumulator array in scratch memory)
+  auto piece = [&](int kt, int p) __attribute__((always_inline)) {
+    const uint32_t st = lds0 + (kt & 1) * STAGE + wave * 1024;
+    if (p < GA) glds16_s(a_k0 + kt * a_step, off[p], st + p * OpTile<BM, NT>::IB);
+    else glds16_s(b_k0 + kt * b_step, off[p], st + A_BYTES + (p - GA) * OpTile<BN, NT>::IB);
+  };
+  // next k-step's fragment r (0..15: A rows 0..7, then B columns 0..7) into set `set`
+  auto read_next = [&](const char* st, int ks, int set, int r) __attribute__((always_inline)) {
+    if (r < MI) fa[set][r] = read_frag<AK>(st, wm * WTM + r * 16, ks, lane);
+    else fb[set][r - MI] = read_frag<BKC>(st + A_BYTES, wn * WTN + (r - MI) * 16, ks, lane);
+  };
+  // One k-step: 64 MFMAs on set `cur`; READ: the 16 fragments of the next k-step into set cur ^ 1, one per 3
+  // MFMAs from the start (all issued by MFMA 48: the barrier's lgkmcnt(0) after k-step 0 then waits on nothing
+  // young); DMA: the 16 pieces of K-tile dma_kt, one per 4 MFMAs.
+  auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int rd_ks, int dma_kt,
+                   bool csk) __attribute__((always_inline)) {
+    constexpr int cur = decltype(cur_c)::value;
+    constexpr bool READ = decltype(read_c)::value, DMA = decltype(dma_c)::value;
+    if (COLSUM && csk)
+      static_for<NJ>([&](auto jc) __attribute__((always_inline)) { cs[jc.value] += frag_sum(fb[cur][jc.value]); });
+    static_for<MI * NJ>([&](auto qc) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+      if constexpr (READ && q % 3 == 0 && q / 3 < MI + NJ) read_next(rd_st, rd_ks, cur ^ 1, q / 3);
+      if constexpr (DMA && q % 4 == 1) piece(dma_kt, q / 4);
+      mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
+    });
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  // prologue: K-tiles 0 and 1 in flight; retire 0 (this wave), barrier (every wave), read k-step (0, 0)
+#pragma unroll
+  for (int p = 0; p < G; ++p) piece(0, p);
+  if (nk > 1) {
+#pragma unroll
+    for (int p = 0; p < G; ++p) piece(1, p);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int r = 0; r < MI + NJ; ++r) read_next(smem, 0, 0, r);
+
+  auto ktile = [&](int kt, auto more_c, auto more2_c) __attribute__((always_inline)) {
+    const char* st = smem + (kt & 1) * STAGE;
+    const bool csk = do_colsum && kt >= cs0 && kt < cs1;
+    FAN_STAMP(0);
+    block(I0{}, T_{}, F_{}, st, 1, 0, csk);
+    FAN_STAMP(1);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    FAN_STAMP(2);
+    __builtin_amdgcn_s_barrier();
+    FAN_STAMP(3);
+    block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk);
+    FAN_STAMP(4);
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) ktile(kt, T_{}, T_{});
+  if (kt + 1 < nk) ktile(kt++, T_{}, F_{});
+  if (kt < nk) ktile(kt, F_{}, F_{});
+
+  // the last MFMAs' results land in the AGPRs before anything reads them (inline asm: no hazard tracking)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
+  if (COLSUM && do_colsum && (!SPLIT || m0 == 0))
+    colsum_finish<NJ, WTN, kEpiNone, true>(
+        cs, lane, n0 + wn * WTN, ws + (SPLIT ? (int64_t)split_k * M * N + (int64_t)ksplit * N : (int64_t)im * N), wo,
+        N);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every operand read retired before the epilogue reuses the LDS
+  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
+                                                 aux, ldaux, M, N, ksplit, ws, wo);
+}
+
 // Ordered split-K reduction + epilogue (deterministic: slabs summed in split order).
 template <int EPI, typename TC, bool ACCUM>
 __global__ void __launch_bounds__(256)
@@ -1049,8 +1214,8 @@ constexpr int lds_bytes() {
   return ((3 * st <= 160 * 1024) ? 3 : 2) * st;
 }
 
-// 256x256 main loop selection (gemm_main_loop_flag(): 0 one-role, 1 staggered, 2 pipelined), read per launch so
-// A/B comparisons run in one process.
+// 256x256 main loop selection (gemm_main_loop_flag(): 0 one-role, 1 staggered, 2 pipelined (4 or 8 waves by
+// layout / K), 3 pipelined 4-wave, 5 pipelined 8-wave), read per launch so A/B comparisons run in one process.
 inline int main_loop_mode() { return gemm_main_loop_flag().load(std::memory_order_relaxed); }
 
 // Launches the main loop; returns the number of bias-gradient partial slabs it left in the workspace for an ordered
@@ -1062,7 +1227,28 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     // the staggered and pipelined loops have no edge path: aligned shapes only
     const int mode = main_loop_mode();
     const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
-    if (mode == 2 && aligned && (!a.colsum || a.workspace)) {
+    // pipelined loops: 4 waves (128x128 per wave, AGPR accumulators) where they measured faster — an MN-contiguous
+    // B, or a long K (its epilogue, half the waves of the 8-wave kernel's, is slower: bwd-data at K 1024 77 vs
+    // 70 us, profiles/r1_gemm_experiments.md) — else 8 waves; modes 3 / 5 force one of them
+    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192));
+    if (pl4 && aligned && (!a.colsum || a.workspace)) {
+      constexpr int lds = 2 * (BM + BN) * BK * 2;
+      auto launch = [&](auto k) {
+        FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        hipLaunchKernelGGL(k, grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
+                           a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
+                           (float*)a.workspace, a.colsum, wo);
+      };
+      if constexpr (!BKC) {
+        if (a.colsum) {
+          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>);
+          return SPLIT ? sk : a.M / BM;
+        }
+      }
+      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>);
+      return 0;
+    }
+    if ((mode == 2 || mode == 5) && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto launch = [&](auto k) {
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
