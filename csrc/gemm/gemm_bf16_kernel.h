@@ -1228,9 +1228,10 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     const int mode = main_loop_mode();
     const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
     // pipelined loops: 4 waves (128x128 per wave, AGPR accumulators) where they measured faster — an MN-contiguous
-    // B, or a long K (its epilogue, half the waves of the 8-wave kernel's, is slower: bwd-data at K 1024 77 vs
-    // 70 us, profiles/r1_gemm_experiments.md) — else 8 waves; modes 3 / 5 force one of them
-    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192));
+    // B, or a long K — else 8 waves: the 4-wave epilogue runs on half the waves (bwd-data at K 1024: 77 vs 70 us;
+    // the in-kernel wire encode: bwd-weight 4096^2 +13 vs +7 us, profiles/r1_gemm_experiments.md); modes 3 / 5
+    // force one of them
+    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192) && !(EPI == kEpiWire && !SPLIT));
     if (pl4 && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto launch = [&](auto k) {

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 from fpga_ai_nic_amd.ops import gemm as G  # noqa: E402
 
 Cx = G._ext.require()
-WG, W, KT, P = 8, 8, 64, 5
+WG, W, KT, P = 8, 8, 64, 5  # waves: up to 8 (the 4-wave kernel fills 4)
 buf = torch.zeros(WG * W * KT * P, dtype=torch.int64, device="cuda")
 shapes = {"fwd1": (8192, 4096, 4096, False, False), "bwdd1": (8192, 4096, 4096, False, True),
           "bwdw1": (4096, 4096, 8192, True, False)}
