@@ -54,6 +54,26 @@ void register_engine(pybind11::module_& m) {
                                   at::TensorOptions().dtype(at::kByte).device(at::kCUDA, at::cuda::current_device()));
            },
            "diagnostics: this rank's receive arena as a uint8 tensor (no copy)")
+      .def("set_timing", &P2PComm::set_timing, "time every flag wait with device events (stall counters)")
+      .def("stats",
+           [](P2PComm& c) {
+             P2PComm::Stats t;
+             {
+               pybind11::gil_scoped_release nogil;  // waits for the timed waits' events
+               t = c.stats();
+             }
+             pybind11::dict d;
+             d["ready_waits"] = t.ready_waits;
+             d["credit_waits"] = t.credit_waits;
+             d["timed_waits"] = t.timed_waits;
+             d["ready_stall_ms"] = t.ready_stall_ms;
+             d["credit_stall_ms"] = t.credit_stall_ms;
+             d["bytes_to_peer"] = t.bytes_to_peer;
+             return d;
+           },
+           "device-side stall counters: flag waits (ready / credit), their device time when timed, bytes per peer")
+      .def("reset_stats", &P2PComm::reset_stats)
+      .def("flags_snapshot", &P2PComm::flags_snapshot, "ready-from-src[world] + ack-from-dst[world] words")
       .def("all_to_all",
            [](P2PComm& c, const at::Tensor& send, at::Tensor& recv) {
              TORCH_CHECK(bytes_of(send) == bytes_of(recv) && bytes_of(send) % c.world() == 0, "all_to_all sizes");
@@ -257,6 +277,8 @@ void register_engine(pybind11::module_& m) {
       .def("latency_ms", &AllReduceEngine::latency_ms, py::call_guard<py::gil_scoped_release>())
       .def("set_timing", &AllReduceEngine::set_timing)
       .def("diagnostics", &AllReduceEngine::diagnostics)
+      .def("debug_status", &AllReduceEngine::debug_status,
+           "JSON snapshot: configuration, every slot, counters, comm error, P2P flags + stall counters")
       .def_property_readonly("verify", &AllReduceEngine::verify)
       .def("check_verify", &AllReduceEngine::check_verify,
            "verify mode: raise if any message so far failed its checksum / sequence check")
@@ -276,6 +298,7 @@ void register_engine(pybind11::module_& m) {
              d["forced_commits"] = c.forced_commits;
              d["verified_rows"] = c.verified_rows;
              d["direct_rounds"] = c.direct_rounds;
+             d["peer_bytes"] = c.peer_bytes;
              return d;
            },
            "perf counters (the NIC's latency / host-stall registers): requests, bytes, host wait, device time")

@@ -222,6 +222,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     if (verify_) launch_msg_tags(P, sb, sb, N, req_seq_, tag_region(0), st);
     fault_.maybe_corrupt("mesh_pack", const_cast<uint8_t*>(P), sb * N, st);  // in flight: after the tags
     comm_->all_to_all(P, R, sb, st);
+    count_peers(sb);
     if (verify_) {
       comm_->all_to_all(tag_region(0), tag_region(1), 16, st);
       verify_rows(R, sb, N, tag_region(1), 1, 0, st);
@@ -239,6 +240,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     if (verify_) launch_msg_tags(S, sb, sb, 1, req_seq_, tag_region(3), st);
     fault_.maybe_corrupt("mesh_reduce", S, sb, st);
     comm_->all_gather(S, G, sb, st);
+    count_peers(sb);
     if (verify_) {
       comm_->all_gather(tag_region(3), tag_region(4), 16, st);
       verify_rows(G, sb, N, tag_region(4), 2, 0, st);
@@ -286,6 +288,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
   }
   mark(kTpPacked);
   d->publish(r1, st);
+  count_peers(sb, d);
   d->wait(r1, st);
   mark(kTpExchanged);
   P2PComm::Round r2 = d->begin(st);
@@ -299,6 +302,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
   }
   mark(kTpReduced);
   d->publish(r2, st);
+  count_peers(sb, d);
   d->wait(r2, st);
   counters_.direct_rounds += 2;
   const uint8_t* Gv = d->src_base(r2);
@@ -362,6 +366,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
     if (verify_) launch_msg_tags(S[ch % 2], sb, sb, 1, req_seq_, tag_region(3), A);
     fault_.maybe_corrupt("mesh_reduce", S[ch % 2], sb, A);
     comm_->all_gather(S[ch % 2], gath(ch), sb, A);
+    count_peers(sb);
     if (verify_) {
       comm_->all_gather(tag_region(3), tag_region(4), 16, A);
       verify_rows(gath(ch), sb, N, tag_region(4), 2, (uint32_t)(ch * N), A);
@@ -390,6 +395,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
       if (verify_) launch_msg_tags(P, sb, sb, N, req_seq_, tag_region(0), A);
       fault_.maybe_corrupt("mesh_pack", const_cast<uint8_t*>(P), cb, A);
       comm_->all_to_all(P, R[ch % 2], sb, A);
+      count_peers(sb);
       if (verify_) {
         comm_->all_to_all(tag_region(0), tag_region(1), 16, A);
         verify_rows(R[ch % 2], sb, N, tag_region(1), 1, (uint32_t)(ch * N), A);
@@ -505,6 +511,8 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
         for (size_t q = 0; q < nr; ++q) recvs.push_back({tag_region(1) + q * 4, 16, recvs[q].peer});
       }
       for (size_t q = 0; q < nd; ++q) fault_.maybe_corrupt("ring_send", static_cast<uint8_t*>(sends[q].ptr), sb, st);
+      if (counters_.peer_bytes.size() != (size_t)world_) counters_.peer_bytes.assign(world_, 0);
+      for (const P2POp& op : sends) counters_.peer_bytes[op.peer] += (int64_t)op.bytes;
       comm_->sendrecv(sends, recvs, st);
       if (verify_)
         for (size_t q = 0; q < nr; ++q)
@@ -671,6 +679,7 @@ bool AllReduceEngine::query(int slot, uint32_t seq) {
 
 void AllReduceEngine::set_tracing(bool on, int capacity) {
   tracing_ = on;
+  if (P2PComm* d = comm_ ? comm_->direct() : nullptr) d->set_timing(on);  // device stall time of the flag waits
   if (!on) return;
   // a new trace window: wait for the previous window's requests before their events are re-recorded
   for (size_t i = 0; i < trace_used_; ++i) hipEventSynchronize(trace_pool_[i].ev[kTpEpiEnd]);
@@ -706,6 +715,52 @@ TraceSummary AllReduceEngine::trace_summary() {
     r.wire_bytes += t.wire_bytes;
   }
   return r;
+}
+
+void AllReduceEngine::count_peers(size_t bytes, P2PComm* direct) {
+  if (counters_.peer_bytes.size() != (size_t)world_) counters_.peer_bytes.assign(world_, 0);
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    counters_.peer_bytes[p] += (int64_t)bytes;
+    if (direct) direct->count_sent(p, bytes);  // the P2P transport's own count (its copies count themselves)
+  }
+}
+
+std::string AllReduceEngine::debug_status() {
+  std::ostringstream os;
+  os << "{\"rank\": " << rank_ << ", \"world\": " << world_ << ", \"algo\": \"" << (cfg_.algo ? "ring" : "mesh")
+     << "\", \"codec\": " << cfg_.codec << ", \"inline\": " << (inline_ ? "true" : "false")
+     << ", \"verify\": " << (verify_ ? "true" : "false") << ", \"requests\": " << seq_
+     << ", \"next_slot\": " << next_slot_ << ", \"slots\": [";
+  for (int i = 0; i < kSlots; ++i) {
+    const Slot& sl = slots_[i];
+    os << (i ? ", " : "") << "{\"slot\": " << i << ", \"seq\": " << sl.seq << ", \"pending\": "
+       << (sl.pending ? "true" : "false") << ", \"done_word\": " << flags_host_[i * 16]
+       << ", \"epilogue_stream\": \""
+       << (sl.epi_stream == nullptr ? "none" : sl.epi_stream == stream_ ? "comm" : sl.epi_stream == epi_stream_ ? "side"
+                                                                                 : "producer")
+       << "\", \"age_s\": " << (sl.seq ? now_s() - sl.t_issue : 0.0) << "}";
+  }
+  os << "], \"forced_commits\": " << counters_.forced_commits << ", \"direct_rounds\": " << counters_.direct_rounds
+     << ", \"peer_bytes\": [";
+  for (size_t p = 0; p < counters_.peer_bytes.size(); ++p) os << (p ? ", " : "") << counters_.peer_bytes[p];
+  std::string err = comm_ ? comm_->async_error() : "";
+  for (char& ch : err)
+    if (ch == '"' || ch == '\\') ch = '\'';
+  os << "], \"comm_error\": \"" << err << "\"";
+  if (verify_) os << ", \"verify_error\": " << (verr_host_->flag ? "true" : "false");
+  if (P2PComm* d = comm_ ? comm_->direct() : nullptr) {
+    const P2PComm::Stats st = d->stats();
+    os << ", \"p2p\": {\"sequence\": " << d->sequence() << ", \"ready_waits\": " << st.ready_waits
+       << ", \"credit_waits\": " << st.credit_waits << ", \"timed_waits\": " << st.timed_waits
+       << ", \"ready_stall_ms\": " << st.ready_stall_ms << ", \"credit_stall_ms\": " << st.credit_stall_ms
+       << ", \"flags\": [";
+    const std::vector<uint64_t> f = d->flags_snapshot();
+    for (size_t i = 0; i < f.size(); ++i) os << (i ? ", " : "") << f[i];
+    os << "]}";
+  }
+  os << "}";
+  return os.str();
 }
 
 std::string AllReduceEngine::diagnostics(int slot) const {

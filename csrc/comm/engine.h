@@ -73,6 +73,7 @@ struct EngineCounters {
   uint64_t forced_commits = 0;  // deferred epilogues committed because their slot was needed (> kSlots deferred)
   uint64_t verified_rows = 0;   // verify mode: message rows whose tags were checked on arrival
   uint64_t direct_rounds = 0;   // direct P2P rounds (kernels stored into / read from peer receive slots in place)
+  std::vector<int64_t> peer_bytes;  // message bytes sent to each peer (all-to-all, all-gather, ring hops, direct)
 };
 
 // Device-side request trace: GPU timestamps (timing events) at the phase boundaries of each request, the MI355X
@@ -150,6 +151,10 @@ class AllReduceEngine {
   bool epilogue_on_producer() const { return epi_on_producer_; }
   bool side_epilogue() const { return side_epi_; }
   std::string diagnostics(int slot) const;
+  // Debug snapshot (the NIC's debug_status register, hw/all_reduce.sv:1415-1421), JSON: engine configuration,
+  // every slot (sequence, pending epilogue, done word, stream kind), counters, the communicator's async error and,
+  // on the P2P transport, its flag block and device stall counters. Host-only reads except the P2P flag copy.
+  std::string debug_status();
   bool verify() const { return verify_; }
   // verify mode: raise (with site, row, checksums, sequence numbers) if any message so far failed its check
   void check_verify();
@@ -189,6 +194,7 @@ class AllReduceEngine {
     if (cur_trace_ >= 0) FAN_HIP_CHECK(hipEventRecord(trace_pool_[cur_trace_].ev[tp], run_stream_));
   }
   void commit_slot(Slot& sl, int slot, bool after_producer, hipStream_t producer);
+  void count_peers(size_t bytes, P2PComm* direct = nullptr);  // `bytes` sent to every other rank
   uint8_t* scratch(const std::string& key, size_t bytes);
   std::vector<EpiThunk> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,

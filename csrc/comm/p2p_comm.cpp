@@ -57,6 +57,57 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
   peer_flags_[rank] = flags_;
   last_sent_[0].assign(world, 0);
   last_sent_[1].assign(world, 0);
+  bytes_to_peer_.assign(world, 0);
+}
+
+void P2PComm::wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool credit) {
+  (credit ? credit_waits_ : ready_waits_)++;
+  TimedWait* t = nullptr;
+  if (timing_) {
+    if (tw_used_ == tw_.size()) {
+      TimedWait n{};
+      FAN_HIP_CHECK(hipEventCreate(&n.ev[0]));
+      FAN_HIP_CHECK(hipEventCreate(&n.ev[1]));
+      tw_.push_back(n);
+    }
+    t = &tw_[tw_used_++];
+    t->credit = credit;
+    FAN_HIP_CHECK(hipEventRecord(t->ev[0], s));
+  }
+  FAN_HIP_CHECK(hipStreamWaitValue64(s, flag, value, hipStreamWaitValueGte));
+  if (t) FAN_HIP_CHECK(hipEventRecord(t->ev[1], s));
+}
+
+P2PComm::Stats P2PComm::stats() {
+  for (size_t i = 0; i < tw_used_; ++i) {  // fold the recorded waits into the totals, then recycle the events
+    float ms = 0.f;
+    FAN_HIP_CHECK(hipEventSynchronize(tw_[i].ev[1]));
+    FAN_HIP_CHECK(hipEventElapsedTime(&ms, tw_[i].ev[0], tw_[i].ev[1]));
+    stall_ms_[tw_[i].credit ? 1 : 0] += ms;
+    timed_++;
+  }
+  tw_used_ = 0;
+  Stats r;
+  r.ready_waits = ready_waits_;
+  r.credit_waits = credit_waits_;
+  r.timed_waits = timed_;
+  r.ready_stall_ms = stall_ms_[0];
+  r.credit_stall_ms = stall_ms_[1];
+  r.bytes_to_peer = bytes_to_peer_;
+  return r;
+}
+
+void P2PComm::reset_stats() {
+  stats();  // drain pending timed waits
+  ready_waits_ = credit_waits_ = timed_ = 0;
+  stall_ms_[0] = stall_ms_[1] = 0.0;
+  bytes_to_peer_.assign(world_, 0);
+}
+
+std::vector<uint64_t> P2PComm::flags_snapshot() const {
+  std::vector<uint64_t> v((size_t)2 * world_);
+  FAN_HIP_CHECK(hipMemcpy(v.data(), flags_, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return v;
 }
 
 void P2PComm::abort() {
@@ -82,6 +133,10 @@ P2PComm::~P2PComm() {
     if (!opened_[p]) continue;
     hipIpcCloseMemHandle(peer_arena_[p]);
     hipIpcCloseMemHandle(peer_flags_[p]);
+  }
+  for (auto& t : tw_) {
+    hipEventDestroy(t.ev[0]);
+    hipEventDestroy(t.ev[1]);
   }
   hipFree(flags_);
   hipFree(arena_);
@@ -140,12 +195,13 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
       if (!any) {
         const uint64_t prev = last_sent_[par][p];
-        if (prev) FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + world_ + p, prev, hipStreamWaitValueGte));
+        if (prev) wait_flag(s, flags_ + world_ + p, prev, true);
         any = true;
         dests.push_back(p);
       }
       FAN_CHECK(off + op.bytes <= slot_, "p2p: message larger than the arena slot (raise slot_bytes)");
       out.push_back({op.ptr, slot_ptr(peer_arena_[p], rank_, q) + off, op.bytes});
+      bytes_to_peer_[p] += (int64_t)op.bytes;
       off += (op.bytes + 15) / 16 * 16;
     }
   }
@@ -164,7 +220,7 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       if (op.peer != src || op.bytes == 0) continue;
       FAN_CHECK(src != rank_, "p2p: self-receive");
       if (!any) {
-        FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + src, q, hipStreamWaitValueGte));
+        wait_flag(s, flags_ + src, q, false);
         any = true;
         srcs.push_back(src);
       }
@@ -185,7 +241,7 @@ P2PComm::Round P2PComm::begin(hipStream_t s) {
     if (p == rank_) continue;
     FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
     const uint64_t prev = last_sent_[par][p];
-    if (prev) FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + world_ + p, prev, hipStreamWaitValueGte));
+    if (prev) wait_flag(s, flags_ + world_ + p, prev, true);
   }
   return r;
 }
@@ -201,7 +257,7 @@ void P2PComm::publish(const Round& r, hipStream_t s) {
 
 void P2PComm::wait(const Round& r, hipStream_t s) {
   for (int p = 0; p < world_; ++p)
-    if (p != rank_) FAN_HIP_CHECK(hipStreamWaitValue64(s, flags_ + p, r.seq, hipStreamWaitValueGte));
+    if (p != rank_) wait_flag(s, flags_ + p, r.seq, false);
 }
 
 void P2PComm::release(const Round& r, hipStream_t s) {

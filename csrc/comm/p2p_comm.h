@@ -93,6 +93,22 @@ class P2PComm : public Comm {
   uint8_t* arena() const { return arena_; }
   size_t arena_bytes() const { return (size_t)world_ * 2 * slot_; }
 
+  // Device-side stall counters (the NIC's stall_* / credit registers, hw/all_reduce.sv:892-1085, 468-483): every
+  // flag wait the command processor parks a stream on, split into ready waits (data from a peer) and credit waits
+  // (a peer acknowledging a slot); with timing on, each wait is bracketed by timing events on its stream, so the
+  // stall time is device time. bytes_to_peer: message bytes this rank stored into / copied to each peer.
+  struct Stats {
+    uint64_t ready_waits = 0, credit_waits = 0, timed_waits = 0;
+    double ready_stall_ms = 0.0, credit_stall_ms = 0.0;
+    std::vector<int64_t> bytes_to_peer;
+  };
+  void set_timing(bool on) { timing_ = on; }
+  Stats stats();  // waits for the timed waits' events
+  void reset_stats();
+  void count_sent(int peer, size_t bytes) { bytes_to_peer_[peer] += (int64_t)bytes; }
+  // flag block snapshot (ready-from-src[world], ack-from-dst[world]) for diagnostics (synchronous copy)
+  std::vector<uint64_t> flags_snapshot() const;
+
  private:
   void copy(const std::vector<P2PCopy>& segs, hipStream_t s);
   uint8_t* slot_ptr(uint8_t* arena, int src, uint64_t seq) const { return arena + ((size_t)src * 2 + (seq & 1)) * slot_; }
@@ -106,6 +122,19 @@ class P2PComm : public Comm {
   std::vector<uint64_t> last_sent_[2];  // per parity: sequence of the last message sent to each peer
   uint64_t seq_ = 0;
   bool aborted_ = false;
+  // stall accounting
+  void wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool credit);
+  bool timing_ = false;
+  uint64_t ready_waits_ = 0, credit_waits_ = 0;
+  struct TimedWait {
+    hipEvent_t ev[2];
+    bool credit;
+  };
+  std::vector<TimedWait> tw_;
+  size_t tw_used_ = 0;
+  double stall_ms_[2] = {0.0, 0.0};
+  uint64_t timed_ = 0;
+  std::vector<int64_t> bytes_to_peer_;
   bool uncached_ = false;
   std::string arena_mem_;
 };

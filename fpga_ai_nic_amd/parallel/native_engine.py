@@ -258,6 +258,14 @@ class NativeAllReduce:
     def diagnostics(self, h: NativeHandle) -> str:
         return self.C.diagnostics(h.slot)
 
+    def debug_status(self) -> dict:
+        """Snapshot of the engine (the NIC's debug_status register, hw/all_reduce.sv:1415-1421): configuration,
+        every request slot, per-peer bytes, communicator error and, on the P2P transport, its flag words and
+        device stall counters."""
+        import json
+
+        return json.loads(self.C.debug_status())
+
     def counters(self) -> dict:
         """Engine perf counters (reference: the NIC's lpbk_latency / stall_host registers read by
         get_all_reduce_latency / get_host_stall_cycles, sw/mlp_mpi_example_f32.cpp:100-112): requests, logical and

@@ -227,6 +227,13 @@ def test_engine_perf_counters(force):
     assert c["wire_bytes"] == 3 * eng.wire_bytes(L)
     assert c["timed_requests"] == 3 and c["device_ms"] > 0
     assert c["host_wait_s"] >= 0 and c["host_waits"] <= 3
+    # debug snapshot (the NIC's debug_status register): every slot, the last three requests' sequence numbers
+    # completed, nothing pending
+    d = eng.debug_status()
+    assert d["world"] == 1 and d["requests"] == 3 and len(d["slots"]) == 8
+    done = sorted(s["done_word"] if not d["inline"] else s["seq"] for s in d["slots"] if s["seq"])
+    assert [s["seq"] for s in d["slots"] if s["seq"]] == [1, 2, 3] and not any(s["pending"] for s in d["slots"])
+    assert d["comm_error"] == "" and d["inline"] == (not force) and done[-1] == 3
 
 
 def test_superseded_handle_never_acts_for_the_newer_request():

@@ -86,6 +86,23 @@ def _worker(rank, world, port, q):
             from fpga_ai_nic_amd.ops import bfp_oracle as O
 
             ok["direct_rounds"] = eng.counters()["direct_rounds"] >= 2
+            # device stall counters + debug snapshot (hw/all_reduce.sv:892-1085, 1415-1421): a traced direct
+            # request parks the stream on every peer's ready flag once per round and times those waits; bytes
+            # per peer = one wire shard per round; the flag words hold the last round's sequence
+            eng.trace(True)
+            comm.reset_stats()
+            eng.allreduce(g, out, n_valid=m).synchronize(30)
+            st = comm.stats()
+            dbg = eng.debug_status()
+            eng.trace(False)
+            sb = eng.wire_bytes(L) // (2 * (world - 1)) if world > 1 else 0
+            peer = (rank + 1) % world
+            ok["stall_counters"] = (st["ready_waits"] == 2 * (world - 1) and st["timed_waits"] >= st["ready_waits"]
+                                    and st["ready_stall_ms"] >= 0.0 and st["bytes_to_peer"][peer] == 2 * sb
+                                    and st["bytes_to_peer"][rank] == 0)
+            ok["debug_status"] = (dbg["world"] == world and len(dbg["slots"]) == 8 and "p2p" in dbg
+                                  and dbg["p2p"]["flags"][peer] == comm.sequence
+                                  and dbg["peer_bytes"][peer] >= 2 * sb and dbg["comm_error"] == "")
             w0 = rng.standard_normal(m).astype(np.float32)
             ref_w, _ = O.sgd(w0, ref[:m], 0.5)
             for defer in (False, True):

@@ -6,7 +6,9 @@ other stream that runs all-reduce work (RCCL collectives, BFP reduce / SGD kerne
 the steady-state window (after the first ``--skip`` fraction of the trace):
 
 * comm busy time, and the part of it that ran while a compute kernel was running (overlapped);
-* compute busy time and the whole window, so exposed-comm = comm busy - overlapped.
+* compute busy time and the whole window, so exposed-comm = comm busy - overlapped;
+* the exposed stretches themselves (comm running while no compute kernel runs): their count, the longest, and the
+  median — at world > 1 the per-step communication tail after the last backward GEMM is one such stretch per step.
 
 Usage: python tools/overlap_report.py gpurun_out/prof_x/run_kernel_trace.csv [--skip 0.3] [--json out.json]
 """
@@ -46,6 +48,25 @@ def _intersect(a, b):
     return out
 
 
+def _subtract(a, b):
+    """Intervals of a not covered by b (both sorted, disjoint)."""
+    out = []
+    j = 0
+    for s, e in a:
+        cur = s
+        while j < len(b) and b[j][1] <= cur:
+            j += 1
+        k = j
+        while k < len(b) and b[k][0] < e:
+            if b[k][0] > cur:
+                out.append((cur, b[k][0]))
+            cur = max(cur, b[k][1])
+            k += 1
+        if cur < e:
+            out.append((cur, e))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -63,6 +84,7 @@ def main():
     comm_names = sorted({n.split("(")[0][-60:] for _, _, st, n in ks if st not in gemm_streams})
     win = max(k[1] for k in ks) - min(k[0] for k in ks)
     ov = _intersect(compute, comm)
+    exposed = sorted((e - s for s, e in _subtract(comm, compute) if e - s > 1000), reverse=True)  # > 1 us
     rep = {
         "window_us": win / 1e3,
         "compute_busy_us": _length(compute) / 1e3,
@@ -70,6 +92,9 @@ def main():
         "comm_overlapped_us": ov / 1e3,
         "comm_exposed_us": (_length(comm) - ov) / 1e3,
         "overlap_fraction_of_comm": (ov / _length(comm)) if comm else 0.0,
+        "exposed_stretches_over_1us": len(exposed),
+        "exposed_stretch_max_us": exposed[0] / 1e3 if exposed else 0.0,
+        "exposed_stretch_median_us": exposed[len(exposed) // 2] / 1e3 if exposed else 0.0,
         "compute_streams": sorted(gemm_streams),
         "comm_kernels": comm_names[:20],
     }
