@@ -19,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "comm/fault_spec.h"
 #include "common/hip_common.h"
 
 namespace fan {
@@ -42,11 +43,6 @@ void launch_msg_verify(const uint8_t* rows, size_t row_bytes, size_t row_stride,
 // Fault injection: p[0] ^= 0xFF (flip) or p[bytes - 1] = 0xFF (nan).
 void launch_fault_byte(uint8_t* p, size_t bytes, int kind, hipStream_t s);
 
-struct FaultRule {
-  std::string site;
-  int64_t index;
-  std::string kind;
-};
 
 class FaultInjector {
  public:

@@ -118,19 +118,7 @@ FaultInjector::FaultInjector() {
   if (const char* e = std::getenv("FAN_FAULT")) *this = FaultInjector(e);
 }
 
-FaultInjector::FaultInjector(const std::string& spec) {
-  std::stringstream ss(spec);
-  std::string item;
-  while (std::getline(ss, item, ',')) {
-    if (item.empty()) continue;
-    const size_t a = item.find(':'), b = item.find(':', a == std::string::npos ? a : a + 1);
-    FAN_CHECK(a != std::string::npos && b != std::string::npos, "FAN_FAULT: expected site:index:kind, got " + item);
-    FaultRule r{item.substr(0, a), std::stoll(item.substr(a + 1, b - a - 1)), item.substr(b + 1)};
-    FAN_CHECK(r.kind == "flip" || r.kind == "nan" || r.kind.rfind("delay_ms=", 0) == 0,
-              "FAN_FAULT: unknown fault kind " + r.kind);
-    rules_.push_back(r);
-  }
-}
+FaultInjector::FaultInjector(const std::string& spec) : rules_(parse_fault_spec(spec)) {}
 
 void FaultInjector::maybe_corrupt(const std::string& site, uint8_t* buf, size_t bytes, hipStream_t s) {
   if (rules_.empty()) return;
@@ -141,7 +129,7 @@ void FaultInjector::maybe_corrupt(const std::string& site, uint8_t* buf, size_t 
     else if (r.kind == "nan") launch_fault_byte(buf, bytes, 1, s);
     else {  // delay_ms: the request's producer-side progress stalls (what a slow link looks like to the peers)
       FAN_HIP_CHECK(hipStreamSynchronize(s));
-      std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(std::stod(r.kind.substr(9)) * 1000.0)));
+      std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(r.delay_ms * 1000.0)));
     }
   }
 }

@@ -110,7 +110,42 @@ static void check_orders(int N) {
   if (N == 8) EXPECT(orders.size() == 7, "8 GPUs should give 7 arc-disjoint rings, got %zu", orders.size());
 }
 
+// Rings restricted to a link matrix (links[a * N + b]: a can send to b; topology.link_matrix): every returned
+// order is a Hamiltonian cycle whose arcs all exist, arc-disjoint across rings; with no usable cycle the planner
+// falls back to the identity order.
+static void check_links(int N, const std::vector<char>& links, size_t expect_min) {
+  const auto orders = ring_orders(N, N - 1 > 0 ? N - 1 : 1, &links);
+  EXPECT(!orders.empty(), "N=%d: no order", N);
+  std::set<std::pair<int, int>> arcs;
+  bool identity_only = orders.size() == 1;
+  for (int i = 0; identity_only && i < N; ++i) identity_only = orders[0][i] == i;
+  for (const auto& o : orders) {
+    EXPECT((int)o.size() == N, "order size");
+    std::set<int> seen(o.begin(), o.end());
+    EXPECT((int)seen.size() == N, "order is not a permutation");
+    if (N < 2 || identity_only) continue;
+    for (int i = 0; i < N; ++i) {
+      const int from = o[i], to = o[(i - 1 + N) % N];  // data flows position p -> p-1
+      EXPECT(links[(size_t)from * N + to], "N=%d: ring uses missing link %d->%d", N, from, to);
+      EXPECT(!arcs.count({from, to}), "N=%d: arc %d->%d used twice", N, from, to);
+      arcs.insert({from, to});
+    }
+  }
+  EXPECT(orders.size() >= expect_min, "N=%d: %zu rings, expected >= %zu", N, orders.size(), expect_min);
+}
+
 int main() {
+  for (int N = 2; N <= 9; ++N) {
+    std::vector<char> full((size_t)N * N, 1), ring((size_t)N * N, 0), none((size_t)N * N, 0);
+    for (int a = 0; a < N; ++a) {
+      full[(size_t)a * N + a] = 0;
+      ring[(size_t)a * N + (a + 1) % N] = ring[(size_t)((a + 1) % N) * N + a] = 1;  // a physical bidirectional ring
+    }
+    check_links(N, full, N == 8 ? 7 : 1);
+    check_links(N, ring, 1);
+    check_links(N, none, 1);  // nothing usable: identity fallback
+  }
+
   for (int N = 1; N <= 9; ++N) {
     for (int b = 1; b <= 3; ++b) check_plan(N, b);
     check_orders(N);

@@ -169,3 +169,14 @@ def test_native_missing_peer_times_out():
     L = eng.layout(1024)
     with pytest.raises(RuntimeError, match="timed out"):  # rank 1 never shows up
         eng.allreduce(torch.ones(L.n_pad, device="cuda"), torch.zeros(L.n_pad, device="cuda"), n_valid=1024)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", ["mesh_pack:x:flip", "mesh_pack:0:boom", "ring_send:1:delay_ms=-1", "mesh_pack"])
+def test_native_fault_spec_rejected_up_front(spec):
+    """A malformed FAN_FAULT rule fails when the engine is configured (csrc/comm/fault_spec.cpp), not in the
+    middle of a request; the grammar parser itself runs under ASan/UBSan in test_native_sanitizers.py."""
+    from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce
+
+    with pytest.raises(ValueError, match="FAN_FAULT"):
+        NativeAllReduce(None, codec="bfp_rne", fault=spec)
