@@ -127,8 +127,20 @@ def main(argv=None):
     comm = None
     impl = a.engine if device.type == "cuda" else "python"
     if world > 1 or a.force_dist:
-        transport = NativeTransport(force_collectives=a.force_dist) if (a.transport == "native" and impl == "native") \
-            else TorchDistTransport(force_collectives=a.force_dist)
+        transport = None
+        if a.transport == "native" and impl == "native":
+            try:  # the C++ engine's own RCCL communicator (unique id exchanged over torch.distributed)
+                transport = NativeTransport(force_collectives=a.force_dist)
+            except Exception as e:  # noqa: BLE001 - keep the run measurable on torch.distributed's communicator
+                print(f"[bench] rank {rank}: native communicator failed ({e}); using torch.distributed", file=sys.stderr)
+                a.transport = "torch"
+            if world > 1:  # every rank on the same communicator
+                ok = torch.tensor([0 if transport is None else 1], device=device)
+                torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
+                if int(ok.item()) == 0:
+                    transport, a.transport = None, "torch"
+        if transport is None:
+            transport = TorchDistTransport(force_collectives=a.force_dist)
         if a.transport == "p2p" and device.type == "cuda" and impl == "native":
             comm = make_p2p_comm()
     else:
