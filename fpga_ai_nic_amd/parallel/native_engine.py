@@ -140,6 +140,8 @@ class NativeAllReduce:
 
                 links = topology.link_matrix(self.world)
         self.links = links
+        if os.environ.get("FAN_COMM_PRIORITY"):  # comm / aux stream priority override (-1 high, 0 normal)
+            stream_priority = int(os.environ["FAN_COMM_PRIORITY"])
         self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
                                    compat_owner_fp32, timeout_s, stream_priority, force_comm or side_stream,
                                    self.device.index, -1 if verify is None else int(bool(verify)), int(chunk_elems),
