@@ -166,11 +166,9 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_supported", &gemm_supported);
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);
-  m.def("gemm_set_pingpong", [](bool on) { gemm_main_loop_flag().store(on ? 1 : 0); },
-        "256x256 GEMM tiles: staggered 4-phase main loop (true) or the one-role loop (false)");
   m.def("gemm_set_main_loop", [](int mode) { gemm_main_loop_flag().store(mode); },
-        "256x256 GEMM tiles: 0 one-role, 1 staggered 4-phase, 2 pipelined (4 or 8 waves by layout / K), "
-        "3 pipelined 4-wave, 5 pipelined 8-wave");
+        "256x256 GEMM tiles: 0 one-role, 2 pipelined (4 or 8 waves by layout / K), 3 pipelined 4-wave, "
+        "5 pipelined 8-wave");
   m.def("gemm_main_loop", []() { return gemm_main_loop_flag().load(); });
   m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {
           gemm_set_stamp_buffer(t ? t->data_ptr() : nullptr);

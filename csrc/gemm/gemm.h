@@ -63,7 +63,7 @@ GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm = 0, int t
 bool gemm_bf16_supported(const GemmArgs& a);
 void launch_gemm_bf16(const GemmArgs& a, hipStream_t stream);
 
-// 256x256 tiles: staggered 4-phase main loop (true; env FAN_GEMM_PP=1 starts with true) or the one-role loop.
+// 256x256 tiles: main-loop selection (0 one-role, 2 pipelined by layout / K, 3 pipelined 4-wave, 5 8-wave).
 std::atomic<int>& gemm_main_loop_flag();
 // diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
 void gemm_set_stamp_buffer(void* p);

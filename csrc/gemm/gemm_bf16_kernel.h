@@ -549,195 +549,6 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Staggered 4-phase 256x256 kernel (8 waves = two groups of 4; one wave of each group per SIMD).
-//
-// Waves are arranged as in the one-role 256x256 kernel (2 x 4; wave w owns rows (w>>2)*128.., cols (w&3)*64..,
-// a 128x64 sub-tile), so the epilogue is shared. Each K-tile runs as 4 phases, one per accumulator quadrant
-// (64x32 = 4x2 MFMA tiles x 2 k-steps = 16 MFMAs):
-//   phase 0: quadrant (0,0), reads A rows 0..63 + B cols 0..31 of the wave tile (12 fragments)
-//   phase 1: quadrant (0,1), reads B cols 32..63 (4)      phase 2: quadrant (1,1), reads A rows 64..127 (8)
-//   phase 3: quadrant (1,0), reads nothing
-// One phase = {glds pieces + fragment reads} barrier {lgkmcnt(0); 16 MFMAs} barrier. Group 1 (waves 4..7) runs
-// one barrier behind group 0 (an extra barrier before the loop, matched by one of group 0 after it), so between
-// any two barriers one wave of each SIMD issues MFMAs while its partner reads LDS and issues DMA.
-//
-// LDS: 2 stages x (A 256x64 + B 256x64 bf16) = 128 KiB, K-tile t in stage t&1. Global barrier index: group 0
-// reads phase p before barrier 2p+1 and runs its MFMAs before 2p+2; group 1 uses 2p+2 / 2p+3.
-//  * WAR: K-tile t+1 overwrites the stage of K-tile t-1, whose last reads (phase 2 of t-1, group 1) retired
-//    before barrier 8t-1; the pieces of t+1 are issued in phases 0..2 of t, after barrier 8t at the earliest.
-//  * RAW: K-tile t+1 is first read after barrier 8t+8 (group 0) / 8t+9 (group 1); every wave retires its own
-//    pieces (vmcnt(0)) before it arrives at barrier 8t+8: group 0 after its phase-3 MFMAs, group 1 before its
-//    phase-3 mid barrier. No other vector-memory operation is in flight in the loop.
-// Raw s_barrier only (a __syncthreads() would drain vmcnt); sched_barrier keeps every instruction on its side.
-__device__ __forceinline__ void pp_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// glds instruction i of a K-tile: 0..3 the A tile, 4..7 the B tile (this wave's 1 KiB piece).
-template <bool AK, bool BKC>
-__device__ __forceinline__ void pp_piece(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
-                                         int64_t ldb, int m0, int n0, int k0, char* st, int wave, int lane, int i) {
-  constexpr int GA = OpTile<256, 512>::GLDS;
-  if (i < GA) stage_one<AK, 256, 512>(A, lda, m0, k0, st, wave, lane, i);
-  else stage_one<BKC, 256, 512>(B, ldb, n0, k0, st + OpTile<256, 512>::BYTES, wave, lane, i - GA);
-}
-
-// Quadrant Q of the phase schedule: fragment reads and MFMAs. fa[qm][ks][i]: A fragments of quadrant row qm;
-// fb[qn][ks][j]: B fragments of quadrant column qn (all indices compile-time after unrolling).
-template <int Q, bool AK, bool BKC>
-struct PPPhase {
-  static constexpr int QM = (Q == 0 || Q == 1) ? 0 : 1;
-  static constexpr int QN = (Q == 1 || Q == 2) ? 1 : 0;
-  __device__ static __forceinline__ void read(const char* sa, const char* sb, int wrow, int wcol, int lane,
-                                              s16x8 (&fa)[2][2][4], s16x8 (&fb)[2][2][2]) {
-    if constexpr (Q == 0 || Q == 2) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[QM][ks][i] = read_frag<AK>(sa, wrow + QM * 64 + i * 16, ks, lane);
-    }
-    if constexpr (Q == 0 || Q == 1) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb[QN][ks][j] = read_frag<BKC>(sb, wcol + QN * 32 + j * 16, ks, lane);
-    }
-  }
-  __device__ static __forceinline__ void mfma(f32x4 (&acc)[8][4], const s16x8 (&fa)[2][2][4],
-                                              const s16x8 (&fb)[2][2][2], bool do_colsum, float (&cs)[4]) {
-    if constexpr (Q == 0 || Q == 1) {  // fused bias gradient: each B fragment is read once per K-tile
-      if (do_colsum) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) cs[QN * 2 + j] += frag_sum(fb[QN][ks][j]);
-      }
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[QM * 4 + i][QN * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, fa[QM][ks][i]), __builtin_bit_cast(bf16x8, fb[QN][ks][j]),
-              acc[QM * 4 + i][QN * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-};
-
-template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
-__global__ void __launch_bounds__(512, 2)
-    gemm_pp_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
-                   TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
-                   int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
-                   float* __restrict__ colsum, WireOut wo) {
-  constexpr int BM = 256, BN = 256, NT = 512;
-  constexpr int A_BYTES = OpTile<BM, NT>::BYTES, B_BYTES = OpTile<BN, NT>::BYTES;
-  constexpr int STAGE = A_BYTES + B_BYTES;
-  static_assert(OpTile<BM, NT>::GLDS == 4 && OpTile<BN, NT>::GLDS == 4, "8 glds pieces per K-tile");
-  constexpr int WTM = 128, WTN = 64;
-  constexpr int MI = WTM / 16, NJ = WTN / 16;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tiles_n = N / BN;
-  const int tiles = (M / BM) * tiles_n;
-  const int nwg = tiles * split_k;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tile = wg % tiles;
-  const int ksplit = wg / tiles;
-  const int tiles_m = M / BM;
-  const int GM = tiles_m >= 4 ? 4 : tiles_m;
-  const int gr = tile / (GM * tiles_n);
-  const int gm = (tiles_m - gr * GM) < GM ? (tiles_m - gr * GM) : GM;
-  const int in_grp = tile % (GM * tiles_n);
-  const int m0 = (gr * GM + in_grp % gm) * BM;
-  const int n0 = (in_grp / gm) * BN;
-  const int k_per = K / split_k;
-  const int kbeg = ksplit * k_per;
-  const int nk = k_per / BK;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = wave >> 2;
-  const int wrow = grp * WTM;         // wave sub-tile origin inside the block tile
-  const int wcol = (wave & 3) * WTN;
-  const bool do_colsum = !BKC && colsum != nullptr && m0 == 0 && grp == 0;
-  float cs[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
-
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 fa[2][2][4], fb[2][2][2];
-
-  // prologue: K-tile 0, every wave its pieces; then the one-barrier stagger of group 1
-#pragma unroll
-  for (int i = 0; i < 8; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, kbeg, smem, wave, lane, i);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  pp_barrier();
-  if (grp == 1) pp_barrier();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* sa = smem + (kt & 1) * STAGE;
-    const char* sb = sa + A_BYTES;
-    char* nst = smem + ((kt + 1) & 1) * STAGE;
-    const bool pf = kt + 1 < nk;
-    const int k1 = kbeg + (kt + 1) * BK;
-    // phase 0: pieces 0..2 of K-tile kt+1, A rows 0..63 + B cols 0..31 of kt
-    if (pf) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, k1, nst, wave, lane, i);
-    }
-    PPPhase<0, AK, BKC>::read(sa, sb, wrow, wcol, lane, fa, fb);
-    pp_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    PPPhase<0, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
-    pp_barrier();
-    // phase 1: pieces 3..5, B cols 32..63
-    if (pf) {
-#pragma unroll
-      for (int i = 3; i < 6; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, k1, nst, wave, lane, i);
-    }
-    PPPhase<1, AK, BKC>::read(sa, sb, wrow, wcol, lane, fa, fb);
-    pp_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    PPPhase<1, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
-    pp_barrier();
-    // phase 2: pieces 6..7, A rows 64..127
-    if (pf) {
-#pragma unroll
-      for (int i = 6; i < 8; ++i) pp_piece<AK, BKC>(A, lda, B, ldb, m0, n0, k1, nst, wave, lane, i);
-    }
-    PPPhase<2, AK, BKC>::read(sa, sb, wrow, wcol, lane, fa, fb);
-    pp_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    PPPhase<2, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
-    pp_barrier();
-    // phase 3: no reads; retire this wave's pieces of kt+1 before barrier 8kt+8 (see the header)
-    if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
-    PPPhase<3, AK, BKC>::mfma(acc, fa, fb, do_colsum, cs);
-    if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
-  }
-  if (grp == 0) pp_barrier();  // match group 1's stagger barrier
-  __syncthreads();             // every operand read retired before the epilogue reuses the LDS
-
-  if (do_colsum)
-    colsum_finish<NJ, WTN, EPI, SPLIT>(cs, lane, n0 + wcol, SPLIT ? ws + (int64_t)split_k * M * N + (int64_t)ksplit * N
-                                                                   : colsum, wo, N);
-  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wrow, n0 + wcol, C, ldc, bias, aux,
-                                                 ldaux, M, N, ksplit, ws, wo);
-}
-
-// ---------------------------------------------------------------------------------------------------------------
 // Software-pipelined 256x256 kernel (8 waves, 2x4, 128x64 per wave) for the K-contiguous-A layouts.
 //
 // The one-role loop runs each K-tile as barrier -> DMA burst -> fragment reads -> MFMAs, with every wave in the same
@@ -1214,8 +1025,10 @@ constexpr int lds_bytes() {
   return ((3 * st <= 160 * 1024) ? 3 : 2) * st;
 }
 
-// 256x256 main loop selection (gemm_main_loop_flag(): 0 one-role, 1 staggered, 2 pipelined (4 or 8 waves by
-// layout / K), 3 pipelined 4-wave, 5 pipelined 8-wave), read per launch so A/B comparisons run in one process.
+// 256x256 main loop selection (gemm_main_loop_flag(): 0 one-role, 2 pipelined (4 or 8 waves by layout / K),
+// 3 pipelined 4-wave, 5 pipelined 8-wave), read per launch so A/B comparisons run in one process. (A staggered
+// two-group loop, mode 1 in round 1, measured within ±5 % of the one-role loop and was removed:
+// profiles/r1_gemm_experiments.md.)
 inline int main_loop_mode() { return gemm_main_loop_flag().load(std::memory_order_relaxed); }
 
 // Launches the main loop; returns the number of bias-gradient partial slabs it left in the workspace for an ordered
@@ -1224,7 +1037,7 @@ template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename T
 int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
   const int grid = cdiv_i(a.M, BM) * cdiv_i(a.N, BN) * sk;
   if constexpr (BM == 256 && BN == 256 && WM * WN == 8) {
-    // the staggered and pipelined loops have no edge path: aligned shapes only
+    // the pipelined loops have no edge path: aligned shapes only
     const int mode = main_loop_mode();
     const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
     // pipelined loops: 4 waves (128x128 per wave, AGPR accumulators) where they measured faster — an MN-contiguous
@@ -1265,15 +1078,6 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
       }
       launch(gemm_pl_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>);
       return 0;
-    }
-    if (mode == 1 && aligned) {
-      constexpr int lds = 2 * (BM + BN) * BK * 2;
-      auto k = gemm_pp_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT>;
-      FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-      hipLaunchKernelGGL(k, grid, 512, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc,
-                         (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
-                         a.colsum, wo);
-      return SPLIT && a.colsum ? sk : 0;
     }
   }
   constexpr int lds = lds_bytes<BM, BN>();

@@ -1,0 +1,9 @@
+// bf16 GEMM instantiations for A K-contiguous, B K-contiguous: 256x256 tiles (one-role, pipelined 8-wave and 4-wave
+// main loops).
+#include "gemm/gemm_bf16_kernel.h"
+
+namespace fan {
+namespace gemm_detail {
+template void launch_epi<256, 256, 2, 4, true, true>(const GemmArgs&, int, hipStream_t);
+}  // namespace gemm_detail
+}  // namespace fan

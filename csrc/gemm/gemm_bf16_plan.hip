@@ -31,12 +31,11 @@ extern template void launch_tile<true, true>(const GemmArgs&, int, int, int, int
 
 std::atomic<int>& gemm_main_loop_flag() {
   // 256x256 main loop (aligned shapes): 2 software-pipelined, 4 or 8 waves by layout / K (default), 0 one-role
-  // loop (FAN_GEMM_PL=0), 1 staggered 4-phase (FAN_GEMM_PP=1), 3 / 5 pipelined 4-wave / 8-wave only. The others stay selectable for in-process A/B (gemm_set_main_loop).
+  // loop (FAN_GEMM_PL=0), 3 / 5 pipelined 4-wave / 8-wave only. Selectable for in-process A/B (gemm_set_main_loop).
   static std::atomic<int> flag{[] {
-    const char* e = getenv("FAN_GEMM_PP");
-    if (e && e[0] == '1') return 1;
     const char* pl = getenv("FAN_GEMM_PL");
-    return pl && pl[0] >= '0' && pl[0] <= '5' ? pl[0] - '0' : 2;
+    const int m = pl && pl[0] >= '0' && pl[0] <= '5' ? pl[0] - '0' : 2;
+    return m == 1 || m == 4 ? 2 : m;
   }()};
   return flag;
 }
