@@ -781,18 +781,21 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false>
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256>
 __global__ void __launch_bounds__(256, 1)
     gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
                     float* __restrict__ colsum, WireOut wo) {
-  constexpr int BM = 256, BN = 256, NT = 256;
+  constexpr int BM = 256, BN = BN_, NT = 256;
   constexpr int A_BYTES = OpTile<BM, NT>::BYTES;
   constexpr int STAGE = A_BYTES + OpTile<BN, NT>::BYTES;
-  constexpr int GA = OpTile<BM, NT>::GLDS, G = GA + OpTile<BN, NT>::GLDS;  // 8 + 8 pieces per wave and K-tile
-  constexpr int WTM = 128, WTN = 128, MI = 8, NJ = 8;
-  static_assert(G == 16, "16 glds pieces per wave and K-tile");
+  constexpr int GA = OpTile<BM, NT>::GLDS, G = GA + OpTile<BN, NT>::GLDS;  // 8 + 8 (BN 128: 8 + 4) pieces per wave
+  constexpr int WTM = 128, WTN = BN / 2, MI = 8, NJ = WTN / 16;
+  constexpr int Q = MI * NJ, R = MI + NJ;  // MFMAs and fragment reads per k-step and wave
+  constexpr int RSP = (Q * 3 / 4) / R, DSP = Q / G;  // read / DMA spacing in MFMAs (64 MFMAs: 3 / 4; 32: 2 / 2)
+  static_assert(BN == 256 || BN == 128, "256x256 or 256x128 tiles");
+  static_assert(RSP >= 1 && DSP >= 1 && G * DSP <= Q, "schedule");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
@@ -838,21 +841,21 @@ __global__ void __launch_bounds__(256, 1)
   const char* b_k0 = reinterpret_cast<const char*>(B) + (BKC ? (int64_t)kbeg * 2 : (int64_t)kbeg * ldb * 2);
   const uint32_t lds0 = lds_addr_of(smem);
 
-  // glds piece p (0..15) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
+  // glds piece p (0..G-1) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
   // the accumulator array in scratch memory)
   auto piece = [&](int kt, int p) __attribute__((always_inline)) {
     const uint32_t st = lds0 + (kt & 1) * STAGE + wave * 1024;
     if (p < GA) glds16_s(a_k0 + kt * a_step, off[p], st + p * OpTile<BM, NT>::IB);
     else glds16_s(b_k0 + kt * b_step, off[p], st + A_BYTES + (p - GA) * OpTile<BN, NT>::IB);
   };
-  // next k-step's fragment r (0..15: A rows 0..7, then B columns 0..7) into set `set`
+  // next k-step's fragment r (0..R-1: A rows 0..7, then B columns 0..NJ-1) into set `set`
   auto read_next = [&](const char* st, int ks, int set, int r) __attribute__((always_inline)) {
     if (r < MI) fa[set][r] = read_frag<AK>(st, wm * WTM + r * 16, ks, lane);
     else fb[set][r - MI] = read_frag<BKC>(st + A_BYTES, wn * WTN + (r - MI) * 16, ks, lane);
   };
-  // One k-step: 64 MFMAs on set `cur`; READ: the 16 fragments of the next k-step into set cur ^ 1, one per 3
-  // MFMAs from the start (all issued by MFMA 48: the barrier's lgkmcnt(0) after k-step 0 then waits on nothing
-  // young); DMA: the 16 pieces of K-tile dma_kt, one per 4 MFMAs.
+  // One k-step: Q MFMAs on set `cur`; READ: the R fragments of the next k-step into set cur ^ 1, one per RSP
+  // MFMAs from the start (all issued by 3/4 of the block: the barrier's lgkmcnt(0) after k-step 0 then waits on
+  // nothing young); DMA: the G pieces of K-tile dma_kt, one per DSP MFMAs.
   auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int rd_ks, int dma_kt,
                    bool csk) __attribute__((always_inline)) {
     constexpr int cur = decltype(cur_c)::value;
@@ -861,8 +864,8 @@ __global__ void __launch_bounds__(256, 1)
       static_for<NJ>([&](auto jc) __attribute__((always_inline)) { cs[jc.value] += frag_sum(fb[cur][jc.value]); });
     static_for<MI * NJ>([&](auto qc) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
-      if constexpr (READ && q % 3 == 0 && q / 3 < MI + NJ) read_next(rd_st, rd_ks, cur ^ 1, q / 3);
-      if constexpr (DMA && q % 4 == 1) piece(dma_kt, q / 4);
+      if constexpr (READ && q % RSP == 0 && q / RSP < R) read_next(rd_st, rd_ks, cur ^ 1, q / RSP);
+      if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_kt, q / DSP);
       mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
     });
   };
@@ -883,7 +886,7 @@ __global__ void __launch_bounds__(256, 1)
   }
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int r = 0; r < MI + NJ; ++r) read_next(smem, 0, 0, r);
+  for (int r = 0; r < R; ++r) read_next(smem, 0, 0, r);
 
   auto ktile = [&](int kt, auto more_c, auto more2_c) __attribute__((always_inline)) {
     const char* st = smem + (kt & 1) * STAGE;
@@ -1077,6 +1080,29 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
         }
       }
       launch(gemm_pl_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>);
+      return 0;
+    }
+  }
+  if constexpr (BM == 256 && BN == 128) {
+    // 256x128 tiles (grids that 256x256 tiles leave half empty, e.g. an 8192x1024 output): the 4-wave pipelined
+    // loop with 128x64 per wave
+    const int mode = main_loop_mode();
+    const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
+    if ((mode == 2 || mode == 3) && aligned && (!a.colsum || a.workspace) && !(EPI == kEpiWire && !SPLIT)) {
+      constexpr int lds = 2 * (BM + BN) * BK * 2;
+      auto launch = [&](auto k) {
+        FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        hipLaunchKernelGGL(k, grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
+                           a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
+                           (float*)a.workspace, a.colsum, wo);
+      };
+      if constexpr (!BKC) {
+        if (a.colsum) {
+          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true, 128>);
+          return SPLIT ? sk : a.M / BM;
+        }
+      }
+      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false, 128>);
       return 0;
     }
   }

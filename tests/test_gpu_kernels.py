@@ -243,6 +243,30 @@ def test_gemm_256_tile_all_layouts_and_k(C, main_loop, K):
                 assert bool((err <= bound).all()), f"a_t={a_t} b_t={b_t} split_k={sk}: max err {err.max().item()}"
 
 
+@pytest.mark.parametrize("K", [64, 192, 2048])
+def test_gemm_256x128_tile_all_layouts(C, main_loop, K):
+    """256x128 tiles (the 4-wave pipelined loop with 128x64 per wave under the default selection) on all four
+    operand layouts, with and without split-K and the fused bias gradient: vs an fp64 reference."""
+    torch.manual_seed(K + 1)
+    M, N = 512, 384
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    Bkn = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    ref = _ref_mm(A.float(), Bkn.float())
+    bound = _elem_bound(A.float(), Bkn.float())
+    for a_t in (False, True):
+        for b_t in (False, True):
+            Ain = A.t().contiguous() if a_t else A
+            Bin = Bkn.t().contiguous() if b_t else Bkn
+            for sk in (1, 3) if K % 192 == 0 else (1,):
+                Cout = torch.full((M, N), float("nan"), device=DEV)
+                cs = torch.full((N,), float("nan"), device=DEV) if (a_t and not b_t) else None
+                G.gemm(Ain, a_t, Bin, b_t, Cout, split_k=sk, tile=(256, 128), colsum=cs)
+                err = (Cout.double() - ref).abs()
+                assert bool((err <= bound).all()), f"a_t={a_t} b_t={b_t} split_k={sk}: max err {err.max().item()}"
+                if cs is not None:  # column sums of B over K (the bias gradient of the bwd-weight layout)
+                    assert (cs.double() - Bkn.double().sum(0)).abs().max().item() < 1e-3 * K ** 0.5
+
+
 def test_gemm_256_tile_epilogues(C, main_loop):
     torch.manual_seed(9)
     M, N, K = 512, 512, 768

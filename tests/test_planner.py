@@ -79,7 +79,7 @@ def test_gemm_plans_for_workload_shapes():
     C = _ext.require()
     expect = {
         (8192, 4096, 4096): (256, 256, 1),   # fwd1 / bwd-data 1: 512 tiles
-        (8192, 1024, 4096): (128, 256, 1),   # fwd2: 256 tiles
+        (8192, 1024, 4096): (256, 128, 1),   # fwd2: 256 tiles (4-wave pipelined loop)
         (4096, 4096, 8192): (256, 256, 1),   # bwd-weight 1
         (4096, 1024, 8192): (256, 256, 4),   # bwd-weight 2: 64 tiles x split 4
         (1024, 4096, 8192): (256, 256, 4),   # bwd-weight 0
