@@ -314,8 +314,32 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   constexpr int C4 = WTN / 4;   // float4 chunks per staged row
   constexpr int RPI = 64 / C4;  // rows covered per pass by the wave
+  // ReLU-mask epilogue: the activation reads are latency-bound (64 MB over a 190 us GEMM is no bandwidth), so the
+  // loads of 16-row block i + kPf are issued before block i is staged and stored; each lane keeps kPf + 1 blocks
+  // of 4-element activation chunks in registers (bwd-data 8192x4096: 19 us of exposed load latency otherwise).
+  constexpr bool kPfAux = EPI == kEpiReluMask && !SPLIT;
+  constexpr int kPf = 2;
+  constexpr int NP = 16 / RPI;
+  using AuxV = typename std::conditional<sizeof(TC) == 2, uint2, uint4>::type;
+  AuxV aq[kPfAux ? MI : 1][kPfAux ? NP : 1];
+  auto aux_load = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+    for (int pass = 0; pass < NP; ++pass) {
+      const int row = row0 + i * 16 + pass * RPI + lane / C4;
+      const int col = col0 + (lane % C4) * 4;
+      if (!mn_edge || (row < M && col < N))
+        aq[i][pass] = *reinterpret_cast<const AuxV*>(aux + (int64_t)row * ldaux + col);
+    }
+  };
+  if constexpr (kPfAux) {
+#pragma unroll
+    for (int i = 0; i < kPf && i < MI; ++i) aux_load(i);
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
+    if constexpr (kPfAux) {
+      if (i + kPf < MI) aux_load(i + kPf);
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
@@ -355,6 +379,20 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
       if (SPLIT) {
         float* slab = ws + (int64_t)ksplit * M * N;
         *reinterpret_cast<float4*>(slab + (int64_t)row * N + col) = q;
+      } else if constexpr (kPfAux) {
+        float m[4];
+        if constexpr (sizeof(TC) == 2) {
+          const uint2 u = aq[i][pass];
+          m[0] = __uint_as_float(u.x << 16); m[1] = __uint_as_float(u.x & 0xFFFF0000u);
+          m[2] = __uint_as_float(u.y << 16); m[3] = __uint_as_float(u.y & 0xFFFF0000u);
+        } else {
+          const uint4 u = aq[i][pass];
+          m[0] = __uint_as_float(u.x); m[1] = __uint_as_float(u.y);
+          m[2] = __uint_as_float(u.z); m[3] = __uint_as_float(u.w);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = m[u] > 0.f ? v[u] : 0.f;
+        epi4<kEpiNone, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
       } else {
         epi4<EPI, TC, ACCUM>(v, C, ldc, bias, aux, ldaux, row, col);
       }

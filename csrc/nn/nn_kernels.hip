@@ -66,6 +66,63 @@ __device__ __forceinline__ void st1(T* p, float v) {
   else *reinterpret_cast<bf16_t*>(p) = f32_to_bf16(v);
 }
 
+// Rows of up to NCH * 512 classes (C, ld, ldd % 8 == 0): the row stays in registers (8 * NCH values per lane), so
+// the logits are read from memory once, every chunk's load is in flight before the first max, and each exp is
+// computed once (the flagship's 8192 x 1024 f32 logits: one 32 MB read + the 16 MB dlogits write).
+template <typename TIN, typename TOUT, int NCH>
+__global__ void __launch_bounds__(256)
+    softmax_xent_reg_kernel(const TIN* __restrict__ logits, int64_t ld, const int32_t* __restrict__ labels,
+                            TOUT* __restrict__ dlogits, int64_t ldd, float* __restrict__ loss_rows, int M, int C,
+                            float grad_scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const TIN* x = logits + (int64_t)row * ld;
+  const int lab = labels[row];
+  float v[NCH][8];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < C) {
+      ld8<TIN>(x + c, v[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = -INFINITY;
+    }
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, v[k][j]);
+  const float gm = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[k][j] = __expf(v[k][j] - gm);  // -inf padding -> 0
+      s += v[k][j];
+    }
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  if (lane == 0) {
+    const float xl = sizeof(TIN) == 4 ? reinterpret_cast<const float*>(x)[lab]
+                                      : bf16_to_f32(reinterpret_cast<const bf16_t*>(x)[lab]);
+    loss_rows[row] = gm + __logf(s) - xl;
+  }
+  TOUT* d = dlogits + (int64_t)row * ldd;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c >= C) continue;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (v[k][j] * inv - (c + j == lab ? 1.f : 0.f)) * grad_scale;
+    st8<TOUT>(d + c, o);
+  }
+}
+
 // One wave per row; 4 waves per block. VEC: 8 values per lane access (C, ld, ldd % 8 == 0); otherwise one value
 // per lane access (any class count, e.g. a 10-class head).
 template <typename TIN, typename TOUT, bool VEC>
@@ -186,8 +243,14 @@ void launch_softmax_xent(int in_dtype, const void* logits, int64_t ld, const int
   FAN_CHECK(C > 0, "softmax_xent needs C > 0");
   const int grid = (M + 3) / 4;
   const bool vec = C % 8 == 0 && ld % 8 == 0 && ldd % 8 == 0;
+  const int nch = vec ? (C + 511) / 512 : 0;
 #define FAN_SMX(TI, TO)                                                                                         \
-  if (vec)                                                                                                      \
+  if (nch >= 1 && nch <= 4) {                                                                                   \
+    auto k = nch == 1 ? softmax_xent_reg_kernel<TI, TO, 1> : nch == 2 ? softmax_xent_reg_kernel<TI, TO, 2>      \
+           : nch == 3 ? softmax_xent_reg_kernel<TI, TO, 3> : softmax_xent_reg_kernel<TI, TO, 4>;                \
+    hipLaunchKernelGGL(k, grid, 256, 0, s, (const TI*)logits, ld, labels, (TO*)dlogits, ldd, loss_rows, M, C,   \
+                       grad_scale);                                                                             \
+  } else if (vec)                                                                                               \
     hipLaunchKernelGGL((softmax_xent_kernel<TI, TO, true>), grid, 256, 0, s, (const TI*)logits, ld, labels,     \
                        (TO*)dlogits, ldd, loss_rows, M, C, grad_scale);                                          \
   else                                                                                                          \

@@ -170,9 +170,11 @@ def test_gemm_epilogues_and_splitk(C):
 
 @pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.bfloat16), (torch.float32, torch.float32),
                                           (torch.bfloat16, torch.bfloat16)])
-def test_softmax_xent(C, in_dt, out_dt):
+@pytest.mark.parametrize("Cc", [1024, 8, 1544, 2048, 4096])
+def test_softmax_xent(C, in_dt, out_dt, Cc):
+    """Register-resident rows (C <= 2048, C % 8 == 0; partial last chunk at 1544) and the streaming kernel."""
     torch.manual_seed(2)
-    M, Cc = 300, 1024
+    M = 300
     x = (torch.randn(M, Cc, device=DEV) * 3).to(in_dt)
     y = torch.randint(0, Cc, (M,), device=DEV, dtype=torch.int32)
     d = torch.empty(M, Cc, device=DEV, dtype=out_dt)
