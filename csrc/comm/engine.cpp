@@ -60,6 +60,7 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     if (!std::strcmp(f, "system")) evf |= hipEventReleaseToSystem;
     else if (!std::strcmp(f, "device")) evf |= hipEventReleaseToDevice;
   }
+  if (const char* ld = std::getenv("FAN_LAZY_DONE")) lazy_done_ = ld[0] != '0';
   const char* ve = std::getenv("FAN_VERIFY");
   verify_ = cfg.verify >= 0 ? cfg.verify > 0 : (ve && ve[0] == '1');
   if (verify_) {
@@ -85,6 +86,7 @@ AllReduceEngine::~AllReduceEngine() {
   for (auto& row : cev_)
     for (auto& e : row) hipEventDestroy(e);
   for (auto& s : slots_) {
+    if (s.done_lazy) hipEventRecord(s.done, s.epi_stream);
     hipEventSynchronize(s.done);  // epilogues may have run on a producer stream and still read the scratch
     hipEventDestroy(s.ready);
     hipEventDestroy(s.update);
@@ -650,7 +652,8 @@ void AllReduceEngine::commit_slot(Slot& sl, int slot, bool after_producer, hipSt
   // producer) skip the extra packet there: their completion is the done event.
   if (sl.epi_stream == sl.stream && !inline_)
     FAN_HIP_CHECK(hipStreamWriteValue32(sl.stream, flags_dev_ + slot * 16, sl.seq, 0));
-  FAN_HIP_CHECK(hipEventRecord(sl.done, sl.epi_stream));
+  sl.done_lazy = lazy_done_ && inline_ && sl.epi_stream == sl.stream && !sl.timed && sl.trace < 0;
+  if (!sl.done_lazy) FAN_HIP_CHECK(hipEventRecord(sl.done, sl.epi_stream));
   sl.pending = false;
 }
 
@@ -661,11 +664,15 @@ void AllReduceEngine::wait_stream(int slot, hipStream_t s, uint32_t seq) {
   // later in every stream order the old request shares (a conservative wait). Never commit the newer one here.
   const bool own = seq == 0 || seq == sl.seq;
   if (own && sl.pending) commit_slot(sl, slot, true, s);
-  if (s != sl.epi_stream || !own) FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
+  if (s != sl.epi_stream || !own) {
+    ensure_done(sl);
+    FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
+  }
 }
 
 bool AllReduceEngine::query(int slot, uint32_t seq) {
-  const Slot& sl = slots_.at(slot);
+  Slot& sl = slots_.at(slot);
+  ensure_done(sl);  // a lazily recorded done event (this request's, or a superseded one's: conservative)
   if (seq != 0 && seq != sl.seq) {
     // superseded request: its completion is the slot's done event while the newer request is pending, and is
     // implied by the done word / done event of the newer one otherwise

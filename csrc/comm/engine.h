@@ -183,7 +183,18 @@ class AllReduceEngine {
     std::vector<EpiThunk> thunks;
     double t_issue = 0.0;
     int trace = -1;  // index into trace_pool_ (-1: not traced)
+    bool done_lazy = false;  // inline request: `done` is recorded only when a host query / other stream needs it
   };
+  // Inline requests complete in their producer's stream order, so nothing needs their done event unless the host
+  // polls it or another stream waits on it: record it then (later in that stream = a conservative completion point).
+  // An event marker after every inline epilogue left the GPU idle ~5.5 us before the next GEMM (3x per step,
+  // profiles/r2_lazy_done_event.txt).
+  void ensure_done(Slot& sl) {
+    if (!sl.done_lazy) return;
+    FAN_HIP_CHECK(hipEventRecord(sl.done, sl.epi_stream));
+    sl.done_lazy = false;
+  }
+  bool lazy_done_ = true;  // FAN_LAZY_DONE=0: record every request's done event at commit
   struct RequestTrace {
     hipEvent_t ev[kTpCount] = {};
     int64_t logical_bytes = 0, wire_bytes = 0;
