@@ -1085,7 +1085,10 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     // B, or a long K — else 8 waves: the 4-wave epilogue runs on half the waves (bwd-data at K 1024: 77 vs 70 us;
     // the in-kernel wire encode: bwd-weight 4096^2 +13 vs +7 us, profiles/r1_gemm_experiments.md); modes 3 / 5
     // force one of them
-    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192) && !(EPI == kEpiWire && !SPLIT));
+    // (the MLP's bwd-data with the ReLU-mask epilogue, activation loads prefetched: 4 waves 197 vs 200 us at
+    // 8192x4096x4096, 67.9 vs 68.5 at K 1024, profiles/r2_gemm_loops_bwdd.jsonl)
+    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192 || EPI == kEpiReluMask) &&
+                                   !(EPI == kEpiWire && !SPLIT));
     if (pl4 && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto launch = [&](auto k) {
