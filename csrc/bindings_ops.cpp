@@ -170,6 +170,9 @@ void register_gemm(pybind11::module_& m) {
         "256x256 GEMM tiles: 0 one-role, 2 pipelined (4 or 8 waves by layout / K), 3 pipelined 4-wave, "
         "5 pipelined 8-wave");
   m.def("gemm_main_loop", []() { return gemm_main_loop_flag().load(); });
+  m.def("gemm_set_persist", [](int cap) { gemm_persist_flag().store(cap); },
+        "grid cap of the persistent 4-wave GEMM kernel (<= 0: one workgroup per tile)");
+  m.def("gemm_persist", []() { return gemm_persist_flag().load(); });
   m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {
           gemm_set_stamp_buffer(t ? t->data_ptr() : nullptr);
         },

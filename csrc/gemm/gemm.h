@@ -65,6 +65,9 @@ void launch_gemm_bf16(const GemmArgs& a, hipStream_t stream);
 
 // 256x256 tiles: main-loop selection (0 one-role, 2 pipelined by layout / K, 3 pipelined 4-wave, 5 8-wave).
 std::atomic<int>& gemm_main_loop_flag();
+// grid cap of the persistent 4-wave pipelined kernel (FAN_GEMM_PERSIST, default 256 = one workgroup per CU; 0: one
+// workgroup per tile); settable for in-process A/B and for tests that force several tiles per workgroup
+std::atomic<int>& gemm_persist_flag();
 // diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
 void gemm_set_stamp_buffer(void* p);
 void* gemm_stamp_buffer();

@@ -317,7 +317,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
   // ReLU-mask epilogue: the activation reads are latency-bound (64 MB over a 190 us GEMM is no bandwidth), so the
   // loads of 16-row block i + kPf are issued before block i is staged and stored; each lane keeps kPf + 1 blocks
   // of 4-element activation chunks in registers (bwd-data 8192x4096: 19 us of exposed load latency otherwise).
-  constexpr bool kPfAux = EPI == kEpiReluMask && !SPLIT;
+  constexpr bool kPfAux = EPI == kEpiReluMask && !SPLIT && sizeof(TC) == 2;  // (f32 chunks: too many registers)
   constexpr int kPf = 2;
   constexpr int NP = 16 / RPI;
   using AuxV = typename std::conditional<sizeof(TC) == 2, uint2, uint4>::type;
@@ -837,7 +837,17 @@ __global__ void __launch_bounds__(256, 1)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
-  const int wg = xcd_remap(blockIdx.x, tiles * split_k);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / 2, wn = wave % 2;
+  const uint32_t lds0 = lds_addr_of(smem);
+  // Persistent over its tiles when the grid is smaller than the tile count (one workgroup per CU, grid a multiple
+  // of the XCD count, so virtual block v = blockIdx.x + i * gridDim.x stays on blockIdx.x's XCD): a workgroup's
+  // next tile starts its operand DMA while the previous tile's epilogue stores drain, instead of a new workgroup
+  // waiting for the old one to retire (the 2-round grids: 8192x4096 forward and bwd-data). Not with the fused
+  // bias gradient: its extra live registers would spill in the loop (the launcher gives it one tile per workgroup).
+  auto tile_body = [&](int v) __attribute__((always_inline)) {
+  const int wg = xcd_remap(v, tiles * split_k);
   const int tile = wg % tiles, ksplit = wg / tiles;
   const int GM = tiles_m >= 4 ? 4 : tiles_m;
   const int grp = tile / (GM * tiles_n);
@@ -849,9 +859,6 @@ __global__ void __launch_bounds__(256, 1)
   const int kbeg = ksplit * k_per;
   const int nk = k_per / BK;
 
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / 2, wn = wave % 2;
   // fused bias gradient: as gemm_pl_kernel (waves wm == 0; spread over the tile rows without split-K)
   const int im = SPLIT ? 0 : m0 / BM;
   const int cs0 = SPLIT ? (m0 == 0 ? 0 : nk) : im * nk / tiles_m;
@@ -877,7 +884,6 @@ __global__ void __launch_bounds__(256, 1)
   const int64_t b_step = BKC ? (int64_t)BK * 2 : (int64_t)BK * ldb * 2;
   const char* a_k0 = reinterpret_cast<const char*>(A) + (AK ? (int64_t)kbeg * 2 : (int64_t)kbeg * lda * 2);
   const char* b_k0 = reinterpret_cast<const char*>(B) + (BKC ? (int64_t)kbeg * 2 : (int64_t)kbeg * ldb * 2);
-  const uint32_t lds0 = lds_addr_of(smem);
 
   // glds piece p (0..G-1) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
   // the accumulator array in scratch memory)
@@ -958,6 +964,15 @@ __global__ void __launch_bounds__(256, 1)
   __syncthreads();  // every operand read retired before the epilogue reuses the LDS
   store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
                                                  aux, ldaux, M, N, ksplit, ws, wo);
+  };
+  if constexpr (COLSUM) {
+    tile_body(blockIdx.x);
+  } else {
+    for (int v = blockIdx.x; v < tiles * split_k; v += gridDim.x) {
+      tile_body(v);
+      __syncthreads();  // every wave's staging reads done before the next tile's DMA overwrites the LDS
+    }
+  }
 }
 
 // Ordered split-K reduction + epilogue (deterministic: slabs summed in split order).
@@ -1071,6 +1086,11 @@ constexpr int lds_bytes() {
 // two-group loop, mode 1 in round 1, measured within ±5 % of the one-role loop and was removed:
 // profiles/r1_gemm_experiments.md.)
 inline int main_loop_mode() { return gemm_main_loop_flag().load(std::memory_order_relaxed); }
+// grid of the persistent 4-wave kernel: at most gemm_persist_flag() workgroups (<= 0: one per tile)
+inline int persist_grid(int grid) {
+  const int cap = gemm_persist_flag().load(std::memory_order_relaxed);
+  return cap > 0 && grid > cap ? cap : grid;
+}
 
 // Launches the main loop; returns the number of bias-gradient partial slabs it left in the workspace for an ordered
 // reduce (split_k with split-K; without: the pipelined loop's tile rows, 0 = colsum written by the kernel).
@@ -1091,19 +1111,19 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
                                    !(EPI == kEpiWire && !SPLIT));
     if (pl4 && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
-      auto launch = [&](auto k) {
+      auto launch = [&](auto k, bool persist) {  // persist: the kernel loops over tiles (not with colsum)
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        hipLaunchKernelGGL(k, grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
-                           a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
+        hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
+                           (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
                            (float*)a.workspace, a.colsum, wo);
       };
       if constexpr (!BKC) {
         if (a.colsum) {
-          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>);
+          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);
           return SPLIT ? sk : a.M / BM;
         }
       }
-      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>);
+      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>, true);
       return 0;
     }
     if ((mode == 2 || mode == 5) && aligned && (!a.colsum || a.workspace)) {
@@ -1131,19 +1151,19 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
     if ((mode == 2 || mode == 3) && aligned && (!a.colsum || a.workspace) && !(EPI == kEpiWire && !SPLIT)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
-      auto launch = [&](auto k) {
+      auto launch = [&](auto k, bool persist) {  // persist: the kernel loops over tiles (not with colsum)
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        hipLaunchKernelGGL(k, grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
-                           a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
+        hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
+                           (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
                            (float*)a.workspace, a.colsum, wo);
       };
       if constexpr (!BKC) {
         if (a.colsum) {
-          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true, 128>);
+          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true, 128>, false);
           return SPLIT ? sk : a.M / BM;
         }
       }
-      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false, 128>);
+      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false, 128>, true);
       return 0;
     }
   }

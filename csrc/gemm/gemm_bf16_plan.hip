@@ -40,6 +40,14 @@ std::atomic<int>& gemm_main_loop_flag() {
   return flag;
 }
 
+std::atomic<int>& gemm_persist_flag() {
+  static std::atomic<int> flag{[] {
+    const char* e = getenv("FAN_GEMM_PERSIST");
+    return e ? atoi(e) : kNumCU;
+  }()};
+  return flag;
+}
+
 // Measured plans for shapes where the heuristic below is not the fastest (bench/gemm_bench.py --sweep on MI355X,
 // profiles/r1_gemm_bert_sweep.jsonl): the BERT-base encoder-layer backward GEMMs at 4096 tokens (BASELINE config
 // 5). Under-filled grids there favour the big tile (and a split-K that keeps one round of workgroups) over

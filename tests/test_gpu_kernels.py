@@ -288,3 +288,51 @@ def test_gemm_256_tile_epilogues(C, main_loop):
     G.gemm(act, True, dZ, False, dW, G.EPI_NONE, split_k=1, tile=(256, 256), colsum=db)
     assert (dW - act.float().t() @ dZ.float()).abs().max().item() < 0.25
     assert (db - dZ.float().sum(0)).abs().max().item() < 1e-2 * M ** 0.5
+
+
+@pytest.fixture
+def persist_cap(C):
+    cap0 = C.gemm_persist()
+    yield C
+    C.gemm_set_persist(cap0)
+
+
+@pytest.mark.parametrize("tile", [(256, 256), (256, 128)])
+@pytest.mark.parametrize("cap", [3, 8])
+def test_gemm_persistent_grid_bit_identical(persist_cap, tile, cap):
+    """The 4-wave pipelined kernel loops over tiles when its grid is capped below the tile count: every layout /
+    epilogue / split-K result is bit-identical to one workgroup per tile (grid caps 3 and 8, 16-32 tiles)."""
+    C = persist_cap
+    mode0 = C.gemm_main_loop()
+    C.gemm_set_main_loop(3)  # 4-wave pipelined loop for the 256x256 tiles
+    try:
+        torch.manual_seed(11)
+        M, N, K = 1024, 1024, 512
+        bf = torch.bfloat16
+        for a_t in (False, True):
+            for b_t in (False, True):
+                A = (torch.randn(K, M, device=DEV) if a_t else torch.randn(M, K, device=DEV)).to(bf)
+                B = (torch.randn(N, K, device=DEV) if b_t else torch.randn(K, N, device=DEV)).to(bf)
+                bias = torch.randn(N, device=DEV).to(bf)
+                act = torch.randn(M, N, device=DEV).to(bf)
+                cases = [(G.EPI_BIAS_RELU, bf, dict(bias=bias)), (G.EPI_RELU_MASK, bf, dict(aux=act)),
+                         (G.EPI_NONE, torch.float32, dict()), (G.EPI_NONE, torch.float32, dict(split_k=2))]
+                for epi, odt, kw in cases:
+                    kw = dict(kw)
+                    sk = kw.pop("split_k", 1)
+                    outs = []
+                    for c in (0, cap):
+                        C.gemm_set_persist(c)
+                        out = torch.full((M, N), 7.0, device=DEV, dtype=odt)
+                        G.gemm(A, a_t, B, b_t, out, epi, split_k=sk, tile=tile, **kw)
+                        torch.cuda.synchronize()
+                        outs.append(out)
+                    assert torch.equal(outs[0], outs[1]), f"a_t={a_t} b_t={b_t} epi={epi} sk={sk}: persistent differs"
+                    ref = (A.double().t() if a_t else A.double()) @ (B.double().t() if b_t else B.double())
+                    if epi == G.EPI_BIAS_RELU:
+                        ref = torch.relu(ref + bias.double())
+                    if epi == G.EPI_RELU_MASK:
+                        ref = ref * (act.double() > 0)
+                    assert (outs[1].double() - ref).abs().max().item() < 0.02 * (1 + ref.abs().max().item())
+    finally:
+        C.gemm_set_main_loop(mode0)
