@@ -833,6 +833,10 @@ __global__ void __launch_bounds__(256, 1)
   constexpr int Q = MI * NJ, R = MI + NJ;  // MFMAs and fragment reads per k-step and wave
   constexpr int RSP = (Q * 3 / 4) / R, DSP = Q / G;  // read / DMA spacing in MFMAs (64 MFMAs: 3 / 4; 32: 2 / 2)
   static_assert(BN == 256 || BN == 128, "256x256 or 256x128 tiles");
+  // 256x128 tiles fit 3 operand stages in the LDS (144 KB): K-tile kt + 2 is then fetched during k-step 0 of kt
+  // (its stage was consumed in kt - 1) instead of k-step 1, so 1.5 K-tiles of fetch latency are covered (the
+  // classifier forward reads a 64 MB activation straight from HBM inside the step: 76 vs 63 us from the MALL).
+  constexpr int STAGES = BN == 128 ? 3 : 2;
   static_assert(RSP >= 1 && DSP >= 1 && G * DSP <= Q, "schedule");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -888,7 +892,7 @@ __global__ void __launch_bounds__(256, 1)
   // glds piece p (0..G-1) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
   // the accumulator array in scratch memory)
   auto piece = [&](int kt, int p) __attribute__((always_inline)) {
-    const uint32_t st = lds0 + (kt & 1) * STAGE + wave * 1024;
+    const uint32_t st = lds0 + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE + wave * 1024;
     if (p < GA) glds16_s(a_k0 + kt * a_step, off[p], st + p * OpTile<BM, NT>::IB);
     else glds16_s(b_k0 + kt * b_step, off[p], st + A_BYTES + (p - GA) * OpTile<BN, NT>::IB);
   };
@@ -933,16 +937,29 @@ __global__ void __launch_bounds__(256, 1)
   for (int r = 0; r < R; ++r) read_next(smem, 0, 0, r);
 
   auto ktile = [&](int kt, auto more_c, auto more2_c) __attribute__((always_inline)) {
-    const char* st = smem + (kt & 1) * STAGE;
+    const char* st = smem + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE;
     const bool csk = do_colsum && kt >= cs0 && kt < cs1;
     FAN_STAMP(0);
-    block(I0{}, T_{}, F_{}, st, 1, 0, csk);
-    FAN_STAMP(1);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    FAN_STAMP(2);
-    __builtin_amdgcn_s_barrier();
-    FAN_STAMP(3);
-    block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk);
+    if constexpr (STAGES == 2) {
+      block(I0{}, T_{}, F_{}, st, 1, 0, csk);
+      FAN_STAMP(1);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      FAN_STAMP(2);
+      __builtin_amdgcn_s_barrier();
+      FAN_STAMP(3);
+      block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk);
+    } else {
+      // DMA of K-tile kt + 2 under k-step 0; the barrier then needs only K-tile kt + 1 (the G younger pieces of
+      // kt + 2 may stay in flight)
+      block(I0{}, T_{}, more2_c, st, 1, kt + 2, csk);
+      FAN_STAMP(1);
+      if constexpr (decltype(more2_c)::value) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      FAN_STAMP(2);
+      __builtin_amdgcn_s_barrier();
+      FAN_STAMP(3);
+      block(I1{}, more_c, F_{}, smem + ((kt + 1) % 3) * STAGE, 0, 0, csk);
+    }
     FAN_STAMP(4);
   };
   int kt = 0;
@@ -1150,7 +1167,7 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     const int mode = main_loop_mode();
     const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
     if ((mode == 2 || mode == 3) && aligned && (!a.colsum || a.workspace) && !(EPI == kEpiWire && !SPLIT)) {
-      constexpr int lds = 2 * (BM + BN) * BK * 2;
+      constexpr int lds = 3 * (BM + BN) * BK * 2;  // 3 operand stages (gemm_pl4_kernel, BN 128)
       auto launch = [&](auto k, bool persist) {  // persist: the kernel loops over tiles (not with colsum)
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
