@@ -1166,7 +1166,8 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     // loop with 128x64 per wave
     const int mode = main_loop_mode();
     const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
-    if ((mode == 2 || mode == 3) && aligned && (!a.colsum || a.workspace) && !(EPI == kEpiWire && !SPLIT)) {
+    // (also with the in-kernel BFP wire encode: only reached through a forced 256x128 plan for the bwd-weight)
+    if ((mode == 2 || mode == 3) && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 3 * (BM + BN) * BK * 2;  // 3 operand stages (gemm_pl4_kernel, BN 128)
       auto launch = [&](auto k, bool persist) {  // persist: the kernel loops over tiles (not with colsum)
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));

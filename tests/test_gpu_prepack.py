@@ -221,7 +221,8 @@ def test_gemm_wire_epilogue_encodes_fused_bias(codec, nsh):
 
 
 @pytest.mark.parametrize("codec", ["bfp_rne", "bfp_trunc"])
-@pytest.mark.parametrize("sk,tile", [(2, None), (4, (256, 256)), (2, (256, 256))])
+@pytest.mark.parametrize("sk,tile", [(2, None), (4, (256, 256)), (2, (256, 256)), (1, (256, 256)), (1, (256, 128)),
+                                     (2, (256, 128))])
 def test_gemm_wire_epilogue_splitk(codec, sk, tile):
     """Split-K bwd-weight with the wire epilogue: the slab reduce encodes W and the fused bias gradient. Byte-
     identical to packing the same split GEMM's f32 output (slabs summed in the same order)."""
