@@ -2,7 +2,7 @@
 # Round-2 check after the persistent GEMM: whole GPU suite, smoke, flagship bench x3, kernel stats, fwd2 probe.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/check4
+O=${CHECK_OUT:-gpurun_out/check4}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
