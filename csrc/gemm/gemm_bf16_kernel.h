@@ -1124,8 +1124,10 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
     // force one of them
     // (the MLP's bwd-data with the ReLU-mask epilogue, activation loads prefetched: 4 waves 197 vs 200 us at
     // 8192x4096x4096, 67.9 vs 68.5 at K 1024, profiles/r2_gemm_loops_bwdd.jsonl)
-    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192 || EPI == kEpiReluMask) &&
-                                   !(EPI == kEpiWire && !SPLIT));
+    // (and the in-kernel wire encode: since the 4-wave kernel became persistent, the 4096^2 bwd-weight with the wire
+    // + bias-gradient epilogue runs faster in the step there, 1.036-1.038 vs 1.042-1.052 ms/step,
+    // profiles/r2_pl3_wire_ab.txt; in isolation it measured +13 vs +7 us for the encode)
+    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192 || EPI == kEpiReluMask));
     if (pl4 && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto launch = [&](auto k, bool persist) {  // persist: the kernel loops over tiles (not with colsum)
