@@ -65,7 +65,11 @@ def parse_args(argv=None):
                     help="side-stream engine: run each request's decode+SGD epilogue on the comm stream (overlapped "
                          "with the remaining backward) or on the compute stream after the last backward GEMM")
     ap.add_argument("--no-trace", action="store_true",
-                    help="do not record per-request device timestamps inside the timed steps (extra.allreduce)")
+                    help="skip the separate traced pass that measures the all-reduce phases (extra.allreduce)")
+    ap.add_argument("--timeout", type=float, default=300.0,
+                    help="watchdog budget per phase in seconds (init, warmup, timed steps, ...) and the bound of every "
+                         "all-reduce wait: on expiry the engine's debug_status() goes to stderr, the communicator is "
+                         "aborted and the rank exits with code 124 (0 disables)")
     return ap.parse_args(argv)
 
 
@@ -117,7 +121,39 @@ def main(argv=None):
     from fpga_ai_nic_amd.parallel.transport import (NativeTransport, ThreadFabric, TorchDistTransport,
                                                     make_p2p_comm)
     from fpga_ai_nic_amd.utils import dist as D
+    from fpga_ai_nic_amd.utils.watchdog import Watchdog
 
+    # watchdog: every phase of the run is bounded; on expiry the engine state goes to stderr and the rank exits 124
+    held = {"engine": None, "comm": None, "transport": None}
+    env_rank = int(os.environ.get("RANK", "0"))
+
+    def _dump():
+        e = held["engine"]
+        d = {"rank": env_rank, "world": int(os.environ.get("WORLD_SIZE", "1"))}
+        if e is not None and hasattr(e, "debug_status"):
+            d["engine"] = e.debug_status()
+        if held["comm"] is not None and hasattr(held["comm"], "flags_snapshot"):
+            d["p2p_flags"] = list(held["comm"].flags_snapshot(2.0))
+        return d
+
+    def _abort():
+        for k in ("comm", "transport"):
+            if held[k] is not None and hasattr(held[k], "abort"):
+                held[k].abort()
+
+    wd = Watchdog(a.timeout, dump=_dump, on_abort=_abort, tag=f"bench rank {env_rank}")
+    wd.arm("init")
+    hook = sys.excepthook
+
+    def _excepthook(et, ev, tb):  # an uncaught error (e.g. an all-reduce timeout) also reports the engine state
+        try:
+            print(f"[bench rank {env_rank}] debug_status " + json.dumps(_dump(), default=str), file=sys.stderr,
+                  flush=True)
+        except Exception:  # noqa: BLE001
+            pass
+        hook(et, ev, tb)
+
+    sys.excepthook = _excepthook
     rank, world, local, device = D.init_distributed(force=a.force_dist)
     if world != a.gpus and rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
@@ -143,10 +179,15 @@ def main(argv=None):
             transport = TorchDistTransport(force_collectives=a.force_dist)
         if a.transport == "p2p" and device.type == "cuda" and impl == "native":
             comm = make_p2p_comm()
+        if comm is None:  # report the transport the gradient plane actually uses
+            a.transport = getattr(transport, "name", a.transport)
     else:
         transport = ThreadFabric(1).transport(0)
+    held["transport"], held["comm"] = transport, comm
     engine = make_engine(transport, a.compress, rounding=a.rounding, algo=a.algo, rings=a.rings,
-                         force_comm=a.force_dist, impl=impl, comm=comm, side_stream=a.side_stream)
+                         force_comm=a.force_dist, impl=impl, comm=comm, side_stream=a.side_stream,
+                         timeout_s=a.timeout + 30.0 if a.timeout > 0 else 600.0)  # the watchdog fires first
+    held["engine"] = engine
     if hasattr(engine, "epilogue_on_producer") and not getattr(engine, "inline", True):
         engine.epilogue_on_producer = a.epi == "producer"
     pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
@@ -156,8 +197,10 @@ def main(argv=None):
             transport.broadcast_(l.master, 0)
         model.sync_lp()
     trainer = DataParallelTrainer(model, engine, lr=a.lr)
-    # device-timed communication phase of every request inside the timed steps (C++ engine, multi-rank path)
+    # device-timed communication phases of the requests (C++ engine, multi-rank path): measured in a separate
+    # traced pass, so the headline steps run with tracing off (its timing events and timed flag waits cost time)
     can_trace = (not a.no_trace and hasattr(engine, "trace") and not getattr(engine, "inline", True))
+    stall_rank = int(os.environ.get("FAN_BENCH_STALL_RANK", "-1"))
 
     def batch(mb, seed):
         g = torch.Generator().manual_seed(seed + rank)
@@ -165,13 +208,17 @@ def main(argv=None):
         y = torch.randint(0, SIZES[-1], (mb,), generator=g, dtype=torch.int32).to(device)
         return x, y
 
-    def run(mb, seed, graph_ok):
+    def run(mb, seed, graph_ok, trace=False, warmup=None, tag="timed"):
         """W warmup + K timed steps at per-GPU batch mb: (elapsed s max over ranks, host enqueue s, loss,
         trace summary or None, graphed)."""
         x, y = batch(mb, seed)
-        for _ in range(a.warmup):
+        wd.arm(f"warmup {tag} mb={mb}")
+        if stall_rank == rank:  # test hook: this rank stops taking part (a hung peer for the watchdog test)
+            time.sleep(float(os.environ.get("FAN_BENCH_STALL_S", "600")))
+        for _ in range(a.warmup if warmup is None else warmup):
             trainer.step(x, y)
         trainer.finish()
+        wd.arm(f"{tag} mb={mb}")
         step = lambda: trainer.step(x, y)  # noqa: E731
         graphed = False
         if graph_ok and a.graph and device.type == "cuda" and world == 1 and \
@@ -189,7 +236,7 @@ def main(argv=None):
             except RuntimeError as e:  # capture unsupported for this configuration: stay eager
                 print(f"[bench] HIP graph capture failed ({e}); running eagerly", file=sys.stderr)
                 torch.cuda.synchronize()
-        if can_trace:
+        if trace:
             engine.trace(True)
         t0 = _time_steps(step, a.steps, device, D)
         loss_rows = model.loss_rows
@@ -200,20 +247,27 @@ def main(argv=None):
         D.barrier()
         elapsed = D.max_over_ranks(time.perf_counter() - t0)
         tr = None
-        if can_trace:
+        if trace:
             tr = engine.trace_summary()
             engine.trace(False)
             tr["comm_ms"] = D.max_over_ranks(tr["comm_ms"])  # the slowest rank's communication time
+            tr["ms_per_step"] = elapsed / a.steps * 1e3
         return elapsed, t_enqueue, float(loss_rows.float().mean().item()), tr, graphed
 
     mb = a.mb_per_gpu
-    elapsed, t_enqueue, loss, tr, graphed = run(mb, 1234, True)
+    elapsed, t_enqueue, loss, _, graphed = run(mb, 1234, True)
+    tr = run(mb, 1234, False, trace=True, warmup=1, tag="traced")[3] if can_trace else None
     ref = None
     if a.ref_mb and a.ref_mb != mb:
-        e2, _, _, tr2, _ = run(a.ref_mb, 4321, False)
+        e2, _, _, _, _ = run(a.ref_mb, 4321, False, tag="ref")
         ref = {"mb_per_gpu": a.ref_mb, "global_batch": a.ref_mb * world,
-               "samples_per_s": round(a.ref_mb * world * a.steps / e2, 2), "ms_per_step": round(e2 / a.steps * 1e3, 4),
-               "allreduce": _allreduce_report(tr2, world)}
+               "samples_per_s": round(a.ref_mb * world * a.steps / e2, 2), "ms_per_step": round(e2 / a.steps * 1e3, 4)}
+    # replicas after every step of the run: bit-identical weights on every rank (the reference reads its NIC
+    # registers back to stdout after programming them, sw/mlp_mpi_example_f32.cpp:65-98; here the run proves
+    # what it ran on and that the replicas agree)
+    wd.arm("verify")
+    dist_rec = _dist_report(a, engine, model, world, rank, device, D)
+    wd.disarm()
 
     ms = elapsed / a.steps * 1e3
     global_batch = mb * world
@@ -257,24 +311,75 @@ def main(argv=None):
                 "allreduce": _allreduce_report(tr, world),
                 f"mb{a.ref_mb}": ref,
                 "final_loss": round(loss, 5),
+                "dist": dist_rec,
                 **({"engine_counters": engine.counters()} if hasattr(engine, "counters") else {}),
             },
         }
         print(json.dumps(rec), flush=True)
+    wd.arm("cleanup")
     D.cleanup()
+    wd.close()
+    if not dist_rec["replicas_identical"]:
+        print(f"[bench] rank {rank}: replicas DIVERGED: {dist_rec['replica_digests']}", file=sys.stderr, flush=True)
+        return 2
     return 0
 
 
+def replica_digest(tensors):
+    """Per tensor: (exact bit hash, fp64 sum). The hash is integer arithmetic on the f32 bit patterns (position-
+    weighted, wrapping mod 2^64), so it is order-independent and equal across ranks iff the bits are."""
+    import torch
+
+    out = []
+    for t in tensors:
+        b = t.detach().reshape(-1).contiguous().view(torch.int32).to(torch.int64)
+        w = torch.arange(b.numel(), device=b.device, dtype=torch.int64).mul_(2).add_(1)
+        h = int((b * w).sum().item()) & 0xFFFFFFFFFFFFFFFF
+        out.append([f"{h:016x}", float(t.detach().double().sum().item())])
+    return out
+
+
+def _dist_report(a, engine, model, world, rank, device, D):
+    """extra.dist: what the run actually ran on — torch's and the engine communicator's rank counts (RCCL:
+    ncclCommCount), the transport, the ring orders and link matrix the planner used, the devices (PCI bus ids) of
+    the ranks — and whether the replicas' weights are bit-identical after the run (all-gathered digests)."""
+    from fpga_ai_nic_amd.utils import topology
+
+    C = getattr(engine, "C", None)
+    mine = {
+        "digest": replica_digest([l.master for l in model.layers]),
+        "comm_ranks": int(C.comm_ranks) if C is not None else (world if engine is not None else 1),
+        "bus_id": topology.device_bus_id(device.index) if device.type == "cuda" else None,
+    }
+    every = D.all_gather_object(mine)
+    digests = [e["digest"] for e in every]
+    ident = all(d == digests[0] for d in digests)
+    return {
+        "world": world,
+        "torch_backend": D.backend(),
+        "transport": a.transport if world > 1 or a.force_dist else "none",
+        "engine_comm": (C.comm_kind if C is not None else ("python" if engine is not None else "none")),
+        "comm_ranks": [e["comm_ranks"] for e in every],
+        "algo": getattr(engine, "algo", None),
+        "ring_orders": getattr(engine, "orders", None) if getattr(engine, "algo", None) == "ring" else None,
+        "links": getattr(engine, "links", None),
+        "bus_ids": [e["bus_id"] for e in every],
+        "replicas_identical": ident,
+        "replica_digests": digests if not ident else digests[0],
+    }
+
+
 def _allreduce_report(tr, world):
-    """All-reduce algo-BW of the requests inside the timed steps: logical (f32 gradient) bytes / summed device time
-    of their communication phases (request start on the comm stream -> end of the all-gather, slowest rank);
-    bus-BW = algo-BW x 2(N-1)/N; wire-BW = bytes this rank actually sent (BFP-packed) / the same time.
-    None when no collective ran (world 1 inline engine: no wire)."""
+    """All-reduce algo-BW of the requests of the traced pass (the same K steps again, with per-request device
+    timestamps): logical (f32 gradient) bytes / summed device time of their communication phases (request start on
+    the comm stream -> end of the all-gather, slowest rank); bus-BW = algo-BW x 2(N-1)/N; wire-BW = bytes this rank
+    actually sent (BFP-packed) / the same time. None when no collective ran (world 1 inline engine: no wire)."""
     if not tr or not tr.get("requests") or tr.get("comm_ms", 0) <= 0:
         return None
     s = tr["comm_ms"] / 1e3
     algo = tr["logical_bytes"] / s / 1e9
     return {
+        "traced_ms_per_step": round(tr["ms_per_step"], 4),
         "requests": tr["requests"],
         "comm_ms_total": round(tr["comm_ms"], 4),
         "allreduce_algo_bw_GBps": round(algo, 2),

@@ -24,7 +24,9 @@ void register_engine(pybind11::module_& m) {
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)
       .def("async_error", &Comm::async_error)
-      .def("abort", &Comm::abort);
+      .def("abort", &Comm::abort)
+      .def("ranks_seen", &Comm::ranks_seen, "ranks this communicator reaches (RCCL: ncclCommCount)")
+      .def_property_readonly("kind", [](const Comm& c) { return std::string(c.kind()); });
   pybind11::class_<LoopbackFabric, std::shared_ptr<LoopbackFabric>>(m, "LoopbackFabric")
       .def(pybind11::init<int, double>(), pybind11::arg("world"), pybind11::arg("timeout_s") = 60.0)
       .def_property_readonly("world", &LoopbackFabric::world)
@@ -73,7 +75,8 @@ void register_engine(pybind11::module_& m) {
            },
            "device-side stall counters: flag waits (ready / credit), their device time when timed, bytes per peer")
       .def("reset_stats", &P2PComm::reset_stats)
-      .def("flags_snapshot", &P2PComm::flags_snapshot, "ready-from-src[world] + ack-from-dst[world] words")
+      .def("flags_snapshot", &P2PComm::flags_snapshot, pybind11::arg("timeout_s") = 2.0,
+           "ready-from-src[world] + ack-from-dst[world] words (empty if the copy did not complete in time)")
       .def("all_to_all",
            [](P2PComm& c, const at::Tensor& send, at::Tensor& recv) {
              TORCH_CHECK(bytes_of(send) == bytes_of(recv) && bytes_of(send) % c.world() == 0, "all_to_all sizes");
@@ -171,6 +174,10 @@ void register_engine(pybind11::module_& m) {
       .def("wire_bytes", [](AllReduceEngine& e, int64_t n) { return e.wire_bytes(e.layout(n)); })
       .def_property_readonly("orders", &AllReduceEngine::orders)
       .def_property_readonly("inline", &AllReduceEngine::is_inline)
+      .def_property_readonly("comm_kind",
+                             [](AllReduceEngine& e) { return std::string(e.comm() ? e.comm()->kind() : "none"); })
+      .def_property_readonly("comm_ranks", [](AllReduceEngine& e) { return e.comm() ? e.comm()->ranks_seen() : 1; },
+                             "ranks the engine's communicator reaches (RCCL: ncclCommCount; P2P: mapped peers + 1)")
       .def_property_readonly("stream", [](AllReduceEngine& e) { return (uintptr_t)e.stream(); })
       .def("submit",
            [](AllReduceEngine& e, const at::Tensor& grad, at::Tensor& master, c10::optional<at::Tensor> lp,

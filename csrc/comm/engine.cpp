@@ -98,6 +98,8 @@ AllReduceEngine::~AllReduceEngine() {
   for (auto& t : trace_pool_)
     for (auto& e : t.ev) hipEventDestroy(e);
   for (auto& kv : scratch_) hipFree(kv.second.first);
+  for (auto& kv : gall_)
+    if (kv.second.free) hipEventDestroy(kv.second.free);
   if (flags_host_) hipHostFree((void*)flags_host_);
   if (tags_) hipFree(tags_);
   if (verr_dev_) hipFree(verr_dev_);
@@ -116,7 +118,14 @@ EngineLayout AllReduceEngine::layout(int64_t n) const {
     // buckets above chunk_elems stream through the collectives in balanced chunks of N shards (multi-rank path
     // only: the inline world-1 engine has no collectives to pipeline)
     const bool local = N == 1 && !cfg_.force_comm;
-    L.chunks = local ? 1 : std::max<int64_t>(1, cdiv(n, cfg_.chunk_elems));
+    int64_t chunk = cfg_.chunk_elems;
+    if (P2PComm* d = comm_ ? comm_->direct() : nullptr) {
+      // a P2P message (one wire shard) must fit one arena slot: chunk the bucket so that it does
+      const int64_t max_shard = (int64_t)(d->slot_bytes() / wire_shard_bytes(cfg_.codec, 256)) * 256;
+      FAN_CHECK(max_shard >= 256, "p2p arena slot smaller than one 256-element wire shard");
+      chunk = std::min<int64_t>(chunk, max_shard * N);
+    }
+    L.chunks = local ? 1 : std::max<int64_t>(1, cdiv(n, chunk));
     L.shard = round_up(std::max<int64_t>(cdiv(n, N * L.chunks), 1), 256);
     L.n_pad = L.shard * N * L.chunks;
     return L;
@@ -360,7 +369,28 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
     S[q] = scratch("meshc_S" + std::to_string(q) + "_" + k, sb);
     if (!defer) Gc[q] = scratch("meshc_G" + std::to_string(q) + "_" + k, cb);
   }
-  uint8_t* Gall = defer ? epi_scratch("meshc_Gall_" + k + "_" + std::to_string(C), cb * C) : nullptr;
+  // A deferred request's epilogue reads the whole gathered bucket at commit. One such buffer per bucket size is
+  // shared by every deferred chunked request (not one per slot: 17 B per 16 elements of a multi-GB bucket, 8 times
+  // over): a new user first commits the previous one if it is still pending (ordered after its producer, as a
+  // 9th deferred request does) and waits for that epilogue to finish reading before the all-gather overwrites it.
+  uint8_t* Gall = nullptr;
+  hipEvent_t gall_free = nullptr;
+  if (defer) {
+    GallBuf& gb = gall_[k + "_" + std::to_string(C)];
+    if (gb.free == nullptr) FAN_HIP_CHECK(hipEventCreateWithFlags(&gb.free, hipEventDisableTiming));
+    if (gb.seq != 0) {
+      Slot& prev = slots_[gb.slot];
+      if (prev.seq == gb.seq && prev.pending && gb.slot != epi_slot_) {
+        counters_.forced_commits++;
+        commit_slot(prev, gb.slot, true, cur_producer_);
+      }
+      FAN_HIP_CHECK(hipStreamWaitEvent(A, gb.free, 0));  // recorded after that epilogue (no-op if it never ran)
+    }
+    gb.slot = epi_slot_;
+    gb.seq = req_seq_;
+    Gall = scratch("meshc_Gall_" + k + "_" + std::to_string(C), cb * C);
+    gall_free = gb.free;
+  }
   auto gath = [&](int64_t ch) { return defer ? Gall + ch * cb : Gc[ch % 2]; };
   auto gather = [&](int64_t ch) {  // comm stream: all-gather of chunk ch's reduced owner shard
     RoctxRange rr("fan/mesh/all_gather");
@@ -420,7 +450,10 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
   if (!defer) return {};
   const int64_t n_pad = L.n_pad, shards = C * N;
   uint8_t* G = Gall;
-  return {[=](hipStream_t es) { epilogue(c, es, G, s, (int)shards, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
+  return {[=](hipStream_t es) {
+    epilogue(c, es, G, s, (int)shards, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum);
+    FAN_HIP_CHECK(hipEventRecord(gall_free, es));  // the shared gathered wire may be reused after this point
+  }};
 }
 
 std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const void* grad, int gdt,
@@ -564,7 +597,17 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
     commit_slot(sl, slot, true, producer);
   }
   const EngineLayout L = layout(n_valid);
-  sl.stream = run_stream_ = inline_ ? producer : stream_;
+  const hipStream_t run = inline_ ? producer : stream_;
+  // The slot's previous epilogue may have run on another stream than this request will (a world-1 side epilogue,
+  // or an epilogue committed on another producer stream) and may still read this slot's scratch, which this
+  // request is about to rewrite: order this request after it. (A multi-rank request waits for `ready` on the
+  // producer below, which already covers an epilogue enqueued there.)
+  if (sl.seq != 0 && sl.epi_stream != nullptr && sl.epi_stream != run && !(!inline_ && sl.epi_stream == producer)) {
+    ensure_done(sl);
+    FAN_HIP_CHECK(hipStreamWaitEvent(run, sl.done, 0));
+  }
+  cur_producer_ = producer;
+  sl.stream = run_stream_ = run;
   if (!inline_) {
     FAN_HIP_CHECK(hipEventRecord(sl.ready, producer));
     FAN_HIP_CHECK(hipStreamWaitEvent(stream_, sl.ready, 0));
@@ -755,16 +798,24 @@ std::string AllReduceEngine::debug_status() {
   for (char& ch : err)
     if (ch == '"' || ch == '\\') ch = '\'';
   os << "], \"comm_error\": \"" << err << "\"";
+  if (comm_) os << ", \"comm_kind\": \"" << comm_->kind() << "\", \"comm_ranks\": " << comm_->ranks_seen();
   if (verify_) os << ", \"verify_error\": " << (verr_host_->flag ? "true" : "false");
   if (P2PComm* d = comm_ ? comm_->direct() : nullptr) {
-    const P2PComm::Stats st = d->stats();
+    // never blocks on the (possibly parked) streams: completed timed waits only, flag copy bounded by 2 s
+    const P2PComm::Stats st = d->stats(false);
     os << ", \"p2p\": {\"sequence\": " << d->sequence() << ", \"ready_waits\": " << st.ready_waits
        << ", \"credit_waits\": " << st.credit_waits << ", \"timed_waits\": " << st.timed_waits
        << ", \"ready_stall_ms\": " << st.ready_stall_ms << ", \"credit_stall_ms\": " << st.credit_stall_ms
-       << ", \"flags\": [";
-    const std::vector<uint64_t> f = d->flags_snapshot();
-    for (size_t i = 0; i < f.size(); ++i) os << (i ? ", " : "") << f[i];
-    os << "]}";
+       << ", \"flags\": ";
+    const std::vector<uint64_t> f = d->flags_snapshot(2.0);
+    if (f.empty()) {
+      os << "null, \"flags_error\": \"flag snapshot copy did not complete within 2 s\"";
+    } else {
+      os << "[";
+      for (size_t i = 0; i < f.size(); ++i) os << (i ? ", " : "") << f[i];
+      os << "]";
+    }
+    os << "}";
   }
   os << "}";
   return os.str();

@@ -112,6 +112,7 @@ class AllReduceEngine {
   EngineLayout layout(int64_t n) const;
   const std::vector<std::vector<int>>& orders() const { return orders_; }
   hipStream_t stream() const { return stream_; }
+  Comm* comm() const { return comm_; }
   bool is_inline() const { return inline_; }
   int codec() const { return cfg_.codec; }
 
@@ -243,6 +244,14 @@ class AllReduceEngine {
   EngineCounters counters_;
   std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
   int epi_slot_ = 0;  // slot of the request being built
+  hipStream_t cur_producer_ = nullptr;  // producer stream of the request being built
+  // deferred chunked requests: the whole-bucket gathered wire, one per bucket size, and who used it last
+  struct GallBuf {
+    int slot = 0;
+    uint32_t seq = 0;
+    hipEvent_t free = nullptr;  // recorded on the epilogue stream after the last user's epilogue
+  };
+  std::map<std::string, GallBuf> gall_;
   bool cur_defer_ = false;  // the request being built defers its epilogue
   bool tracing_ = false;
   std::vector<RequestTrace> trace_pool_;

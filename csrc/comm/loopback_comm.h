@@ -47,6 +47,7 @@ class LoopbackComm : public Comm {
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override;
   std::string async_error() override { return f_->aborted ? "loopback fabric aborted" : ""; }
   void abort() override { f_->aborted = true; }
+  const char* kind() const override { return "loopback"; }
   void drop_after(int64_t k) { drop_after_ = k; }
   // fault injection: the messages of this rank's k-th sendrecv round (0-based, counted over sendrecv calls) are lost
   // in flight — the receivers' buffers keep their stale contents, the schedule goes on (a silent loss, what

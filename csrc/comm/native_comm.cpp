@@ -68,6 +68,12 @@ std::string NativeComm::async_error() {
   return ncclGetErrorString(r);
 }
 
+int NativeComm::ranks_seen() {
+  int n = -1;
+  if (comm_ && !aborted_ && ncclCommCount(comm_, &n) != ncclSuccess) n = -1;
+  return n;
+}
+
 void NativeComm::abort() {
   if (comm_ && !aborted_) {
     ncclCommAbort(comm_);

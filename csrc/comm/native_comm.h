@@ -49,6 +49,11 @@ class Comm {
   virtual void abort() = 0;
   // Transports whose receive buffers the engine's kernels may write and read in place (direct peer stores):
   virtual P2PComm* direct() { return nullptr; }
+  // Run-time echo of what this communicator actually reaches (the reference reads node_info back after
+  // programming it, sw/mlp_mpi_example_f32.cpp:65-98): RCCL's own rank count (ncclCommCount), the P2P transport's
+  // this rank + peers whose receive arenas are mapped, the loopback fabric's virtual ranks.
+  virtual int ranks_seen() { return world(); }
+  virtual const char* kind() const = 0;
 };
 
 class NativeComm : public Comm {
@@ -65,6 +70,8 @@ class NativeComm : public Comm {
   void broadcast(void* buf, size_t bytes, int root, hipStream_t s);
   std::string async_error() override;
   void abort() override;
+  int ranks_seen() override;
+  const char* kind() const override { return "rccl"; }
 
  private:
   ncclComm_t comm_ = nullptr;

@@ -1,8 +1,11 @@
 // Direct peer-to-peer transport. See p2p_comm.h.
 #include "comm/p2p_comm.h"
 
+#include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace fan {
 
@@ -78,15 +81,21 @@ void P2PComm::wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool cred
   if (t) FAN_HIP_CHECK(hipEventRecord(t->ev[1], s));
 }
 
-P2PComm::Stats P2PComm::stats() {
-  for (size_t i = 0; i < tw_used_; ++i) {  // fold the recorded waits into the totals, then recycle the events
+P2PComm::Stats P2PComm::stats(bool wait) {
+  // fold the recorded waits into the totals, then recycle the events (in order: a wait still parked keeps itself
+  // and every later one for the next call)
+  size_t i = 0;
+  for (; i < tw_used_; ++i) {
+    if (!wait && hipEventQuery(tw_[i].ev[1]) != hipSuccess) break;
     float ms = 0.f;
     FAN_HIP_CHECK(hipEventSynchronize(tw_[i].ev[1]));
     FAN_HIP_CHECK(hipEventElapsedTime(&ms, tw_[i].ev[0], tw_[i].ev[1]));
     stall_ms_[tw_[i].credit ? 1 : 0] += ms;
     timed_++;
   }
-  tw_used_ = 0;
+  (void)hipGetLastError();  // a not-ready query is not an error
+  if (i > 0 && i < tw_used_) std::rotate(tw_.begin(), tw_.begin() + i, tw_.begin() + tw_used_);
+  tw_used_ -= i;
   Stats r;
   r.ready_waits = ready_waits_;
   r.credit_waits = credit_waits_;
@@ -104,9 +113,31 @@ void P2PComm::reset_stats() {
   bytes_to_peer_.assign(world_, 0);
 }
 
-std::vector<uint64_t> P2PComm::flags_snapshot() const {
-  std::vector<uint64_t> v((size_t)2 * world_);
-  FAN_HIP_CHECK(hipMemcpy(v.data(), flags_, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+std::vector<uint64_t> P2PComm::flags_snapshot(double timeout_s) const {
+  const size_t n = (size_t)2 * world_;
+  // pinned staging + a non-blocking stream of its own: nothing here waits on the (possibly parked) engine streams;
+  // on timeout the staging buffer and stream are leaked on purpose (the copy may still land in them later)
+  void* h = nullptr;
+  hipStream_t s = nullptr;
+  if (hipHostMalloc(&h, n * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess ||
+      hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    return {};
+  }
+  std::vector<uint64_t> v;
+  if (hipMemcpyAsync(h, flags_, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s) == hipSuccess) {
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q;
+    while ((q = hipStreamQuery(s)) == hipErrorNotReady &&
+           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < timeout_s)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (q == hipSuccess) {
+      v.assign(static_cast<const uint64_t*>(h), static_cast<const uint64_t*>(h) + n);
+      hipStreamDestroy(s);
+      hipHostFree(h);
+    }
+  }
+  (void)hipGetLastError();
   return v;
 }
 
@@ -117,13 +148,21 @@ void P2PComm::abort() {
   // dead receiver): overwrite all ready / ack words with a poison value above any sequence number, from a stream of
   // its own (the parked stream cannot run it). The released streams then copy stale arena bytes; the aborted_
   // state makes every later call and the engine's synchronize() raise, so nothing trusts them.
+  // The poison write is polled for a bounded time rather than synchronized: if the new stream shares a hardware
+  // queue with a parked one, it waits behind it, and abort() must still return (the caller is usually a watchdog
+  // about to end the process).
   hipSetDevice(device_);
   hipStream_t s = nullptr;
   if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
     hipMemsetAsync(flags_, 0x7F, (size_t)2 * world_ * sizeof(uint64_t), s);
-    hipStreamSynchronize(s);
-    hipStreamDestroy(s);
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q;
+    while ((q = hipStreamQuery(s)) == hipErrorNotReady &&
+           std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 5.0)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (q == hipSuccess) hipStreamDestroy(s);
   }
+  (void)hipGetLastError();
 }
 
 P2PComm::~P2PComm() {

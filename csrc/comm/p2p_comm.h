@@ -87,6 +87,12 @@ class P2PComm : public Comm {
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override;
   std::string async_error() override { return aborted_ ? "p2p transport aborted" : ""; }
   void abort() override;
+  int ranks_seen() override {
+    int n = 1;
+    for (int p = 0; p < world_; ++p) n += (p != rank_ && peer_arena_[p] != nullptr && peer_flags_[p] != nullptr);
+    return n;
+  }
+  const char* kind() const override { return "p2p"; }
   uint64_t sequence() const { return seq_; }
   bool uncached() const { return uncached_; }
   const std::string& arena_memory() const { return arena_mem_; }
@@ -103,11 +109,15 @@ class P2PComm : public Comm {
     std::vector<int64_t> bytes_to_peer;
   };
   void set_timing(bool on) { timing_ = on; }
-  Stats stats();  // waits for the timed waits' events
+  // wait=true: waits for the timed waits' events. wait=false (diagnostics of a possibly hung run): folds in only
+  // the timed waits whose end event has already completed and keeps the others for later.
+  Stats stats(bool wait = true);
   void reset_stats();
   void count_sent(int peer, size_t bytes) { bytes_to_peer_[peer] += (int64_t)bytes; }
-  // flag block snapshot (ready-from-src[world], ack-from-dst[world]) for diagnostics (synchronous copy)
-  std::vector<uint64_t> flags_snapshot() const;
+  // flag block snapshot (ready-from-src[world], ack-from-dst[world]) for diagnostics. The copy runs on a stream of
+  // its own and is polled for at most timeout_s, so a snapshot taken while a stream is parked on one of these flags
+  // (the hang it is meant to diagnose) returns instead of blocking; empty when the copy did not complete in time.
+  std::vector<uint64_t> flags_snapshot(double timeout_s = 2.0) const;
 
  private:
   void copy(const std::vector<P2PCopy>& segs, hipStream_t s);

@@ -138,7 +138,7 @@ class NativeAllReduce:
             if algo == "ring" and self.world > 1 and not isinstance(comm, C.LoopbackComm):
                 from ..utils import topology
 
-                links = topology.link_matrix(self.world)
+                links = topology.agreed_link_matrix(self.world)  # rank 0 decides, every rank plans the same rings
         self.links = links
         if os.environ.get("FAN_COMM_PRIORITY"):  # comm / aux stream priority override (-1 high, 0 normal)
             stream_priority = int(os.environ["FAN_COMM_PRIORITY"])

@@ -60,6 +60,19 @@ def max_over_ranks(x: float) -> float:
     return float(t.item())
 
 
+def backend() -> str | None:
+    return dist.get_backend() if dist.is_initialized() else None
+
+
+def all_gather_object(obj) -> list:
+    """Every rank's ``obj`` in rank order (``[obj]`` without a multi-rank process group)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def cleanup():
     if dist.is_initialized():
         try:

@@ -53,22 +53,111 @@ def rocm_smi_links():
     return links
 
 
-def link_matrix(world: int):
-    """Direct-link matrix of the first ``world`` GPUs (rank r = device r, one process per GPU on one node):
-    links[a][b] = 1 when a reaches b over xGMI — rocm-smi's link type when it reports one (XGMI), else HIP peer
-    access. None when the devices are not all visible (the planner then assumes a fully connected node)."""
-    if not torch.cuda.is_available() or torch.cuda.device_count() < world:
+def rocm_smi_bus_ids():
+    """rocm-smi GPU index -> PCI bus id (``rocm-smi --showbus``), {} when unavailable. rocm-smi numbers the GPUs
+    of the whole node and ignores HIP_VISIBLE_DEVICES, so its indices are matched to HIP devices by bus id."""
+    exe = shutil.which("rocm-smi")
+    if not exe:
+        return {}
+    try:
+        txt = subprocess.run([exe, "--showbus"], capture_output=True, text=True, timeout=20).stdout
+    except Exception:  # pragma: no cover - tool missing / restricted
+        return {}
+    return parse_showbus(txt)
+
+
+def parse_showbus(txt: str) -> dict:
+    out = {}
+    for l in txt.splitlines():
+        m = re.match(r"^\s*GPU\[(\d+)\]\s*:\s*PCI Bus:\s*([0-9A-Fa-f:.]+)", l)
+        if m:
+            out[int(m.group(1))] = normalize_bus_id(m.group(2))
+    return out
+
+
+def normalize_bus_id(b: str) -> str:
+    """'0000:05:00.0' / '05:00.0' -> '05:00' (domain and function dropped: one GPU per bus on a node)."""
+    parts = b.strip().lower().split(":")
+    if len(parts) >= 3:
+        parts = parts[-2:]
+    return f"{int(parts[0], 16):02x}:{int(parts[1].split('.')[0], 16):02x}"
+
+
+def device_bus_id(index: int) -> str | None:
+    """PCI bus id of HIP device ``index`` (as the current process numbers it), normalised."""
+    if not torch.cuda.is_available():
         return None
-    peer = peer_matrix()
-    types = rocm_smi_links()
+    p = torch.cuda.get_device_properties(index)
+    try:
+        return f"{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}"
+    except (AttributeError, TypeError, ValueError):  # pragma: no cover - older torch
+        return None
+
+
+def link_matrix_for(bus_ids, peer=None, types=None, smi_bus=None):
+    """Direct-link matrix between the GPUs of the ranks (rank r runs on the GPU with PCI bus id ``bus_ids[r]``):
+    links[a][b] = 1 when a reaches b over xGMI — rocm-smi's link type when it reports one for that pair (XGMI),
+    else ``peer[a][b]`` (HIP peer access between the ranks' devices) when given. None when the ranks' GPUs cannot
+    be identified (the planner then assumes a fully connected node). Ranks that share a GPU are linked."""
+    world = len(bus_ids)
+    if world == 0 or any(b is None for b in bus_ids):
+        return None
+    types = rocm_smi_links() if types is None else types
+    smi_bus = rocm_smi_bus_ids() if smi_bus is None else smi_bus
+    smi_of = {b: i for i, b in smi_bus.items()}
     out = [[0] * world for _ in range(world)]
     for a in range(world):
         for b in range(world):
             if a == b:
                 continue
-            t = types.get((a, b))
-            out[a][b] = int(t.upper() == "XGMI") if t else int(peer[a][b])
+            if bus_ids[a] == bus_ids[b]:
+                out[a][b] = 1
+                continue
+            ia, ib = smi_of.get(bus_ids[a]), smi_of.get(bus_ids[b])
+            t = types.get((ia, ib)) if ia is not None and ib is not None else None
+            if t:
+                out[a][b] = int(t.upper() == "XGMI")
+            elif peer is not None:
+                out[a][b] = int(bool(peer[a][b]))
+            else:
+                return None
     return out
+
+
+def link_matrix(world: int, devices=None):
+    """Direct-link matrix of the GPUs of ``world`` ranks of ONE process view: rank r runs on HIP device
+    ``devices[r]`` (default r). None when those devices are not all visible. For a multi-process job use
+    :func:`agreed_link_matrix`, which makes every rank use rank 0's answer."""
+    devices = list(range(world)) if devices is None else list(devices)
+    if not torch.cuda.is_available() or max(devices) >= torch.cuda.device_count():
+        return None
+    pm = peer_matrix()
+    peer = [[pm[devices[a]][devices[b]] for b in range(world)] for a in range(world)]
+    return link_matrix_for([device_bus_id(d) for d in devices], peer=peer)
+
+
+def agreed_link_matrix(world: int):
+    """The link matrix every rank of the default process group uses: each rank reports the PCI bus id of its own
+    device; rank 0 derives the matrix (rocm-smi link types of those GPUs, else peer access from its view) and
+    broadcasts it, so all ranks plan the SAME rings even if their local tool calls would disagree (a timed-out
+    or restricted rocm-smi on one rank would otherwise give that rank different rings and mismatched peers)."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() == world):
+        return link_matrix(world)
+    bus = [None] * world
+    dist.all_gather_object(bus, device_bus_id(torch.cuda.current_device()) if torch.cuda.is_available() else None)
+    obj = [None]
+    if dist.get_rank() == 0:
+        peer = None
+        if torch.cuda.is_available():  # peer access from rank 0's view, for the devices it can see
+            local = {device_bus_id(i): i for i in range(torch.cuda.device_count())}
+            if all(b in local for b in bus):
+                pm = peer_matrix()
+                peer = [[pm[local[a]][local[b]] for b in bus] for a in bus]
+        obj = [{"links": link_matrix_for(bus, peer=peer), "bus_ids": bus}]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]["links"]
 
 
 def ring_orders(world: int, max_rings: int | None = None, links=None):

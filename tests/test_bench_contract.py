@@ -69,3 +69,16 @@ def test_bench_self_launches_ranks(tmp_path):
     ref = rec["extra"]["mb8"]
     assert ref["global_batch"] == 16 and ref["samples_per_s"] > 0
     assert "effective_allreduce_algo_bw_GBps" not in rec["extra"]
+
+
+def test_bench_watchdog_ends_a_hung_run(tmp_path):
+    """A rank that stops taking part (test hook FAN_BENCH_STALL_RANK) leaves its peer blocked in a collective:
+    the per-phase watchdog ends the whole job non-zero within its budget and reports which phase hung."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--mb-per-gpu", "16", "--ref-mb", "0", "--timeout", "15"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", FAN_BENCH_STALL_RANK="1",
+               FAN_BENCH_STALL_S="600")
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0 and not _json_lines(r.stdout)
+    assert "phase 'warmup timed mb=16' exceeded 15 s" in r.stderr, r.stderr[-3000:]
