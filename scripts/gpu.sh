@@ -14,6 +14,7 @@
 #   pmc=<c1,c2,...>[:<args>]  ONE rocprofv3 --pmc pass (counters within the per-block slot limits) over a bench run
 #   py=<script> [args]        any python tool / probe in the tree (e.g. py=bench/gemm_bench.py --shapes mlp)
 #   sh=<command>              a shell command (non-GPU post-processing, listings)
+#   env=<NAME>=<value>        export a variable for the following steps (unenv=<NAME> removes it): in-call A/B
 #
 # Knobs: T_TEST, T_BENCH, T_PROF, T_PY (seconds; defaults 600 / 300 / 300 / 300).
 set -o pipefail
@@ -59,6 +60,10 @@ for step in "$@"; do
     sh)
       bash -c "$arg" > "$log" 2>&1; rc=$?; tail -25 "$log" | cut -c1-400
       [ $rc -eq 0 ] || exit $rc ;;
+    env)
+      export "$arg"; echo "  export $arg" ;;
+    unenv)
+      unset "$arg"; echo "  unset $arg" ;;
     *)
       echo "[gpu.sh] unknown step '$name'"; exit 2 ;;
   esac
