@@ -31,10 +31,11 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     for (int i = 0; i < world; ++i) orders_[0][i] = i;
   }
   inline_ = world == 1 && !cfg.force_comm;
+  bool side_epi = false;
   if (inline_) {
     const char* se = std::getenv("FAN_SIDE_EPI");
-    side_epi_ = cfg.side_epilogue >= 0 ? cfg.side_epilogue > 0 : (se && se[0] == '1');
-    if (side_epi_) FAN_HIP_CHECK(hipStreamCreateWithPriority(&epi_stream_, hipStreamNonBlocking, 0));
+    side_epi = cfg.side_epilogue >= 0 ? cfg.side_epilogue > 0 : (se && se[0] == '1');
+    if (side_epi) FAN_HIP_CHECK(hipStreamCreateWithPriority(&epi_stream_, hipStreamNonBlocking, 0));
   }
   if (cfg_.chunk_elems <= 0) {
     const char* ce = std::getenv("FAN_CHUNK_ELEMS");
@@ -60,7 +61,8 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     if (!std::strcmp(f, "system")) evf |= hipEventReleaseToSystem;
     else if (!std::strcmp(f, "device")) evf |= hipEventReleaseToDevice;
   }
-  if (const char* ld = std::getenv("FAN_LAZY_DONE")) lazy_done_ = ld[0] != '0';
+  bool lazy_done = true;
+  if (const char* ld = std::getenv("FAN_LAZY_DONE")) lazy_done = ld[0] != '0';
   const char* ve = std::getenv("FAN_VERIFY");
   verify_ = cfg.verify >= 0 ? cfg.verify > 0 : (ve && ve[0] == '1');
   if (verify_) {
@@ -70,14 +72,28 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     FAN_HIP_CHECK(hipHostMalloc(&verr_host_, sizeof(VerifyError), hipHostMallocDefault));
     std::memset(verr_host_, 0, sizeof(VerifyError));
   }
-  for (auto& s : slots_) {
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.ready, evf));
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.update, evf));
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.comm_done, evf));
-    FAN_HIP_CHECK(hipEventCreateWithFlags(&s.done, evf));
-    FAN_HIP_CHECK(hipEventCreate(&s.t0));
-    FAN_HIP_CHECK(hipEventCreate(&s.t1));
+  // request-slot state machine (slot_table.h): per slot the ready / update / comm_done / done events
+  slot_events_.resize((size_t)kSlots * 4);
+  for (auto& e : slot_events_) FAN_HIP_CHECK(hipEventCreateWithFlags(&e, evf));
+  for (auto& x : extra_) {
+    FAN_HIP_CHECK(hipEventCreate(&x.t0));
+    FAN_HIP_CHECK(hipEventCreate(&x.t1));
   }
+  dev_.host_words = flags_host_;
+  dev_.dev_words = flags_dev_;
+  SlotTable<HipSlotDevice>::Config tc;
+  tc.inline_mode = inline_;
+  tc.side_epi = side_epi;
+  tc.lazy_done = lazy_done;
+  tc.comm = stream_;
+  tc.side = epi_stream_;
+  table_ = std::make_unique<SlotTable<HipSlotDevice>>(dev_, tc, slot_events_);
+  table_->on_forced_commit = [this](int) { counters_.forced_commits++; };
+  table_->on_epilogue = [this](int slot, hipStream_t es) {  // the epilogue's end: timing / trace points
+    const SlotExtra& x = extra_[slot];
+    if (x.timed) FAN_HIP_CHECK(hipEventRecord(x.t1, es));
+    if (x.trace >= 0) FAN_HIP_CHECK(hipEventRecord(trace_pool_[x.trace].ev[kTpEpiEnd], es));
+  };
 }
 
 AllReduceEngine::~AllReduceEngine() {
@@ -85,15 +101,12 @@ AllReduceEngine::~AllReduceEngine() {
   hipStreamSynchronize(aux_stream_);
   for (auto& row : cev_)
     for (auto& e : row) hipEventDestroy(e);
-  for (auto& s : slots_) {
-    if (s.done_lazy) hipEventRecord(s.done, s.epi_stream);
-    hipEventSynchronize(s.done);  // epilogues may have run on a producer stream and still read the scratch
-    hipEventDestroy(s.ready);
-    hipEventDestroy(s.update);
-    hipEventDestroy(s.comm_done);
-    hipEventDestroy(s.done);
-    hipEventDestroy(s.t0);
-    hipEventDestroy(s.t1);
+  // epilogues may have run on a producer stream and still read the scratch
+  table_->for_each_used([](int, const SlotTable<HipSlotDevice>::Slot& sl) { hipEventSynchronize(sl.done); });
+  for (auto& e : slot_events_) hipEventDestroy(e);
+  for (auto& x : extra_) {
+    hipEventDestroy(x.t0);
+    hipEventDestroy(x.t1);
   }
   for (auto& t : trace_pool_)
     for (auto& e : t.ev) hipEventDestroy(e);
@@ -379,10 +392,10 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
     GallBuf& gb = gall_[k + "_" + std::to_string(C)];
     if (gb.free == nullptr) FAN_HIP_CHECK(hipEventCreateWithFlags(&gb.free, hipEventDisableTiming));
     if (gb.seq != 0) {
-      Slot& prev = slots_[gb.slot];
+      const auto& prev = table_->slot(gb.slot);
       if (prev.seq == gb.seq && prev.pending && gb.slot != epi_slot_) {
         counters_.forced_commits++;
-        commit_slot(prev, gb.slot, true, cur_producer_);
+        table_->commit(gb.slot, true, cur_producer_, gb.seq);
       }
       FAN_HIP_CHECK(hipStreamWaitEvent(A, gb.free, 0));  // recorded after that epilogue (no-op if it never ran)
     }
@@ -585,45 +598,29 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
                             const uint8_t* prepacked, int64_t prepacked_elems) {
   RoctxRange rr("fan/allreduce/submit");
   FAN_HIP_CHECK(hipSetDevice(device_));
-  req_seq_ = seq_ + 1;  // the sequence number this request will get (its messages' tags carry it)
-  const int slot = next_slot_;
-  next_slot_ = (slot + 1) % kSlots;
-  Slot& sl = slots_[slot];
-  // The slot still holds a request whose epilogue was never committed (more than kSlots requests deferred, e.g.
-  // a deep model whose trainer commits at the end of backward): commit it now, ordered after everything the
-  // producer has enqueued so far (the hardware analogue: the NIC's 8-deep command queue never drops a request).
-  if (sl.pending) {
-    counters_.forced_commits++;
-    commit_slot(sl, slot, true, producer);
-  }
+  // slot state machine (slot_table.h): the next slot (a still-deferred occupant is committed first, ordered after
+  // the producer: the NIC's 8-deep command queue never drops a request), ordering after anything that may still
+  // read the slot's buffers, and the stream this request's communication phase runs on
+  const SlotTable<HipSlotDevice>::Begin b = table_->begin(producer);
+  const int slot = b.slot;
+  req_seq_ = b.seq;  // the sequence number this request will get (its messages' tags carry it)
+  submitted_++;
   const EngineLayout L = layout(n_valid);
-  const hipStream_t run = inline_ ? producer : stream_;
-  // The slot's previous epilogue may have run on another stream than this request will (a world-1 side epilogue,
-  // or an epilogue committed on another producer stream) and may still read this slot's scratch, which this
-  // request is about to rewrite: order this request after it. (A multi-rank request waits for `ready` on the
-  // producer below, which already covers an epilogue enqueued there.)
-  if (sl.seq != 0 && sl.epi_stream != nullptr && sl.epi_stream != run && !(!inline_ && sl.epi_stream == producer)) {
-    ensure_done(sl);
-    FAN_HIP_CHECK(hipStreamWaitEvent(run, sl.done, 0));
-  }
   cur_producer_ = producer;
-  sl.stream = run_stream_ = run;
-  if (!inline_) {
-    FAN_HIP_CHECK(hipEventRecord(sl.ready, producer));
-    FAN_HIP_CHECK(hipStreamWaitEvent(stream_, sl.ready, 0));
-  }
-  sl.timed = timing_;
-  sl.counted = false;
-  if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t0, sl.stream));
+  run_stream_ = b.run;
+  SlotExtra& x = extra_[slot];
+  x.timed = timing_;
+  x.counted = false;
+  if (x.timed) FAN_HIP_CHECK(hipEventRecord(x.t0, run_stream_));
   const int64_t wb = wire_bytes(L);
   counters_.requests++;
   counters_.logical_bytes += n_valid * 4;
   counters_.wire_bytes += wb;
-  sl.trace = -1;
+  x.trace = -1;
   cur_trace_ = -1;
   if (tracing_) {
     if (trace_used_ < trace_pool_.size()) {
-      sl.trace = cur_trace_ = (int)trace_used_++;
+      x.trace = cur_trace_ = (int)trace_used_++;
       trace_pool_[cur_trace_].logical_bytes = n_valid * 4;
       trace_pool_[cur_trace_].wire_bytes = wb;
       mark(kTpStart);
@@ -640,9 +637,10 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   epi_slot_ = slot;
   cur_defer_ = defer;
   trace_marked_ = 1u << kTpStart;
-  sl.thunks = cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum,
-                                        prepacked, prepacked_elems)
-                             : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
+  std::vector<EpiThunk> thunks =
+      cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum, prepacked,
+                                prepacked_elems)
+                     : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
   FAN_HIP_CHECK(hipGetLastError());
   // phases this schedule does not have (ring hops, the world-1 local path) collapse onto the end of comm
   for (int tp = kTpPacked; tp <= kTpCommEnd; ++tp)
@@ -650,82 +648,20 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   // verify mode: the device error block's host mirror, refreshed after every request's communication phase
   if (verify_) FAN_HIP_CHECK(hipMemcpyAsync(verr_host_, verr_dev_, sizeof(VerifyError), hipMemcpyDeviceToHost, run_stream_));
   cur_trace_ = -1;
-  // end of this request's communication phase: what an epilogue on the producer stream waits for
-  if (!inline_) FAN_HIP_CHECK(hipEventRecord(sl.comm_done, stream_));
-  sl.pending = true;
-  sl.seq = ++seq_;
-  sl.t_issue = now_s();
-  if (!defer) commit_slot(sl, slot, false, nullptr);
+  x.t_issue = now_s();
+  table_->set_keep_done(slot, x.timed || x.trace >= 0);  // timed / traced: a real done point, not a lazy one
+  table_->end(slot, std::move(thunks), defer);  // comm_done, sequence number; an immediate request commits now
   return slot;
 }
 
 void AllReduceEngine::commit(int slot, bool after_producer, hipStream_t producer, uint32_t seq) {
-  Slot& sl = slots_.at(slot);
-  if (seq != 0 && seq != sl.seq) return;  // superseded: committed when its slot was reused
-  commit_slot(sl, slot, after_producer, producer);
-}
-
-void AllReduceEngine::commit_slot(Slot& sl, int slot, bool after_producer, hipStream_t producer) {
-  if (!sl.pending) return;
   RoctxRange rr("fan/allreduce/epilogue");
-  sl.epi_stream = sl.stream;
-  if (epi_on_producer_ && !inline_ && after_producer && producer != sl.stream) {
-    // Epilogue on the producer (compute) stream: it waits for the request's communication phase, then the
-    // decode+SGD runs there, ordered after everything already enqueued on it and not concurrently with
-    // the producer's GEMMs (a side-stream epilogue takes CU slots from their tiles).
-    FAN_HIP_CHECK(hipStreamWaitEvent(producer, sl.comm_done, 0));
-    sl.epi_stream = producer;
-  } else if (side_epi_ && after_producer) {
-    // world 1: the request has no communication phase (it ran in the producer's order); its decode + SGD runs on
-    // the side stream after everything the producer has enqueued so far, beside the producer's next GEMMs
-    FAN_HIP_CHECK(hipEventRecord(sl.update, producer));
-    FAN_HIP_CHECK(hipStreamWaitEvent(epi_stream_, sl.update, 0));
-    sl.epi_stream = epi_stream_;
-  } else if (after_producer && producer != sl.stream) {
-    // inline requests already run on the producer's stream: stream order is the dependency
-    FAN_HIP_CHECK(hipEventRecord(sl.update, producer));
-    FAN_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.update, 0));
-  }
-  for (auto& t : sl.thunks) t(sl.epi_stream);
-  sl.thunks.clear();
-  if (sl.timed) FAN_HIP_CHECK(hipEventRecord(sl.t1, sl.epi_stream));
-  if (sl.trace >= 0) FAN_HIP_CHECK(hipEventRecord(trace_pool_[sl.trace].ev[kTpEpiEnd], sl.epi_stream));
-  // Side-stream requests: completion word written by the GPU into host-mapped memory (the NIC's "write 1 to
-  // done_addr + done_id"). Requests finishing on the critical compute stream (inline, or epilogue on the
-  // producer) skip the extra packet there: their completion is the done event.
-  if (sl.epi_stream == sl.stream && !inline_)
-    FAN_HIP_CHECK(hipStreamWriteValue32(sl.stream, flags_dev_ + slot * 16, sl.seq, 0));
-  sl.done_lazy = lazy_done_ && inline_ && sl.epi_stream == sl.stream && !sl.timed && sl.trace < 0;
-  if (!sl.done_lazy) FAN_HIP_CHECK(hipEventRecord(sl.done, sl.epi_stream));
-  sl.pending = false;
+  table_->commit(slot, after_producer, producer, seq);
 }
 
-void AllReduceEngine::wait_stream(int slot, hipStream_t s, uint32_t seq) {
-  Slot& sl = slots_.at(slot);
-  // A superseded request (seq != slot's) was committed at reuse. If the newer request is still pending, the
-  // slot's done event still marks the old request's completion; otherwise it marks the newer one, which is
-  // later in every stream order the old request shares (a conservative wait). Never commit the newer one here.
-  const bool own = seq == 0 || seq == sl.seq;
-  if (own && sl.pending) commit_slot(sl, slot, true, s);
-  if (s != sl.epi_stream || !own) {
-    ensure_done(sl);
-    FAN_HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
-  }
-}
+void AllReduceEngine::wait_stream(int slot, hipStream_t s, uint32_t seq) { table_->wait_stream(slot, s, seq); }
 
-bool AllReduceEngine::query(int slot, uint32_t seq) {
-  Slot& sl = slots_.at(slot);
-  ensure_done(sl);  // a lazily recorded done event (this request's, or a superseded one's: conservative)
-  if (seq != 0 && seq != sl.seq) {
-    // superseded request: its completion is the slot's done event while the newer request is pending, and is
-    // implied by the done word / done event of the newer one otherwise
-    if (!inline_ && ((flags_host_[slot * 16] - seq) & 0xFFFFFFFFu) < (1u << 31)) return true;
-    return hipEventQuery(sl.done) == hipSuccess;
-  }
-  if (sl.pending) return false;
-  if (inline_ || sl.epi_stream != sl.stream) return hipEventQuery(sl.done) == hipSuccess;
-  return flags_host_[slot * 16] == sl.seq;
-}
+bool AllReduceEngine::query(int slot, uint32_t seq) { return table_->query(slot, seq); }
 
 void AllReduceEngine::set_tracing(bool on, int capacity) {
   tracing_ = on;
@@ -746,7 +682,7 @@ TraceSummary AllReduceEngine::trace_summary() {
   TraceSummary r;
   r.dropped = trace_dropped_;
   for (int s = 0; s < kSlots; ++s)  // traced epilogues still deferred: their end point is not recorded yet
-    if (slots_[s].pending && slots_[s].trace >= 0)
+    if (table_->slot(s).pending && extra_[s].trace >= 0)
       throw std::runtime_error("trace_summary: a traced request's epilogue is not committed yet");
   for (size_t i = 0; i < trace_used_; ++i) {
     RequestTrace& t = trace_pool_[i];
@@ -780,16 +716,18 @@ std::string AllReduceEngine::debug_status() {
   std::ostringstream os;
   os << "{\"rank\": " << rank_ << ", \"world\": " << world_ << ", \"algo\": \"" << (cfg_.algo ? "ring" : "mesh")
      << "\", \"codec\": " << cfg_.codec << ", \"inline\": " << (inline_ ? "true" : "false")
-     << ", \"verify\": " << (verify_ ? "true" : "false") << ", \"requests\": " << seq_
-     << ", \"next_slot\": " << next_slot_ << ", \"slots\": [";
+     << ", \"verify\": " << (verify_ ? "true" : "false") << ", \"requests\": " << submitted_
+     << ", \"next_slot\": " << table_->next_slot() << ", \"slots\": [";
   for (int i = 0; i < kSlots; ++i) {
-    const Slot& sl = slots_[i];
+    const auto& sl = table_->slot(i);
     os << (i ? ", " : "") << "{\"slot\": " << i << ", \"seq\": " << sl.seq << ", \"pending\": "
        << (sl.pending ? "true" : "false") << ", \"done_word\": " << flags_host_[i * 16]
        << ", \"epilogue_stream\": \""
-       << (sl.epi_stream == nullptr ? "none" : sl.epi_stream == stream_ ? "comm" : sl.epi_stream == epi_stream_ ? "side"
-                                                                                 : "producer")
-       << "\", \"age_s\": " << (sl.seq ? now_s() - sl.t_issue : 0.0) << "}";
+       << (!sl.used || sl.pending ? "none"
+           : sl.epi_stream == stream_ ? "comm"
+           : (epi_stream_ && sl.epi_stream == epi_stream_) ? "side"
+                                                             : "producer")
+       << "\", \"age_s\": " << (sl.seq ? now_s() - extra_[i].t_issue : 0.0) << "}";
   }
   os << "], \"forced_commits\": " << counters_.forced_commits << ", \"direct_rounds\": " << counters_.direct_rounds
      << ", \"peer_bytes\": [";
@@ -822,18 +760,17 @@ std::string AllReduceEngine::debug_status() {
 }
 
 std::string AllReduceEngine::diagnostics(int slot) const {
-  const Slot& sl = slots_.at(slot);
+  const auto& sl = table_->slot(slot);
   std::ostringstream os;
   os << "rank=" << rank_ << " world=" << world_ << " algo=" << (cfg_.algo ? "ring" : "mesh") << " codec=" << cfg_.codec
      << " slot=" << slot << " seq=" << sl.seq << " done_word=" << flags_host_[slot * 16]
-     << " elapsed=" << (now_s() - sl.t_issue) << "s";
+     << " elapsed=" << (now_s() - extra_.at(slot).t_issue) << "s";
   if (comm_) os << " rccl_async_error='" << comm_->async_error() << "'";
   return os.str();
 }
 
 void AllReduceEngine::synchronize(int slot, double timeout_s, uint32_t seq) {
-  Slot& sl = slots_.at(slot);
-  if ((seq == 0 || seq == sl.seq) && sl.pending) commit_slot(sl, slot, false, nullptr);
+  table_->commit_for_host_wait(slot, seq);
   const double t0 = now_s();
   const double tmo = timeout_s > 0 ? timeout_s : cfg_.timeout_s;
   int spins = 0;
@@ -884,7 +821,7 @@ void AllReduceEngine::check_verify() {
 }
 
 float AllReduceEngine::latency_ms(int slot) {
-  Slot& sl = slots_.at(slot);
+  SlotExtra& sl = extra_.at(slot);
   if (!sl.timed) return -1.f;
   synchronize(slot);
   float ms = 0.f;

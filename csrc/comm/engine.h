@@ -23,6 +23,7 @@
 #include "bfp/bfp_format.h"
 #include "comm/native_comm.h"
 #include "comm/planner.h"
+#include "comm/slot_table.h"
 #include "comm/verify.h"
 
 namespace fan {
@@ -102,9 +103,29 @@ struct TraceSummary {
 // Deferred epilogue of a request (decode + SGD), launched on the given stream at commit().
 using EpiThunk = std::function<void(hipStream_t)>;
 
+// The HIP device policy of the request-slot state machine (slot_table.h): events, stream waits, and the done
+// words the GPU writes into host-mapped memory (one 64-B line per slot).
+struct HipSlotDevice {
+  using Stream = hipStream_t;
+  using Event = hipEvent_t;
+  volatile uint32_t* host_words = nullptr;
+  uint32_t* dev_words = nullptr;
+  void record(Event e, Stream s) { FAN_HIP_CHECK(hipEventRecord(e, s)); }
+  void wait(Stream s, Event e) { FAN_HIP_CHECK(hipStreamWaitEvent(s, e, 0)); }
+  bool query(Event e) {
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipSuccess) (void)hipGetLastError();  // not-ready is not an error
+    return r == hipSuccess;
+  }
+  void write_done(Stream s, int slot, uint32_t seq) {
+    FAN_HIP_CHECK(hipStreamWriteValue32(s, dev_words + slot * 16, seq, 0));
+  }
+  uint32_t read_done(int slot) { return host_words[slot * 16]; }
+};
+
 class AllReduceEngine {
  public:
-  static constexpr int kSlots = 8;
+  static constexpr int kSlots = SlotTable<HipSlotDevice>::kSlots;
 
   AllReduceEngine(Comm* comm, int rank, int world, EngineConfig cfg, int device);
   ~AllReduceEngine();
@@ -113,7 +134,7 @@ class AllReduceEngine {
   const std::vector<std::vector<int>>& orders() const { return orders_; }
   hipStream_t stream() const { return stream_; }
   Comm* comm() const { return comm_; }
-  bool is_inline() const { return inline_; }
+  bool is_inline() const { return table_->config().inline_mode; }
   int codec() const { return cfg_.codec; }
 
   // Enqueue the communication phase of a request. grad: padded flat buffer (f32 or bf16) ready on `producer`.
@@ -137,7 +158,7 @@ class AllReduceEngine {
   void wait_stream(int slot, hipStream_t s, uint32_t seq = 0);  // GPU-side wait
   bool query(int slot, uint32_t seq = 0);                       // host: request done?
   uint32_t done_word(int slot) const { return flags_host_[slot * 16]; }  // last completed sequence number
-  uint32_t slot_seq(int slot) const { return slots_.at(slot).seq; }
+  uint32_t slot_seq(int slot) const { return table_->slot(slot).seq; }
   void synchronize(int slot, double timeout_s = -1.0, uint32_t seq = 0);  // host: bounded wait (throws)
   float latency_ms(int slot);
   void set_timing(bool on) { timing_ = on; }
@@ -148,9 +169,9 @@ class AllReduceEngine {
   TraceSummary trace_summary();
   // Side-stream engine: run each request's epilogue on the stream passed to commit() (after its communication
   // phase) instead of on the comm stream.
-  void set_epilogue_on_producer(bool on) { epi_on_producer_ = on; }
-  bool epilogue_on_producer() const { return epi_on_producer_; }
-  bool side_epilogue() const { return side_epi_; }
+  void set_epilogue_on_producer(bool on) { table_->set_epi_on_producer(on); }
+  bool epilogue_on_producer() const { return table_->config().epi_on_producer; }
+  bool side_epilogue() const { return table_->config().side_epi; }
   std::string diagnostics(int slot) const;
   // Debug snapshot (the NIC's debug_status register, hw/all_reduce.sv:1415-1421), JSON: engine configuration,
   // every slot (sequence, pending epilogue, done word, stream kind), counters, the communicator's async error and,
@@ -161,7 +182,7 @@ class AllReduceEngine {
   void check_verify();
   // test-only fault injection (FAN_FAULT grammar, see verify.h); replaces the rules taken from the environment
   void set_fault(const std::string& spec) { fault_ = FaultInjector(spec); }
-  uint64_t requests() const { return seq_; }
+  uint64_t requests() const { return submitted_; }
   const EngineCounters& counters() const { return counters_; }
   void reset_counters() { counters_ = EngineCounters{}; }
   int64_t wire_bytes(const EngineLayout& L) const;
@@ -173,29 +194,21 @@ class AllReduceEngine {
   }
 
  private:
-  struct Slot {
-    hipEvent_t ready = nullptr, update = nullptr, comm_done = nullptr, done = nullptr, t0 = nullptr, t1 = nullptr;
-    uint32_t seq = 0;
-    bool pending = false;   // epilogue not yet committed
+  // Per-slot engine data beside the state machine (slot_table.h holds sequence / pending / streams / events).
+  struct SlotExtra {
+    hipEvent_t t0 = nullptr, t1 = nullptr;
     bool timed = false;
     bool counted = false;   // device time already added to counters_
-    hipStream_t stream = nullptr;  // stream the request runs on (comm stream, or the producer when inline)
-    hipStream_t epi_stream = nullptr;  // stream the epilogue was enqueued on (== stream unless epi_on_producer_)
-    std::vector<EpiThunk> thunks;
     double t_issue = 0.0;
     int trace = -1;  // index into trace_pool_ (-1: not traced)
-    bool done_lazy = false;  // inline request: `done` is recorded only when a host query / other stream needs it
   };
-  // Inline requests complete in their producer's stream order, so nothing needs their done event unless the host
-  // polls it or another stream waits on it: record it then (later in that stream = a conservative completion point).
-  // An event marker after every inline epilogue left the GPU idle ~5.5 us before the next GEMM (3x per step,
-  // profiles/r2_lazy_done_event.txt).
-  void ensure_done(Slot& sl) {
-    if (!sl.done_lazy) return;
-    FAN_HIP_CHECK(hipEventRecord(sl.done, sl.epi_stream));
-    sl.done_lazy = false;
-  }
-  bool lazy_done_ = true;  // FAN_LAZY_DONE=0: record every request's done event at commit
+  std::array<SlotExtra, kSlots> extra_;
+  // Inline requests record their done event lazily (only when a host query / other stream needs it): an event
+  // marker after every inline epilogue left the GPU idle ~5.5 us before the next GEMM (3x per step,
+  // profiles/r2_lazy_done_event.txt). FAN_LAZY_DONE=0 records every request's done event at commit.
+  HipSlotDevice dev_;
+  std::unique_ptr<SlotTable<HipSlotDevice>> table_;
+  std::vector<hipEvent_t> slot_events_;
   struct RequestTrace {
     hipEvent_t ev[kTpCount] = {};
     int64_t logical_bytes = 0, wire_bytes = 0;
@@ -205,7 +218,6 @@ class AllReduceEngine {
     trace_marked_ |= 1u << tp;
     if (cur_trace_ >= 0) FAN_HIP_CHECK(hipEventRecord(trace_pool_[cur_trace_].ev[tp], run_stream_));
   }
-  void commit_slot(Slot& sl, int slot, bool after_producer, hipStream_t producer);
   void count_peers(size_t bytes, P2PComm* direct = nullptr);  // `bytes` sent to every other rank
   uint8_t* scratch(const std::string& key, size_t bytes);
   std::vector<EpiThunk> run_mesh(const EngineLayout& L, const void* grad, int gdt, float* master,
@@ -228,19 +240,15 @@ class AllReduceEngine {
   hipStream_t stream_ = nullptr;
   hipStream_t aux_stream_ = nullptr;  // chunked mesh: owner reduces + per-chunk epilogues beside the collectives
   hipStream_t epi_stream_ = nullptr;  // world-1 side epilogues (normal priority: the producer's GEMMs keep theirs)
-  bool side_epi_ = false;
   hipEvent_t cev_[4][2] = {};         // chunked mesh pipeline events: [all-to-all, reduce, all-gather, epilogue][parity]
-  bool epi_on_producer_ = false;
   // world 1 without forced collectives: nothing to overlap, so requests run inline on the producer's
   // stream (no cross-stream event packets); run_stream_ is the stream of the request being issued.
   bool inline_ = false;
   hipStream_t run_stream_ = nullptr;
-  std::array<Slot, kSlots> slots_;
   volatile uint32_t* flags_host_ = nullptr;  // host-mapped done words (one 64-B line per slot)
   uint32_t* flags_dev_ = nullptr;
-  uint32_t seq_ = 0;
-  int next_slot_ = 0;
   bool timing_ = false;
+  uint64_t submitted_ = 0;
   EngineCounters counters_;
   std::map<std::string, std::pair<uint8_t*, size_t>> scratch_;
   int epi_slot_ = 0;  // slot of the request being built

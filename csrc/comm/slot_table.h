@@ -1,0 +1,241 @@
+// Request-slot state machine of the all-reduce engine, free of HIP: the host-side logic that decides which stream
+// waits for which event, when a deferred epilogue is committed and on which stream, when a request counts as done.
+//
+// Reference behaviour: the NIC accepts at most 8 requests, processes them in
+// order and signals each by writing 1 to done_addr + done_id, done_id cycling 0..7 (hw/all_reduce.sv:1228,
+// 1368-1375; sw/mlp_mpi_example_f32.cpp:114-180). Here a request is (a) a communication phase enqueued at submit and
+// (b) a decode + SGD epilogue that may be DEFERRED until the producer's remaining work (the bwd-data GEMM that still
+// reads the weights) is enqueued; completion is a 32-bit sequence number the GPU writes into host-mapped memory.
+//
+// The class is a template over a device policy D so the same code runs on HIP (engine.cpp) and on a simulated
+// device with random stream interleavings under AddressSanitizer / UBSan (tests/native/slot_table_selftest.cpp).
+// D provides:
+//   using Stream; using Event;                           (Stream values compare by identity; any value is a real
+//                                                         stream, including the null/legacy stream 0)
+//   void record(Event, Stream); void wait(Stream, Event); bool query(Event);
+//   void write_done(Stream, int slot, uint32_t seq);     GPU writes the done word of a slot, stream-ordered
+//   uint32_t read_done(int slot);                        host read of that word
+//
+// Invariants (checked by the self-test):
+//   I1 a request's epilogue runs after its own communication phase and, when committed "after the producer",
+//      after everything the producer stream had enqueued at commit time;
+//   I2 a slot's buffers are not rewritten by a new request while the previous request's epilogue on that slot
+//      (wherever it runs) may still read them;
+//   I3 query()/synchronize() report a request done only once its epilogue has executed; wait_stream(s) orders
+//      stream s after it; both stay correct for a handle whose slot has since been reused (superseded), and across
+//      the 32-bit sequence wrap-around;
+//   I4 more than kSlots deferred requests never drop one: the oldest is committed when its slot is needed.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <functional>
+#include <stdexcept>
+#include <vector>
+
+namespace fan {
+
+template <class D>
+class SlotTable {
+ public:
+  using Stream = typename D::Stream;
+  using Event = typename D::Event;
+  using Thunk = std::function<void(Stream)>;
+  static constexpr int kSlots = 8;
+
+  struct Config {
+    bool inline_mode = false;     // world 1, no collectives: requests run in the producer's stream order
+    bool epi_on_producer = false; // multi-rank: epilogue on the committing (compute) stream after comm_done
+    bool side_epi = false;        // world 1: epilogue on the side stream after the producer's enqueued work
+    bool lazy_done = true;        // inline: record the done event only when something needs it
+    Stream comm{};                // the engine's communication stream (multi-rank)
+    Stream side{};                // the world-1 side-epilogue stream (side_epi)
+  };
+
+  struct Slot {
+    Event ready{}, update{}, comm_done{}, done{};
+    uint32_t seq = 0;
+    bool pending = false;        // epilogue not yet committed
+    bool used = false;           // has held a request
+    Stream stream{};             // stream the communication phase ran on
+    Stream epi_stream{};         // stream the epilogue was enqueued on
+    bool done_lazy = false;      // inline request whose done event is not recorded yet
+    bool keep_done = false;      // the engine times / traces this request: record its done event at commit
+    std::vector<Thunk> thunks;
+  };
+
+  // hooks the engine uses for its timing / tracing events (called on the epilogue stream, after the thunks)
+  std::function<void(int slot, Stream epi)> on_epilogue;
+  // called when a deferred request is force-committed because its slot is needed (> kSlots deferred)
+  std::function<void(int slot)> on_forced_commit;
+
+  SlotTable(D& dev, Config cfg, const std::vector<Event>& events) : dev_(dev), cfg_(cfg) {
+    if (events.size() != (size_t)kSlots * 4) throw std::invalid_argument("SlotTable: need 4 events per slot");
+    for (int i = 0; i < kSlots; ++i) {
+      slots_[i].ready = events[i * 4 + 0];
+      slots_[i].update = events[i * 4 + 1];
+      slots_[i].comm_done = events[i * 4 + 2];
+      slots_[i].done = events[i * 4 + 3];
+    }
+  }
+
+  const Config& config() const { return cfg_; }
+  void set_epi_on_producer(bool on) { cfg_.epi_on_producer = on && !cfg_.inline_mode; }
+  void set_seq(uint32_t s) { seq_ = s; }  // test hook: start near the 32-bit wrap-around
+  uint32_t last_seq() const { return seq_; }
+  int next_slot() const { return next_; }
+  const Slot& slot(int i) const { return slots_.at(i); }
+
+  // A new request from `producer`: takes the next slot (force-committing a still-deferred occupant), orders the
+  // request after anything that may still read that slot's buffers, and returns (slot, stream its communication
+  // phase runs on). For a multi-rank request the comm stream waits for the producer's work so far.
+  struct Begin {
+    int slot;
+    Stream run;
+    uint32_t seq;  // the sequence number this request will carry
+  };
+  Begin begin(Stream producer) {
+    const int s = next_;
+    next_ = (s + 1) % kSlots;
+    Slot& sl = slots_[s];
+    if (sl.pending) {  // I4: the 9th deferred request commits the oldest, ordered after the producer
+      if (on_forced_commit) on_forced_commit(s);
+      commit_slot(s, true, producer);
+    }
+    const Stream run = cfg_.inline_mode ? producer : cfg_.comm;
+    // I2: the slot's previous epilogue may run on another stream than this request and read this slot's
+    // buffers (a side epilogue, or one committed on another producer stream). A multi-rank request waits for
+    // `ready` on the producer below, which covers an epilogue enqueued there.
+    if (sl.used && !(sl.epi_stream == run) && !(!cfg_.inline_mode && sl.epi_stream == producer)) {
+      ensure_done(sl);
+      dev_.wait(run, sl.done);
+    }
+    sl.stream = run;
+    sl.keep_done = false;
+    if (!cfg_.inline_mode) {
+      dev_.record(sl.ready, producer);
+      dev_.wait(run, sl.ready);
+    }
+    return Begin{s, run, following(seq_)};
+  }
+
+  // The request's communication phase is enqueued (on Begin::run); `thunks` enqueue its epilogue on a given
+  // stream. Immediate requests commit now (in the comm stream's order).
+  uint32_t end(int s, std::vector<Thunk> thunks, bool defer) {
+    Slot& sl = slots_.at(s);
+    if (!cfg_.inline_mode) dev_.record(sl.comm_done, sl.stream);
+    sl.thunks = std::move(thunks);
+    sl.pending = true;
+    sl.used = true;
+    sl.seq = seq_ = following(seq_);
+    if (!defer) commit_slot(s, false, Stream{});
+    return sl.seq;
+  }
+
+  // Enqueue a deferred epilogue; `seq` (0: whoever holds the slot) names the request — a superseded handle's
+  // epilogue was committed when its slot was reused, so it never commits the newer request.
+  void commit(int s, bool after_producer, Stream producer, uint32_t seq = 0) {
+    Slot& sl = slots_.at(s);
+    if (seq != 0 && seq != sl.seq) return;
+    commit_slot(s, after_producer, producer);
+  }
+
+  // GPU-side: stream `st` waits for the request.
+  void wait_stream(int s, Stream st, uint32_t seq = 0) {
+    Slot& sl = slots_.at(s);
+    // A superseded request: if the newer one is still pending, the slot's done event still marks the old
+    // request's completion; otherwise it marks the newer one, later in every stream order the old request
+    // shares (a conservative wait). Never commit the newer request on the old handle's behalf.
+    const bool own = seq == 0 || seq == sl.seq;
+    if (own && sl.pending) commit_slot(s, true, st);
+    if (!(st == sl.epi_stream) || !own) {
+      ensure_done(sl);
+      dev_.wait(st, sl.done);
+    }
+  }
+
+  // Host: is the request done (its epilogue executed)?
+  bool query(int s, uint32_t seq = 0) {
+    Slot& sl = slots_.at(s);
+    ensure_done(sl);  // a lazily recorded done event (this request's, or a superseded one's: conservative)
+    if (seq != 0 && seq != sl.seq) {
+      // superseded: done if the newer request's done word has passed it (wrap-safe), else the slot's done event
+      if (!cfg_.inline_mode && ((dev_.read_done(s) - seq) & 0xFFFFFFFFu) < (1u << 31)) return true;
+      return dev_.query(sl.done);
+    }
+    if (sl.pending) return false;
+    if (cfg_.inline_mode || !(sl.epi_stream == sl.stream)) return dev_.query(sl.done);
+    return dev_.read_done(s) == sl.seq;
+  }
+
+  // commit an own pending request before a host wait (synchronize)
+  void commit_for_host_wait(int s, uint32_t seq) {
+    Slot& sl = slots_.at(s);
+    if ((seq == 0 || seq == sl.seq) && sl.pending) commit_slot(s, false, Stream{});
+  }
+
+  // Inline requests complete in their producer's stream order, so nothing needs their done event unless the host
+  // polls it or another stream waits on it: record it then (later in that stream = a conservative completion point).
+  void ensure_done(Slot& sl) {
+    if (!sl.done_lazy) return;
+    dev_.record(sl.done, sl.epi_stream);
+    sl.done_lazy = false;
+  }
+  void ensure_done(int s) { ensure_done(slots_.at(s)); }
+  void set_keep_done(int s, bool on) { slots_.at(s).keep_done = on; }
+
+  // destructor helper: every slot's epilogue that may still run
+  template <class F>
+  void for_each_used(F f) {
+    for (int i = 0; i < kSlots; ++i)
+      if (slots_[i].used) {
+        ensure_done(slots_[i]);
+        f(i, slots_[i]);
+      }
+  }
+
+ private:
+  // sequence numbers run 1, 2, ..., 2^32-1, 1, ...: 0 means "no request / whoever holds the slot"
+  static uint32_t following(uint32_t q) { return q == 0xFFFFFFFFu ? 1u : q + 1u; }
+
+  void commit_slot(int s, bool after_producer, Stream producer) {
+    Slot& sl = slots_[s];
+    if (!sl.pending) return;
+    sl.epi_stream = sl.stream;
+    if (cfg_.epi_on_producer && !cfg_.inline_mode && after_producer && !(producer == sl.stream)) {
+      // epilogue on the producer (compute) stream, after the request's communication phase: it runs after
+      // everything already enqueued there and never concurrently with the producer's GEMMs
+      dev_.wait(producer, sl.comm_done);
+      sl.epi_stream = producer;
+    } else if (cfg_.side_epi && after_producer) {
+      // world 1: no communication phase; decode + SGD on the side stream after the producer's enqueued work and
+      // after the request's own inline work (on the stream it was submitted from, when another stream commits)
+      dev_.record(sl.update, producer);
+      dev_.wait(cfg_.side, sl.update);
+      if (!(producer == sl.stream)) {
+        dev_.record(sl.comm_done, sl.stream);
+        dev_.wait(cfg_.side, sl.comm_done);
+      }
+      sl.epi_stream = cfg_.side;
+    } else if (after_producer && !(producer == sl.stream)) {
+      dev_.record(sl.update, producer);
+      dev_.wait(sl.stream, sl.update);
+    }
+    for (auto& t : sl.thunks) t(sl.epi_stream);
+    sl.thunks.clear();
+    if (on_epilogue) on_epilogue(s, sl.epi_stream);
+    // multi-rank requests finishing on the comm stream: the GPU writes the done word ("write 1 to done_addr +
+    // done_id"); requests finishing on the critical compute stream skip that packet: their completion is the event
+    if (sl.epi_stream == sl.stream && !cfg_.inline_mode) dev_.write_done(sl.stream, s, sl.seq);
+    sl.done_lazy = cfg_.lazy_done && cfg_.inline_mode && sl.epi_stream == sl.stream && !sl.keep_done;
+    if (!sl.done_lazy) dev_.record(sl.done, sl.epi_stream);
+    sl.pending = false;
+  }
+
+  D& dev_;
+  Config cfg_;
+  std::array<Slot, kSlots> slots_;
+  uint32_t seq_ = 0;
+  int next_ = 0;
+};
+
+}  // namespace fan

@@ -1,0 +1,281 @@
+// Host-only self-test of the engine's request-slot state machine (csrc/comm/slot_table.h), built with
+// AddressSanitizer + UndefinedBehaviorSanitizer by tests/test_native_sanitizers.py.
+//
+// The state machine runs against a SIMULATED device: streams are FIFO queues of operations (event record, event
+// wait, done-word write, labelled work), events follow HIP/CUDA semantics (a wait binds to the event's latest
+// record at the time the wait is enqueued; a never-recorded event is complete; re-recording replaces it), and the
+// "GPU" executes the heads of random runnable streams in random order. Random request traffic (immediate and
+// deferred requests, more than 8 deferred at once, commits after the producer, GPU-side waits, host queries of
+// current and superseded handles, two producer streams one of which is the null stream 0, sequence numbers that
+// wrap around 2^32) is driven through every engine mode (inline with lazy / eager done events, inline with side
+// epilogues, multi-rank with the epilogue on the comm stream or on the producer). Checked on every run:
+//   I1 epilogue after its own communication phase, and after all producer work enqueued before its commit;
+//   I2 a slot's buffer is not rewritten by the next request before the previous epilogue on that slot has read it;
+//   I3 a handle that query() reports done has its epilogue executed; work a stream enqueues after wait_stream()
+//      runs after that epilogue;
+//   I4 every request's epilogue runs exactly once, and the device always drains (no deadlock).
+#include <cstdio>
+#include <map>
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "comm/slot_table.h"
+
+using namespace fan;
+
+static int failures = 0;
+#define EXPECT(c, ...)                                          \
+  do {                                                          \
+    if (!(c)) {                                                 \
+      if (failures < 30) {                                      \
+        std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+        std::fprintf(stderr, __VA_ARGS__);                      \
+        std::fprintf(stderr, "\n");                             \
+      }                                                         \
+      ++failures;                                               \
+    }                                                           \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------- simulated device
+struct Op {
+  enum Kind { kRecord, kWait, kWrite, kWork } kind;
+  int ev = -1;
+  long inst = 0;         // record: the instance id; wait: the instance it waits for (0: nothing)
+  int slot = -1;
+  uint32_t seq = 0;
+  long work = -1;        // work id
+};
+
+struct SimDevice {
+  using Stream = int;
+  using Event = int;
+  int n_streams;
+  std::vector<std::vector<Op>> q;
+  std::vector<size_t> head;
+  std::map<int, long> last_record;     // event -> latest record instance enqueued
+  std::set<long> done_inst;            // executed record instances
+  long next_inst = 1;
+  uint32_t words[8] = {};
+  long clock = 0;                      // global execution order
+  std::map<long, long> work_time;      // work id -> execution time
+  explicit SimDevice(int ns) : n_streams(ns), q(ns), head(ns, 0) {}
+
+  void record(Event e, Stream s) {
+    Op o{Op::kRecord};
+    o.ev = e;
+    o.inst = next_inst++;
+    last_record[e] = o.inst;
+    q.at(s).push_back(o);
+  }
+  void wait(Stream s, Event e) {
+    Op o{Op::kWait};
+    o.ev = e;
+    auto it = last_record.find(e);
+    o.inst = it == last_record.end() ? 0 : it->second;
+    q.at(s).push_back(o);
+  }
+  bool query(Event e) {
+    auto it = last_record.find(e);
+    return it == last_record.end() || done_inst.count(it->second) > 0;
+  }
+  void write_done(Stream s, int slot, uint32_t seq) {
+    Op o{Op::kWrite};
+    o.slot = slot;
+    o.seq = seq;
+    q.at(s).push_back(o);
+  }
+  uint32_t read_done(int slot) { return words[slot]; }
+  void work(Stream s, long id) {
+    Op o{Op::kWork};
+    o.work = id;
+    q.at(s).push_back(o);
+  }
+  bool runnable(int s) const {
+    if (head[s] >= q[s].size()) return false;
+    const Op& o = q[s][head[s]];
+    return o.kind != Op::kWait || o.inst == 0 || done_inst.count(o.inst) > 0;
+  }
+  bool step(std::mt19937& rng) {  // execute one runnable head op of a random stream; false if none can run
+    std::vector<int> r;
+    for (int s = 0; s < n_streams; ++s)
+      if (runnable(s)) r.push_back(s);
+    if (r.empty()) return false;
+    const int s = r[rng() % r.size()];
+    const Op& o = q[s][head[s]++];
+    ++clock;
+    if (o.kind == Op::kRecord) done_inst.insert(o.inst);
+    if (o.kind == Op::kWrite) words[o.slot] = o.seq;
+    if (o.kind == Op::kWork) work_time[o.work] = clock;
+    return true;
+  }
+  bool drained() const {
+    for (int s = 0; s < n_streams; ++s)
+      if (head[s] < q[s].size()) return false;
+    return true;
+  }
+};
+
+// -------------------------------------------------------------------------------------------------- driver
+struct Req {
+  int slot;
+  uint32_t seq;
+  long comm_work, epi_work = -1;  // work ids
+  bool committed = false;
+  std::vector<long> must_follow;   // producer work that must precede the epilogue (commit after producer)
+  int epi_runs = 0;
+};
+
+static constexpr int P0 = 0, P1 = 1, COMM = 2, SIDE = 3, OTHER = 4;
+
+static void run_case(int mode, unsigned seed, bool wrap) {
+  std::mt19937 rng(seed);
+  SimDevice dev(5);
+  SlotTable<SimDevice>::Config cfg;
+  cfg.inline_mode = mode <= 2;
+  cfg.lazy_done = mode != 1;
+  cfg.side_epi = mode == 2;
+  cfg.epi_on_producer = mode == 4;
+  cfg.comm = COMM;
+  cfg.side = SIDE;
+  std::vector<int> evs;
+  for (int i = 0; i < 32; ++i) evs.push_back(100 + i);
+  SlotTable<SimDevice> t(dev, cfg, evs);
+  if (wrap) {  // a long-running engine: sequence numbers and done words just below the 32-bit wrap-around
+    t.set_seq(0xFFFFFFFFu - 5);
+    for (auto& w : dev.words) w = 0xFFFFFFFFu - 5;
+  }
+  std::vector<Req> reqs;
+  long next_work = 1;
+  std::map<long, int> epi_of;        // epilogue work id -> request index
+  std::vector<int> slot_owner(8, -1);  // last request per slot
+  std::vector<std::pair<long, int>> after_wait;  // (work enqueued after wait_stream, request it must follow)
+  std::vector<std::pair<long, long>> slot_order;  // (epilogue of previous, comm of next) on a slot: I2
+  auto producer = [&]() { return (rng() % 4 == 0) ? P1 : P0; };  // P0 is the null stream (id 0)
+  const int actions = 400;
+  for (int a = 0; a < actions; ++a) {
+    const int kind = rng() % 10;
+    if (kind <= 3) {  // submit a request from a producer
+      const int P = producer();
+      dev.work(P, next_work++);  // the producer's GEMM that wrote the gradient
+      const auto b = t.begin(P);
+      Req r;
+      r.slot = b.slot;
+      r.seq = b.seq;
+      r.comm_work = next_work++;
+      dev.work(b.run, r.comm_work);  // communication phase: writes this slot's buffers
+      const int idx = (int)reqs.size();
+      if (slot_owner[b.slot] >= 0) slot_order.push_back({-1 - slot_owner[b.slot], r.comm_work});
+      slot_owner[b.slot] = idx;
+      const long ew = next_work++;
+      r.epi_work = ew;
+      epi_of[ew] = idx;
+      reqs.push_back(r);
+      const bool defer = rng() % 3 != 0;
+      std::vector<SlotTable<SimDevice>::Thunk> th;
+      th.push_back([&dev, &reqs, idx, ew](int es) {
+        dev.work(es, ew);  // the epilogue reads this slot's buffers, writes the weights
+        reqs[idx].epi_runs++;
+        reqs[idx].committed = true;
+      });
+      const uint32_t seq = t.end(b.slot, std::move(th), defer);
+      EXPECT(seq == r.seq && seq != 0, "sequence %u vs announced %u", seq, r.seq);
+      if (!defer) reqs[idx].committed = true;
+      // the producer keeps reading the old weights (bwd-data GEMM) after the request is issued
+      dev.work(P, next_work++);
+    } else if (kind == 4 && !reqs.empty()) {  // commit a handle after the producer's work so far
+      const int i = rng() % reqs.size();
+      const int P = producer();
+      const bool was_pending = !reqs[i].committed && t.slot(reqs[i].slot).seq == reqs[i].seq;
+      std::vector<long> before;
+      for (size_t k = 0; k < dev.q[P].size(); ++k)
+        if (dev.q[P][k].kind == Op::kWork) before.push_back(dev.q[P][k].work);
+      t.commit(reqs[i].slot, true, P, reqs[i].seq);
+      if (was_pending) reqs[i].must_follow = before;
+    } else if (kind == 5 && !reqs.empty()) {  // GPU-side wait, then work on that stream
+      const int i = rng() % reqs.size();
+      const int S = (rng() % 3 == 0) ? OTHER : producer();
+      const bool pending = !reqs[i].committed && t.slot(reqs[i].slot).seq == reqs[i].seq;
+      std::vector<long> before;
+      if (pending)
+        for (auto& o : dev.q[S])
+          if (o.kind == Op::kWork) before.push_back(o.work);
+      t.wait_stream(reqs[i].slot, S, reqs[i].seq);
+      if (pending) reqs[i].must_follow = before;
+      const long w = next_work++;
+      dev.work(S, w);
+      after_wait.push_back({w, i});
+    } else if (kind == 6 && !reqs.empty()) {  // host query of a (possibly superseded) handle
+      const int i = rng() % reqs.size();
+      if (t.query(reqs[i].slot, reqs[i].seq))
+        EXPECT(dev.work_time.count(reqs[i].epi_work) > 0, "mode %d seed %u: query(req %d) true before its epilogue",
+               mode, seed, i);
+    } else {  // the GPU makes progress
+      const int n = rng() % 12;
+      for (int k = 0; k < n; ++k) dev.step(rng);
+    }
+  }
+  // drain: every request committed (host waits), then the device runs to completion
+  for (size_t i = 0; i < reqs.size(); ++i) t.commit_for_host_wait(reqs[i].slot, reqs[i].seq);
+  long guard = 0;
+  while (dev.step(rng)) ++guard;
+  EXPECT(dev.drained(), "mode %d seed %u: device deadlocked with work left", mode, seed);
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    const Req& r = reqs[i];
+    EXPECT(r.epi_runs == 1, "mode %d seed %u: request %zu epilogue ran %d times", mode, seed, i, r.epi_runs);
+    if (!dev.work_time.count(r.epi_work) || !dev.work_time.count(r.comm_work)) continue;
+    const long te = dev.work_time[r.epi_work];
+    EXPECT(te > dev.work_time[r.comm_work], "mode %d seed %u: I1 epilogue before comm (req %zu)", mode, seed, i);
+    for (long w : r.must_follow)
+      EXPECT(!dev.work_time.count(w) || dev.work_time[w] < te,
+             "mode %d seed %u: I1 epilogue of req %zu before producer work %ld", mode, seed, i, w);
+    t.query(r.slot, r.seq);  // may record a lazy done event: let the device run it, then ask again
+    while (dev.step(rng)) {
+    }
+    EXPECT(t.query(r.slot, r.seq), "mode %d seed %u: drained request %zu not reported done", mode, seed, i);
+  }
+  for (auto& so : slot_order) {
+    const long prev_epi = reqs[-1 - so.first].epi_work;
+    EXPECT(dev.work_time.count(prev_epi) && dev.work_time.count(so.second) &&
+               dev.work_time[prev_epi] < dev.work_time[so.second],
+           "mode %d seed %u: I2 slot buffer rewritten before the previous epilogue read it", mode, seed);
+  }
+  for (auto& aw : after_wait) {
+    const long e = reqs[aw.second].epi_work;
+    EXPECT(dev.work_time[aw.first] > dev.work_time[e], "mode %d seed %u: I3 work after wait_stream ran first",
+           mode, seed);
+  }
+}
+
+int main() {
+  int cases = 0;
+  for (int mode = 0; mode <= 4; ++mode)
+    for (unsigned seed = 1; seed <= 150; ++seed) {
+      run_case(mode, seed, seed % 5 == 0);
+      ++cases;
+    }
+  // sequence numbers never take the value 0 (it means "whoever holds the slot")
+  {
+    SimDevice dev(3);
+    SlotTable<SimDevice>::Config cfg;
+    cfg.inline_mode = true;
+    std::vector<int> evs;
+    for (int i = 0; i < 32; ++i) evs.push_back(i);
+    SlotTable<SimDevice> t(dev, cfg, evs);
+    t.set_seq(0xFFFFFFFEu);
+    uint32_t seen[4];
+    for (int k = 0; k < 4; ++k) {
+      auto b = t.begin(0);
+      seen[k] = t.end(b.slot, {}, false);
+    }
+    EXPECT(seen[0] == 0xFFFFFFFFu && seen[1] == 1 && seen[2] == 2 && seen[3] == 3, "wrap %u %u %u %u", seen[0],
+           seen[1], seen[2], seen[3]);
+  }
+  if (failures) {
+    std::printf("%d failures over %d cases\n", failures, cases);
+    return 1;
+  }
+  std::printf("%d cases OK\n", cases);
+  return 0;
+}
