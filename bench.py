@@ -312,6 +312,7 @@ def main(argv=None):
                 f"mb{a.ref_mb}": ref,
                 "final_loss": round(loss, 5),
                 "dist": dist_rec,
+                "gemm_tuning": _tuning_report(),
                 **({"engine_counters": engine.counters()} if hasattr(engine, "counters") else {}),
             },
         }
@@ -323,6 +324,14 @@ def main(argv=None):
         print(f"[bench] rank {rank}: replicas DIVERGED: {dist_rec['replica_digests']}", file=sys.stderr, flush=True)
         return 2
     return 0
+
+
+def _tuning_report():
+    """The GEMM plans the on-device tuner chose on this rank (shape key, static plan, chosen plan, their times)."""
+    from fpga_ai_nic_amd.ops import gemm_tune
+
+    t = gemm_tune.tuner()
+    return {"enabled": t.enabled, "decisions": t.log}
 
 
 def replica_digest(tensors):

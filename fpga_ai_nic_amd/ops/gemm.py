@@ -60,48 +60,27 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     if wire is not None:
         if not C.is_cuda or A.dtype != torch.bfloat16 or not a_t or b_t:
             raise ValueError("wire epilogue: bf16 GPU bwd-weight layout only")
-        Cx = _ext.require()
-        M, K, N = A.shape[1], A.shape[0], B.shape[1]
-        tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
-        buf, shard, own, codec = wire[:4]
-        period = int(wire[4]) if len(wire) > 4 else 0
-        sk = 0 if split_k is None else int(split_k)
-        bm, bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
-        if bm == 0:
-            raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
-        tbm, tbn = bm, bn  # launch exactly the planned tile (re-planning with an explicit split_k differs)
-        need = _bf16_ws_floats(M, N, sk, bm, colsum)
-        ws = _workspace(C.device, need) if need else None
-        Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, tbm, tbn, colsum, tw, buf, int(shard),
-                int(own), int(codec), period)
+        _bf16(_ext.require(), A, a_t, B, b_t, C, EPI_WIRE, None, None, False, split_k, tile, colsum, wire)
         return C
     if C.is_cuda:
         Cx = _ext.require()
+        if colsum is not None and (A.dtype != torch.bfloat16 or b_t):
+            from . import nn as _nn
+
+            gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile)
+            _nn.col_sum(B.t() if b_t else B, colsum)
+            return C
+        if A.dtype == torch.bfloat16:
+            _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, None)
+            return C
         M = A.shape[1] if a_t else A.shape[0]
         K = A.shape[0] if a_t else A.shape[1]
         N = B.shape[0] if b_t else B.shape[1]
         ws = None
-        sk = 0 if split_k is None else int(split_k)
-        if colsum is not None:
-            if A.dtype != torch.bfloat16 or b_t:
-                from . import nn as _nn
-
-                gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile)
-                _nn.col_sum(B.t() if b_t else B, colsum)
-                return C
         tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
-        if A.dtype == torch.bfloat16:
-            bm, bn, sk, _w = Cx.gemm_plan(M, N, K, sk, tbm, tbn, tw)
-            if bm == 0:
-                raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
-            tbm, tbn = bm, bn  # launch exactly the planned tile (re-planning with an explicit split_k differs)
-            need = _bf16_ws_floats(M, N, sk, bm, colsum)
-            if need:
-                ws = _workspace(C.device, need)
-        else:
-            sk = Cx.gemm_f32_split(M, N, K, sk)
-            if sk > 1:
-                ws = _workspace(C.device, sk * M * N)
+        sk = Cx.gemm_f32_split(M, N, K, 0 if split_k is None else int(split_k))
+        if sk > 1:
+            ws = _workspace(C.device, sk * M * N)
         Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, tbm, tbn, colsum, tw)
         return C
     # CPU reference path
@@ -120,6 +99,51 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     if colsum is not None:
         colsum.copy_(b.sum(0).to(colsum.dtype))
     return C
+
+
+def _shares_storage(C, *ts) -> bool:
+    c = C.untyped_storage().data_ptr()
+    return any(t is not None and t.untyped_storage().data_ptr() == c for t in ts)
+
+
+def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, wire):
+    """bf16 MFMA GEMM launch with its plan: explicit (tile / split_k given), tuned on the device on a shape's first
+    call (ops/gemm_tune.py), or the static planner's."""
+    M = A.shape[1] if a_t else A.shape[0]
+    K = A.shape[0] if a_t else A.shape[1]
+    N = B.shape[0] if b_t else B.shape[1]
+    tbm, tbn, tw = (tuple(tile) + (0,))[:3] if tile is not None else (0, 0, 0)
+    sk0 = 0 if split_k is None else int(split_k)
+    static = Cx.gemm_plan(M, N, K, sk0, tbm, tbn, tw)
+    if static[0] == 0:
+        raise ValueError(f"gemm: unsupported bf16 shape M={M} N={N} K={K} split_k={split_k} tile={tile}")
+    if wire is not None:
+        buf, shard, own, codec = wire[:4]
+        period = int(wire[4]) if len(wire) > 4 else 0
+
+    def run(plan, waves=0):
+        bm, bn, sk = plan  # launch exactly this tile (re-planning with an explicit split_k differs)
+        need = _bf16_ws_floats(M, N, sk, bm, colsum)
+        ws = _workspace(C.device, need) if need else None
+        if wire is not None:
+            Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, bm, bn, colsum, waves, buf, int(shard),
+                    int(own), int(codec), period)
+        else:
+            Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, bm, bn, colsum, waves)
+
+    from . import gemm_tune
+
+    T = gemm_tune.tuner()
+    if (tile is not None or split_k is not None or not T.enabled or accumulate
+            or torch.cuda.is_current_stream_capturing() or _shares_storage(C, A, B, aux, bias)):
+        run(tuple(static[:3]), tw)
+        return
+    k = T.key(M, N, K, a_t, b_t, epilogue, colsum is not None, wire is not None, C.device)
+    plan = T.lookup(k)
+    if plan is None:
+        T.tune(k, static, T.candidates(Cx, M, N, K), run)
+    else:
+        run(plan)
 
 
 def linear_fwd(x, w, b, out, relu: bool):
