@@ -165,12 +165,13 @@ void register_engine(pybind11::module_& m) {
            py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"),
            py::arg("verify") = -1, py::arg("chunk_elems") = 0, py::arg("links") = py::none())
       .def("layout",
-           [](AllReduceEngine& e, int64_t n) {
-             const EngineLayout L = e.layout(n);
+           [](AllReduceEngine& e, int64_t n, int64_t shard, int64_t chunks) {
+             const EngineLayout L = e.layout(n, shard, chunks);
              return py::dict(py::arg("n") = L.n, py::arg("n_pad") = L.n_pad, py::arg("algo") = L.algo,
                              py::arg("shard") = L.shard, py::arg("slice") = L.slice, py::arg("blocks") = L.blocks,
                              py::arg("rings") = L.rings, py::arg("part") = L.part, py::arg("chunks") = L.chunks);
-           })
+           },
+           py::arg("n"), py::arg("shard") = 0, py::arg("chunks") = 0)
       .def("wire_bytes", [](AllReduceEngine& e, int64_t n) { return e.wire_bytes(e.layout(n)); })
       .def_property_readonly("orders", &AllReduceEngine::orders)
       .def_property_readonly("inline", &AllReduceEngine::is_inline)
@@ -183,11 +184,12 @@ void register_engine(pybind11::module_& m) {
            [](AllReduceEngine& e, const at::Tensor& grad, at::Tensor& master, c10::optional<at::Tensor> lp,
               c10::optional<at::Tensor> mom, int64_t n_valid, double lr, double grad_scale, double wd,
               double momentum, bool nesterov, bool defer, bool update, c10::optional<at::Tensor> out_sum,
-              c10::optional<at::Tensor> prepacked, int64_t prepacked_elems) {
+              c10::optional<at::Tensor> prepacked, int64_t prepacked_elems, int64_t layout_shard,
+              int64_t layout_chunks) {
              FAN_T_CUDA_CONTIG(grad);
              TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
                          "gradients must be f32 or bf16");
-             const EngineLayout L = e.layout(n_valid);
+             const EngineLayout L = e.layout(n_valid, layout_shard, layout_chunks);
              TORCH_CHECK(grad.numel() >= L.n_pad, "gradient buffer has ", grad.numel(), " elements; layout needs ",
                          L.n_pad);
              if (update) {
@@ -216,23 +218,23 @@ void register_engine(pybind11::module_& m) {
              const uint8_t* pre = nullptr;
              if (prepacked && prepacked->defined()) {
                FAN_T_CUDA_CONTIG(*prepacked);
-               const auto shp = e.prepack_shape(n_valid);
-               TORCH_CHECK(shp[0] > 0, "this engine configuration cannot take prepacked input");
-               TORCH_CHECK(prepacked->scalar_type() == at::kByte &&
-                               prepacked->numel() >= shp[1] * (int64_t)wire_shard_bytes(e.codec(), shp[0]),
+               TORCH_CHECK(e.prepack_shape(n_valid)[0] > 0, "this engine configuration cannot take prepacked input");
+               TORCH_CHECK(L.algo == 0 && prepacked->scalar_type() == at::kByte &&
+                               prepacked->numel() >= L.chunks * e.world() * (int64_t)wire_shard_bytes(e.codec(), L.shard),
                            "prepacked wire buffer too small");
                pre = prepacked->data_ptr<uint8_t>();
              }
              SgdParams p{(float)lr, (float)grad_scale, (float)wd, (float)momentum, nesterov ? 1 : 0};
              return e.submit(grad.data_ptr(), grad.scalar_type() == at::kFloat ? kF32 : kBF16,
                              update ? master.data_ptr<float>() : nullptr, lpp, momp, n_valid, p, fan_stream(), defer,
-                             update, outp, pre, prepacked_elems);
+                             update, outp, pre, prepacked_elems, layout_shard, layout_chunks);
            },
            py::arg("grad"), py::arg("master"), py::arg("lp") = py::none(), py::arg("mom") = py::none(),
            py::arg("n_valid"), py::arg("lr"), py::arg("grad_scale") = 1.0, py::arg("weight_decay") = 0.0,
            py::arg("momentum") = 0.0, py::arg("nesterov") = false, py::arg("defer") = false,
            py::arg("update") = true, py::arg("out_sum") = py::none(), py::arg("prepacked") = py::none(),
-           py::arg("prepacked_elems") = 0, py::call_guard<py::gil_scoped_release>())
+           py::arg("prepacked_elems") = 0, py::arg("layout_shard") = 0, py::arg("layout_chunks") = 0,
+           py::call_guard<py::gil_scoped_release>())
       .def("prepack_shape", [](AllReduceEngine& e, int64_t n) {
         const auto s = e.prepack_shape(n);
         return py::make_tuple(s[0], s[1], s[2]);

@@ -122,11 +122,22 @@ AllReduceEngine::~AllReduceEngine() {
   hipStreamDestroy(stream_);
 }
 
-EngineLayout AllReduceEngine::layout(int64_t n) const {
+EngineLayout AllReduceEngine::layout(int64_t n, int64_t shard, int64_t chunks) const {
   EngineLayout L;
   L.n = n;
   L.algo = cfg_.algo;
   const int N = world_;
+  if (shard > 0 || chunks > 0) {
+    FAN_CHECK(cfg_.algo == 0, "explicit shard / chunk layouts are a mesh feature");
+    FAN_CHECK(shard > 0 && shard % 256 == 0 && chunks >= 1, "explicit layout: shard % 256 == 0 and chunks >= 1");
+    FAN_CHECK(shard * N * chunks >= n, "explicit layout smaller than the bucket");
+    if (P2PComm* d = comm_ ? comm_->direct() : nullptr)
+      FAN_CHECK(wire_shard_bytes(cfg_.codec, (size_t)shard) <= d->slot_bytes(), "explicit shard exceeds the p2p slot");
+    L.shard = shard;
+    L.chunks = chunks;
+    L.n_pad = shard * N * chunks;
+    return L;
+  }
   if (cfg_.algo == 0) {
     // buckets above chunk_elems stream through the collectives in balanced chunks of N shards (multi-rank path
     // only: the inline world-1 engine has no collectives to pipeline)
@@ -595,7 +606,8 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
 
 int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
                             SgdParams sgd, hipStream_t producer, bool defer, bool update, float* out_sum,
-                            const uint8_t* prepacked, int64_t prepacked_elems) {
+                            const uint8_t* prepacked, int64_t prepacked_elems, int64_t layout_shard,
+                            int64_t layout_chunks) {
   RoctxRange rr("fan/allreduce/submit");
   FAN_HIP_CHECK(hipSetDevice(device_));
   // slot state machine (slot_table.h): the next slot (a still-deferred occupant is committed first, ordered after
@@ -605,7 +617,7 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   const int slot = b.slot;
   req_seq_ = b.seq;  // the sequence number this request will get (its messages' tags carry it)
   submitted_++;
-  const EngineLayout L = layout(n_valid);
+  const EngineLayout L = layout(n_valid, layout_shard, layout_chunks);
   cur_producer_ = producer;
   run_stream_ = b.run;
   SlotExtra& x = extra_[slot];
@@ -629,7 +641,8 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
     }
   }
   if (prepacked) {
-    FAN_CHECK(prepack_shape(n_valid)[0] > 0, "prepacked input needs the mesh algorithm and a BFP codec");
+    FAN_CHECK(cfg_.algo == 0 && (cfg_.codec == kBfpTrunc || cfg_.codec == kBfpRne),
+              "prepacked input needs the mesh algorithm and a BFP codec");
     FAN_CHECK(prepacked_elems % 16 == 0 && prepacked_elems <= L.n_pad, "bad prepacked_elems");
   }
   // buffers the deferred epilogue reads are per slot: a later request of the same size must not overwrite

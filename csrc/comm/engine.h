@@ -130,10 +130,16 @@ class AllReduceEngine {
   AllReduceEngine(Comm* comm, int rank, int world, EngineConfig cfg, int device);
   ~AllReduceEngine();
 
-  EngineLayout layout(int64_t n) const;
+  // Layout of a bucket of n elements. shard / chunks > 0 (mesh): an explicit chunked layout of `chunks` chunks of
+  // world shards of `shard` elements each (a multiple of 256): the trainer's row-panel split of a bucket submits
+  // each chunk as a request of its own (chunks = 1) with the same shard size as the whole-bucket layout, so both
+  // schedules reduce every element on the same owner, bit for bit.
+  EngineLayout layout(int64_t n, int64_t shard = 0, int64_t chunks = 0) const;
   const std::vector<std::vector<int>>& orders() const { return orders_; }
   hipStream_t stream() const { return stream_; }
   Comm* comm() const { return comm_; }
+  int world() const { return world_; }
+  int rank() const { return rank_; }
   bool is_inline() const { return table_->config().inline_mode; }
   int codec() const { return cfg_.codec; }
 
@@ -144,7 +150,8 @@ class AllReduceEngine {
   // the pack pass (and, at world 1, the reduce pass). The owner shard must also be present in f32 in `grad`.
   int submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
              SgdParams sgd, hipStream_t producer, bool defer, bool update = true, float* out_sum = nullptr,
-             const uint8_t* prepacked = nullptr, int64_t prepacked_elems = 0);
+             const uint8_t* prepacked = nullptr, int64_t prepacked_elems = 0, int64_t layout_shard = 0,
+             int64_t layout_chunks = 0);
   // (shard elements, shards, owner shard whose f32 values the reduce needs or -1) for a prepacked bucket,
   // or shard elements 0 when this configuration cannot take prepacked input.
   std::array<int64_t, 3> prepack_shape(int64_t n) const;

@@ -138,6 +138,23 @@ class MLP:
             l.b_master.copy_(sd[f"fc{i}.bias"].to(l.master.dtype))
         self.sync_lp()
 
+    def repad(self, i: int, n_pad: int):
+        """Grow layer i's bucket planes to ``n_pad`` elements (values kept, new tail zero): the trainer's row-panel
+        layout of a bucket pads it to whole panels."""
+        l = self.layers[i]
+        if n_pad <= l.n_pad:
+            return
+
+        def grow(t):
+            if t is None:
+                return None
+            u = torch.zeros(n_pad, dtype=t.dtype, device=t.device)
+            u[: l.n_pad] = t
+            return u
+
+        l.master, l.grad, l.lp, l.mom = grow(l.master), grow(l.grad), grow(l.lp), grow(l.mom)
+        l.n_pad = n_pad
+
     # ------------------------------------------------------------------ activations
     def alloc_activations(self, mb: int):
         if self._act_mb == mb:
@@ -174,6 +191,14 @@ class MLP:
         else:
             G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
             NN.col_sum(self.dz[i + 1], l.gb)
+
+    def backward_weight_rows(self, i: int, r0: int, r1: int, wire, with_bias: bool):
+        """Rows [r0, r1) of dW of layer i (a row panel: a contiguous flat range of the bucket), BFP-encoded into
+        ``wire`` (that panel's chunk of the wire buffer); ``with_bias``: the panel that ends at the last row also
+        produces the bias gradient (fused colsum, the bucket segment right after dW)."""
+        l = self.layers[i]
+        G.linear_bwd_weight(self.act[i][:, r0:r1], self.dz[i + 1], l.gw[r0:r1],
+                            bias_grad=l.gb if (with_bias and self.bias) else None, wire=wire)
 
     def backward_data(self, i: int):
         if i == 0:

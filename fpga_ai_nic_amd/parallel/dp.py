@@ -12,6 +12,7 @@ backward runs. MI355X mapping:
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -76,7 +77,12 @@ class DataParallelTrainer:
     def __init__(self, model: MLP, engine: CompressedAllReduce | None, *, lr: float = 0.1,
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
                  loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True,
-                 commit_at_end: bool | None = None):
+                 commit_at_end: bool | None = None, panels: int | None = None, panel_submit: str = "split"):
+        """``panels`` (default env FAN_PANELS or 4; < 2 disables): the last-issued bucket (layer 0: no backward left
+        to hide its exchange behind) is computed as row panels of dW, each submitted as a request of its own right
+        after its GEMM (multi-rank C++ engine, mesh, GEMM-encoded wire only). ``panel_submit='whole'`` computes
+        the same panels but submits the bucket as one request of the same chunked layout (the unsplit schedule,
+        bit-identical results)."""
         self.m = model
         self.engine = engine
         self.world = engine.world if engine is not None else 1
@@ -97,6 +103,15 @@ class DataParallelTrainer:
                               else commit_at_end)
         self.prepack = (prepack and engine is not None and getattr(engine, "prepack", False) and self.cuda
                         and model.dtype == torch.bfloat16)
+        self.panel_submit = panel_submit
+        self.panel_plans: dict[int, dict] = {}
+        P = int(os.environ.get("FAN_PANELS", "4")) if panels is None else int(panels)
+        if self.prepack and P >= 2 and hasattr(engine, "panel_plan"):
+            l0 = model.layers[0]
+            pp = engine.panel_plan(l0.cin, l0.cout, P)
+            if pp is not None:
+                model.repad(0, pp["n_pad"])
+                self.panel_plans[0] = pp
 
     def _sgd_local(self, l):
         wire.sgd(wire.as_bytes(l.grad), l.n_pad, 1, l.master, codec="raw_f32", lp=l.lp, mom=l.mom, lr=self.lr,
@@ -128,17 +143,44 @@ class DataParallelTrainer:
 
     def _wait_layer(self, i: int):
         """Layer i's weights must be updated before its forward reads them: a GPU-side wait on layer i's
-        request only (free when its epilogue already runs on this stream), so layer i's forward starts as soon
+        request(s) only (free when its epilogue already runs on this stream), so layer i's forward starts as soon
         as ITS update lands rather than after the whole step's (reference: the host waits per layer request,
         sw/mlp_mpi_example_f32.cpp:757-787)."""
         h = self.pending[i]
         if h is None:
             return
-        if self.cuda:
-            h.wait()
-        else:
-            h.synchronize()
+        for x in (h if isinstance(h, list) else [h]):
+            if self.cuda:
+                x.wait()
+            else:
+                x.synchronize()
         self.pending[i] = None
+
+    def _backward_weight_panels(self, i: int):
+        """dW of layer i as row panels (see ``panels``): panel p's GEMM encodes its rows straight into chunk p of
+        the wire buffer, then chunk p is submitted (deferred) while panel p+1's GEMM runs."""
+        m, l, pp, eng = self.m, self.m.layers[i], self.panel_plans[i], self.engine
+        R, C, S, N = pp["rows"], pp["chunks"], pp["shard"], eng.world
+        buf, shard, own, codec, period = eng.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout,
+                                                            layout=(S, C))
+        sb = wire.shard_bytes(codec, S)
+        ext = N * S
+        kw = dict(lr=self.lr, grad_scale=self.grad_scale, weight_decay=self.wd, momentum=self.momentum,
+                  nesterov=self.nesterov, defer=True)
+        hs = []
+        for p in range(C):
+            r0, r1 = p * R, min((p + 1) * R, l.cin)
+            chunk = buf[p * N * sb:(p + 1) * N * sb]
+            m.backward_weight_rows(i, r0, r1, (chunk, S, own, codec, period), with_bias=p == C - 1)
+            if self.panel_submit == "split":
+                sl = slice(p * ext, (p + 1) * ext)
+                hs.append(eng.allreduce_sgd(l.grad[sl], l.master[sl], None if l.lp is None else l.lp[sl],
+                                            None if l.mom is None else l.mom[sl], n_valid=min(l.n, (p + 1) * ext) - p * ext,
+                                            prepacked=(chunk, ext), layout=(S, 1), name=f"fc{i}.p{p}", **kw))
+        if self.panel_submit != "split":
+            hs.append(eng.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, prepacked=(buf, C * ext),
+                                        layout=(S, C), name=f"fc{i}", **kw))
+        return hs
 
     def _wait_updates(self):
         """Every outstanding update has landed (GPU-side order on the current stream; host waits on CPU)."""
@@ -161,6 +203,13 @@ class DataParallelTrainer:
             t0 = t1
         for i in reversed(range(m.L)):
             l = m.layers[i]
+            if i in self.panel_plans and self.engine is not None:
+                with tracing.range(f"bwd{i}"):
+                    hs = self._backward_weight_panels(i)
+                    m.backward_data(i)
+                    self.pending[i] = hs if self.commit_at_end else [h.commit_after_current() for h in hs]
+                    self.last_handle = hs[-1]
+                continue
             with tracing.range(f"bwd{i}"):
                 # the bwd-weight GEMM encodes dW (and the fused bias gradient) straight into the wire buffer;
                 # the zero tail (padding, or the bias segment of a bias-free model) is encoded once
@@ -189,8 +238,9 @@ class DataParallelTrainer:
                 t0 = t1
         if self.commit_at_end:  # issue order L-1..0: the epilogues run in the order their all-reduces finish
             for i in reversed(range(m.L)):
-                if self.pending[i] is not None:
-                    self.pending[i].commit_after_current()
+                h = self.pending[i]
+                for x in (h if isinstance(h, list) else [] if h is None else [h]):
+                    x.commit_after_current()
         if prof:
             self._sync()
             self.times["bwd"] += time.perf_counter() - t0
@@ -208,7 +258,8 @@ class DataParallelTrainer:
         """Wait (host) for every outstanding all-reduce/update."""
         for i, h in enumerate(self.pending):
             if h is not None:
-                h.synchronize(timeout)
+                for x in (h if isinstance(h, list) else [h]):
+                    x.synchronize(timeout)
                 self.pending[i] = None
         self.last_handle = None
         self._sync()

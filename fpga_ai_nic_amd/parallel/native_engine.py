@@ -189,8 +189,9 @@ class NativeAllReduce:
     def stream(self):
         return torch.cuda.ExternalStream(self.C.stream, device=self.device)
 
-    def layout(self, n: int) -> BucketLayout:
-        d = self.C.layout(int(n))
+    def layout(self, n: int, shard: int = 0, chunks: int = 0) -> BucketLayout:
+        """Bucket layout; ``shard`` / ``chunks`` > 0: an explicit chunked mesh layout (row-panel buckets)."""
+        d = self.C.layout(int(n), int(shard), int(chunks))
         return BucketLayout(n=d["n"], n_pad=d["n_pad"], algo=self.algo, world=self.world, shard=d["shard"],
                             slice_elems=d["slice"], blocks=d["blocks"], rings=d["rings"], part=d["part"],
                             chunks=d["chunks"])
@@ -198,7 +199,32 @@ class NativeAllReduce:
     def wire_bytes(self, L: BucketLayout) -> int:
         return int(self.C.wire_bytes(L.n))
 
-    def prepack_target(self, grad: torch.Tensor, n: int, static_from: int | None = None):
+    def panel_plan(self, cin: int, cout: int, panels: int):
+        """Row-panel layout of a [W (cin x cout) | b (cout)] bucket in ``panels`` chunks (or None when this engine /
+        shape cannot take one): every chunk holds R whole rows of dW (R*cout = world shards of 256-multiple size,
+        R % 8 == 0 for 16-B aligned operand slices), the last chunk the remaining rows + the bias. The trainer
+        computes dW panel by panel and submits each chunk as a request of its own as soon as its GEMM is enqueued,
+        so chunk p's exchange overlaps panel p+1's GEMM (the reference overlaps each request with the following
+        backward, sw/mlp_mpi_example_f32.cpp:752-764)."""
+        if (self.algo != "mesh" or not self.prepack or self.inline or panels < 2 or cout % 16
+                or self.codec not in ("bfp_rne", "bfp_trunc")):
+            return None
+        N = self.world
+        R = max(8, -(-(cin + 1) // panels))
+        while R <= cin:
+            C = -(-(cin + 1) // R)
+            last_rows = cin - (C - 1) * R
+            if R % 8 == 0 and (R * cout) % (256 * N) == 0 and C >= 2 and last_rows >= 8:
+                S = R * cout // N
+                try:
+                    self.C.layout(cin * cout + cout, S, C)
+                except RuntimeError:
+                    return None
+                return {"rows": R, "chunks": C, "shard": S, "n_pad": C * N * S}
+            R += 8
+        return None
+
+    def prepack_target(self, grad: torch.Tensor, n: int, static_from: int | None = None, layout=None):
         """Wire target for a producer that encodes the gradient itself (GEMM ``kEpiWire`` epilogue):
         ``(wire_u8, shard_elems, own_shard, codec_id, period)`` — one persistent buffer per gradient bucket — or None
         when this configuration (ring / raw codec) cannot take prepacked input.
@@ -209,9 +235,11 @@ class NativeAllReduce:
         shard, shards, own = self.C.prepack_shape(int(n))
         if shard == 0 or n % 16:
             return None
+        if layout is not None:  # explicit chunked layout (row panels): shard x world x chunks
+            shard, shards = int(layout[0]), int(layout[1]) * self.world
         need = shards * wire.shard_bytes(self.codec_id, shard)
         static_from = n if static_from is None else int(static_from)
-        key = (grad.data_ptr(), static_from)
+        key = (grad.data_ptr(), static_from, shard, shards)
         buf = self._prepack_bufs.get(key)
         if buf is None or buf.numel() < need:
             buf = torch.empty(need, dtype=torch.uint8, device=self.device)
@@ -226,17 +254,19 @@ class NativeAllReduce:
                       mom: torch.Tensor | None = None, *, n_valid: int | None = None, lr: float,
                       grad_scale: float = 1.0, weight_decay: float = 0.0, momentum: float = 0.0,
                       nesterov: bool = False, update_after=None, defer: bool = False,
-                      name: str = "bucket", prepacked=None) -> NativeHandle:
+                      name: str = "bucket", prepacked=None, layout=None) -> NativeHandle:
         """``prepacked=(wire_u8, elems)``: flat elements [0, elems) were already encoded into ``wire_u8``
-        (from :meth:`prepack_target`); the engine encodes the rest and skips its pack pass."""
+        (from :meth:`prepack_target`); the engine encodes the rest and skips its pack pass. ``layout=(shard,
+        chunks)``: an explicit chunked mesh layout (see :meth:`panel_plan`)."""
         n_valid = int(n_valid if n_valid is not None else master.numel())
         pre, pre_n = (None, 0) if prepacked is None else prepacked
+        ls, lc = (0, 0) if layout is None else (int(layout[0]), int(layout[1]))
         # an immediate request (no ordering after the producer's later work) is committed by the engine itself, so
         # a chunked bucket runs its per-chunk epilogues inside the pipeline (bounded scratch)
         eng_defer = defer or update_after is not None
         slot = self.C.submit(grad.view(-1), master.view(-1), None if lp is None else lp.view(-1),
                              None if mom is None else mom.view(-1), n_valid, lr, grad_scale, weight_decay, momentum,
-                             nesterov, eng_defer, True, None, pre, int(pre_n))
+                             nesterov, eng_defer, True, None, pre, int(pre_n), ls, lc)
         h = NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=eng_defer)
         self._account(n_valid)
         return h if defer else h.commit(update_after)
