@@ -1,9 +1,10 @@
 // Wire-codec kernels of the compressed all-reduce engine (gfx950).
 //
-// All kernels are HBM-streaming: each lane owns 8 consecutive elements (16-B loads of bf16,
-// 2x16-B of f32) and a lane PAIR owns one 16-element BFP group. Grids are capped at 2048
-// blocks and grid-stride over every shard, so each lane runs the same number of iterations
-// per shard and lane pairs never split (all lane counts are multiples of 64).
+// All kernels are HBM-streaming: each lane owns one 16-element BFP group (32-B loads of bf16, 64-B of f32; one
+// 16-B mantissa store, and the group exponents of 16 consecutive lanes leave as one 16-B store, bfp_format.h
+// WireLane16) — except wire_pack_range (the short bias / padding tails at any 16-element offset), where a lane
+// PAIR owns a group. Grids are capped at 2048 blocks and grid-stride over every shard, so each lane runs the same
+// number of iterations per shard and 16-lane segments never split (group counts are multiples of 16).
 //
 // Reference parity:
 //   wire_pack    = bfp_adapter TX (hw/bfp_adapter.sv:100-154, 279-379)
@@ -36,16 +37,16 @@ constexpr int kBlock = 256;
 template <typename TIN, int C>
 __global__ void __launch_bounds__(kBlock) wire_pack_kernel(const TIN* __restrict__ in, uint8_t* __restrict__ out,
                                                           size_t n_s, int n_shards) {
-  const size_t tasks = n_s >> 3;
+  const size_t tasks = n_s >> 4;  // one 16-value group per lane (WireLane16)
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   const size_t sb = wire_shard_bytes(C, n_s);
   for (int s = 0; s < n_shards; ++s) {
     const TIN* src = in + (size_t)s * n_s;
     uint8_t* dst = out + (size_t)s * sb;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-      float v[8];
-      DenseLane<TIN>::load8(src, t << 3, v);
-      WireLane<C>::store8(dst, n_s, t << 3, v);
+      float v[16];
+      DenseLane16<TIN>::load16(src, t << 4, v);
+      WireLane16<C>::store16(dst, n_s, t << 4, v);
     }
   }
 }
@@ -70,16 +71,16 @@ __global__ void __launch_bounds__(kBlock) wire_pack_range_kernel(const TIN* __re
 template <typename TOUT, int C>
 __global__ void __launch_bounds__(kBlock) wire_unpack_kernel(const uint8_t* __restrict__ in, TOUT* __restrict__ out,
                                                             size_t n_s, int n_shards) {
-  const size_t tasks = n_s >> 3;
+  const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   const size_t sb = wire_shard_bytes(C, n_s);
   for (int s = 0; s < n_shards; ++s) {
     const uint8_t* src = in + (size_t)s * sb;
     TOUT* dst = out + (size_t)s * n_s;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-      float v[8];
-      WireLane<C>::load8(src, n_s, t << 3, v);
-      DenseLane<TOUT>::store8(dst, t << 3, v);
+      float v[16];
+      WireLane16<C>::load16(src, n_s, t << 4, v);
+      DenseLane16<TOUT>::store16(dst, t << 4, v);
     }
   }
 }
@@ -89,25 +90,25 @@ __global__ void __launch_bounds__(kBlock)
     wire_reduce_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
                        const TL* __restrict__ local, uint8_t* __restrict__ out_wire, float* __restrict__ out_f32,
                        size_t n_s) {
-  const size_t tasks = n_s >> 3;
+  const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-    const size_t le = t << 3;
-    float acc[8];
+    const size_t le = t << 4;
+    float acc[16];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.0f;
+    for (int j = 0; j < 16; ++j) acc[j] = 0.0f;
     for (int r = 0; r < n_slots; ++r) {
-      float v[8];
+      float v[16];
       if (HAS_LOCAL && r == self_pos) {
-        DenseLane<TL>::load8(local, le, v);
+        DenseLane16<TL>::load16(local, le, v);
       } else {
-        WireLane<C>::load8(slots + (size_t)r * slot_stride, n_s, le, v);
+        WireLane16<C>::load16(slots + (size_t)r * slot_stride, n_s, le, v);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      for (int j = 0; j < 16; ++j) acc[j] += v[j];
     }
-    if (OUT_F32) DenseLane<float>::store8(out_f32, le, acc);
-    if (OUT_WIRE) WireLane<C>::store8(out_wire, n_s, le, acc);
+    if (OUT_F32) DenseLane16<float>::store16(out_f32, le, acc);
+    if (OUT_WIRE) WireLane16<C>::store16(out_wire, n_s, le, acc);
   }
 }
 
@@ -116,16 +117,16 @@ __global__ void __launch_bounds__(kBlock)
 template <typename TIN, int C>
 __global__ void __launch_bounds__(kBlock) wire_pack_to_kernel(const TIN* __restrict__ in, WirePtrs dst, size_t n_s,
                                                              int n_shards) {
-  const size_t tasks = n_s >> 3;
+  const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (int s = 0; s < n_shards; ++s) {
     uint8_t* d = dst.p[s];
     if (d == nullptr) continue;
     const TIN* src = in + (size_t)s * n_s;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-      float v[8];
-      DenseLane<TIN>::load8(src, t << 3, v);
-      WireLane<C>::store8(d, n_s, t << 3, v);
+      float v[16];
+      DenseLane16<TIN>::load16(src, t << 4, v);
+      WireLane16<C>::store16(d, n_s, t << 4, v);
     }
   }
   __threadfence_system();
@@ -135,22 +136,22 @@ template <typename TL, int C>
 __global__ void __launch_bounds__(kBlock)
     wire_reduce_to_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
                           const TL* __restrict__ local, WirePtrs dst, int n_dst, size_t n_s) {
-  const size_t tasks = n_s >> 3;
+  const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-    const size_t le = t << 3;
-    float acc[8];
+    const size_t le = t << 4;
+    float acc[16];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.0f;
+    for (int j = 0; j < 16; ++j) acc[j] = 0.0f;
     for (int r = 0; r < n_slots; ++r) {
-      float v[8];
-      if (r == self_pos) DenseLane<TL>::load8(local, le, v);
-      else WireLane<C>::load8(slots + (size_t)r * slot_stride, n_s, le, v);
+      float v[16];
+      if (r == self_pos) DenseLane16<TL>::load16(local, le, v);
+      else WireLane16<C>::load16(slots + (size_t)r * slot_stride, n_s, le, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      for (int j = 0; j < 16; ++j) acc[j] += v[j];
     }
-    for (int i = 0; i < n_dst; ++i)
-      if (dst.p[i] != nullptr) WireLane<C>::store8(dst.p[i], n_s, le, acc);
+    for (int i = 0; i < n_dst; ++i)  // wave-uniform condition: every lane of a 16-lane segment stores
+      if (dst.p[i] != nullptr) WireLane16<C>::store16(dst.p[i], n_s, le, acc);
   }
   __threadfence_system();
 }
@@ -159,15 +160,15 @@ template <typename TOUT, int C>
 __global__ void __launch_bounds__(kBlock) wire_unpack_strided_kernel(const uint8_t* __restrict__ in,
                                                                     size_t shard_stride, TOUT* __restrict__ out,
                                                                     size_t n_s, int n_shards) {
-  const size_t tasks = n_s >> 3;
+  const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (int s = 0; s < n_shards; ++s) {
     const uint8_t* src = in + (size_t)s * shard_stride;
     TOUT* dst = out + (size_t)s * n_s;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-      float v[8];
-      WireLane<C>::load8(src, n_s, t << 3, v);
-      DenseLane<TOUT>::store8(dst, t << 3, v);
+      float v[16];
+      WireLane16<C>::load16(src, n_s, t << 4, v);
+      DenseLane16<TOUT>::store16(dst, t << 4, v);
     }
   }
 }
@@ -177,22 +178,22 @@ __global__ void __launch_bounds__(kBlock)
     wire_sgd_kernel(const uint8_t* __restrict__ wire, size_t n_s, int n_shards, int skip_shard, int skip_period,
                     float* __restrict__ master, bf16_t* __restrict__ lp, float* __restrict__ mom, SgdParams p,
                     size_t n_valid, size_t sb) {
-  const size_t tasks = n_s >> 3;
+  const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (int s = 0; s < n_shards; ++s) {
     if (skip_shard >= 0 && (s % skip_period) == skip_shard) continue;
     const uint8_t* src = wire + (size_t)s * sb;
     const size_t base = (size_t)s * n_s;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-      const size_t e = base + (t << 3);
+      const size_t e = base + (t << 4);
       if (e >= n_valid) continue;
-      float g[8], w[8];
-      WireLane<C>::load8(src, n_s, t << 3, g);
-      DenseLane<float>::load8(master, e, w);
-      float m[8];
-      if (HAS_MOM) DenseLane<float>::load8(mom, e, m);
+      float g[16], w[16];
+      WireLane16<C>::load16(src, n_s, t << 4, g);
+      DenseLane16<float>::load16(master, e, w);
+      float m[16];
+      if (HAS_MOM) DenseLane16<float>::load16(mom, e, m);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 16; ++j) {
         float gj = g[j] * p.grad_scale;
         if (p.weight_decay != 0.0f) gj = fmaf(p.weight_decay, w[j], gj);
         if (HAS_MOM) {
@@ -201,13 +202,13 @@ __global__ void __launch_bounds__(kBlock)
         }
         w[j] = fmaf(-p.lr, gj, w[j]);
       }
-      const bool full = e + 8 <= n_valid;
+      const bool full = e + 16 <= n_valid;
       if (full) {
-        DenseLane<float>::store8(master, e, w);
-        if (HAS_MOM) DenseLane<float>::store8(mom, e, m);
-        if (HAS_LP) DenseLane<bf16_t>::store8(lp, e, w);
+        DenseLane16<float>::store16(master, e, w);
+        if (HAS_MOM) DenseLane16<float>::store16(mom, e, m);
+        if (HAS_LP) DenseLane16<bf16_t>::store16(lp, e, w);
       } else {
-        for (int j = 0; j < 8 && e + j < n_valid; ++j) {
+        for (int j = 0; j < 16 && e + j < n_valid; ++j) {
           master[e + j] = w[j];
           if (HAS_MOM) mom[e + j] = m[j];
           if (HAS_LP) lp[e + j] = f32_to_bf16(w[j]);
@@ -236,7 +237,7 @@ void launch_wire_pack(int codec, int in_dtype, const void* in, void* out, size_t
                       hipStream_t stream) {
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (in_dtype == kF32)
       hipLaunchKernelGGL((wire_pack_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in, (uint8_t*)out,
@@ -269,7 +270,7 @@ void launch_wire_unpack(int codec, int out_dtype, const void* in, void* out, siz
                         hipStream_t stream) {
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (out_dtype == kF32)
       hipLaunchKernelGGL((wire_unpack_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)in, (float*)out,
@@ -284,7 +285,7 @@ void launch_wire_unpack(int codec, int out_dtype, const void* in, void* out, siz
 template <typename TL, int C>
 static void reduce_dispatch(const void* slots, size_t slot_stride, int n_slots, int self_pos, const void* local,
                             void* out_wire, float* out_f32, size_t n_s, hipStream_t stream) {
-  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
   const uint8_t* sl = (const uint8_t*)slots;
   const TL* lo = (const TL*)local;
   uint8_t* ow = (uint8_t*)out_wire;
@@ -325,7 +326,7 @@ void launch_wire_sgd(int codec, const void* wire, size_t n_s, int n_shards, int 
   if (skip_period < 1) skip_period = 1 << 30;
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
   const uint8_t* w = (const uint8_t*)wire;
   FAN_CODEC_SWITCH(codec, {
     const size_t sb = shard_stride ? shard_stride : wire_shard_bytes(C, n_s);
@@ -349,7 +350,7 @@ void launch_wire_unpack_strided(int codec, int out_dtype, const void* in, size_t
                                 int n_shards, hipStream_t stream) {
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (out_dtype == kF32)
       hipLaunchKernelGGL((wire_unpack_strided_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)in,
@@ -366,7 +367,7 @@ void launch_wire_pack_to(int codec, int in_dtype, const void* in, const WirePtrs
   check_ns(n_s);
   FAN_CHECK(n_shards <= kMaxPeers, "pack_to: at most 16 destinations");
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (in_dtype == kF32)
       hipLaunchKernelGGL((wire_pack_to_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in, dst, n_s,
@@ -383,7 +384,7 @@ void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t
   check_ns(n_s);
   FAN_CHECK(n_dst <= kMaxPeers && local != nullptr, "reduce_to: local operand and at most 16 destinations");
   if (n_s == 0) return;
-  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
   FAN_CODEC_SWITCH(codec, {
     if (local_dtype == kF32)
       hipLaunchKernelGGL((wire_reduce_to_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,

@@ -37,6 +37,24 @@ void wire_pack(const at::Tensor& x, at::Tensor& out, int64_t shard_elems, int64_
                         fan_stream());
 }
 
+// shard s of x encoded straight into dsts[s] (each a uint8 view, e.g. a peer's receive-arena slot); ends with a
+// system-scope release (the direct P2P transport's producer kernel)
+void wire_pack_to(const at::Tensor& x, const std::vector<at::Tensor>& dsts, int64_t shard_elems, int64_t codec) {
+  FAN_T_CUDA_CONTIG(x);
+  TORCH_CHECK(x.numel() == shard_elems * (int64_t)dsts.size(), "one destination per shard");
+  TORCH_CHECK(dsts.size() <= (size_t)fan::kMaxPeers, "at most 16 destinations");
+  fan::WirePtrs to{};
+  for (size_t i = 0; i < dsts.size(); ++i) {
+    TORCH_CHECK(dsts[i].is_cuda() && dsts[i].scalar_type() == at::kByte &&
+                    (size_t)dsts[i].numel() >= fan::wire_shard_bytes((int)codec, shard_elems) &&
+                    ((uintptr_t)dsts[i].data_ptr() & 15) == 0,
+                "destination ", i, ": 16-B aligned uint8 buffer of one wire shard");
+    to.p[i] = dsts[i].data_ptr<uint8_t>();
+  }
+  fan::launch_wire_pack_to((int)codec, dtype_code(x), x.data_ptr(), to, (size_t)shard_elems, (int)dsts.size(),
+                           fan_stream());
+}
+
 void wire_pack_range(const at::Tensor& x, at::Tensor& out, int64_t shard_elems, int64_t begin, int64_t end,
                      int64_t codec) {
   FAN_T_CUDA_CONTIG(x);
@@ -130,6 +148,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wire_pack", &wire_pack, "encode dense f32/bf16 into the wire format (per shard)");
   m.def("wire_unpack", &wire_unpack, "decode wire format into dense f32/bf16");
   m.def("wire_pack_range", &wire_pack_range, "encode flat elements [begin, end) into the shard layout");
+  m.def("wire_pack_to", &wire_pack_to, "encode shard s straight into dsts[s] (e.g. peers' receive slots)");
   m.def("wire_reduce", &wire_reduce, "sum wire slots (+ dense local) -> wire and/or f32", pybind11::arg("slots"),
         pybind11::arg("n_slots"), pybind11::arg("self_pos"), pybind11::arg("local"), pybind11::arg("out_wire"),
         pybind11::arg("out_f32"), pybind11::arg("shard_elems"), pybind11::arg("codec"));
