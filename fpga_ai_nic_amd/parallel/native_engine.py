@@ -210,7 +210,7 @@ class NativeAllReduce:
                 or self.codec not in ("bfp_rne", "bfp_trunc")):
             return None
         N = self.world
-        R = max(8, -(-(cin + 1) // panels))
+        R = -(-max(8, -(-(cin + 1) // panels)) // 8) * 8
         while R <= cin:
             C = -(-(cin + 1) // R)
             last_rows = cin - (C - 1) * R
