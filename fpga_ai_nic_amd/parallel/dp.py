@@ -78,9 +78,10 @@ class DataParallelTrainer:
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
                  loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True,
                  commit_at_end: bool | None = None, panels: int | None = None, panel_submit: str = "split"):
-        """``panels`` (default env FAN_PANELS or 4; < 2 disables): the last-issued bucket (layer 0: no backward left
-        to hide its exchange behind) is computed as row panels of dW, each submitted as a request of its own right
-        after its GEMM (multi-rank C++ engine, mesh, GEMM-encoded wire only). ``panel_submit='whole'`` computes
+        """``panels`` (default env FAN_PANELS, else 4 at world > 1 and off at world 1; < 2 disables): the
+        last-issued bucket (layer 0: no backward left to hide its exchange behind) is computed as row panels of dW,
+        each submitted as a request of its own right after its GEMM (multi-rank C++ engine, mesh, GEMM-encoded
+        wire only). ``panel_submit='whole'`` computes
         the same panels but submits the bucket as one request of the same chunked layout (the unsplit schedule,
         bit-identical results)."""
         self.m = model
@@ -105,7 +106,9 @@ class DataParallelTrainer:
                         and model.dtype == torch.bfloat16)
         self.panel_submit = panel_submit
         self.panel_plans: dict[int, dict] = {}
-        P = int(os.environ.get("FAN_PANELS", "4")) if panels is None else int(panels)
+        # default: 4 panels when there is a real exchange to hide (world > 1); a forced 1-rank path has none, and
+        # panels cost GEMM efficiency (smaller M per launch, more split-K slabs), so it opts in with FAN_PANELS
+        P = (int(os.environ.get("FAN_PANELS", "4" if self.world > 1 else "0")) if panels is None else int(panels))
         if self.prepack and P >= 2 and hasattr(engine, "panel_plan"):
             l0 = model.layers[0]
             pp = engine.panel_plan(l0.cin, l0.cout, P)
