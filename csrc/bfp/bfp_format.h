@@ -243,6 +243,30 @@ struct DenseLane16 {
   }
 };
 
+// ---------------------------------------------------------------- release of stores into peer memory
+// A kernel that stores into peers' receive arenas (direct P2P transport) must have every store performed before the
+// stream-ordered flag write that tells the peer to read them (p2p_comm.h, memory ordering). Modes (FAN_P2P_RELEASE,
+// settable at run time for A/B: p2p_release_mode()):
+//   1 block (default): every wave drains its own stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier,
+//     then ONE lane issues the system-scope release (the valid form of MI355X_MICROARCH.md §Workgroup dispatch);
+//   2 thread: every wave issues __threadfence_system() (the round-2 form: one system fence per wave);
+//   0 none: rely on the end-of-kernel release alone (diagnostic only).
+int p2p_release_mode();
+void set_p2p_release_mode(int mode);
+
+__device__ __forceinline__ void p2p_release(int mode) {
+  if (mode == 2) {
+    __threadfence_system();
+  } else if (mode == 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the wait after the write-back (compiler hazard)
+    }
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 // Destination table of a kernel that stores its output straight into several buffers (the direct peer-to-peer
 // transport: one entry per rank, each an IPC-mapped slot of that peer's receive arena; nullptr entries skipped).

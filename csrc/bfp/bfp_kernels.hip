@@ -14,6 +14,9 @@
 //                  into the all-gather epilogue so weights never take an extra HBM round trip.
 #include "bfp/bfp_format.h"
 
+#include <atomic>
+#include <cstring>
+
 namespace fan {
 
 // Upper bound on the workgroups of one wire kernel (env FAN_WIRE_MAX_BLOCKS, default 2048): these memory-bound
@@ -21,6 +24,19 @@ namespace fan {
 // workgroup (profiles/r1_gemm_cu_contention_probe.txt), so the footprint is a tunable. Measured at world 1 through
 // the multi-rank path: capping it at 512 / 128 / 64 made the step 0.4 / 4 / 11 % slower
 // (profiles/r1_wire_grid_cap_ab.txt) — the kernels are on the critical path more than they crowd the GEMMs.
+static std::atomic<int>& release_mode_flag() {
+  static std::atomic<int> m{[] {
+    const char* e = getenv("FAN_P2P_RELEASE");
+    if (!e) return 1;
+    if (!strcmp(e, "thread")) return 2;
+    if (!strcmp(e, "none")) return 0;
+    return 1;
+  }()};
+  return m;
+}
+int p2p_release_mode() { return release_mode_flag().load(std::memory_order_relaxed); }
+void set_p2p_release_mode(int mode) { release_mode_flag().store(mode < 0 ? 0 : mode > 2 ? 2 : mode); }
+
 static int wire_max_blocks() {
   static const int v = [] {
     const char* e = getenv("FAN_WIRE_MAX_BLOCKS");
@@ -116,7 +132,7 @@ __global__ void __launch_bounds__(kBlock)
 // receive slots over xGMI), then release at system scope before the kernel retires.
 template <typename TIN, int C>
 __global__ void __launch_bounds__(kBlock) wire_pack_to_kernel(const TIN* __restrict__ in, WirePtrs dst, size_t n_s,
-                                                             int n_shards) {
+                                                             int n_shards, int rel) {
   const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (int s = 0; s < n_shards; ++s) {
@@ -129,13 +145,13 @@ __global__ void __launch_bounds__(kBlock) wire_pack_to_kernel(const TIN* __restr
       WireLane16<C>::store16(d, n_s, t << 4, v);
     }
   }
-  __threadfence_system();
+  p2p_release(rel);
 }
 
 template <typename TL, int C>
 __global__ void __launch_bounds__(kBlock)
     wire_reduce_to_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
-                          const TL* __restrict__ local, WirePtrs dst, int n_dst, size_t n_s) {
+                          const TL* __restrict__ local, WirePtrs dst, int n_dst, size_t n_s, int rel) {
   const size_t tasks = n_s >> 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
@@ -153,7 +169,7 @@ __global__ void __launch_bounds__(kBlock)
     for (int i = 0; i < n_dst; ++i)  // wave-uniform condition: every lane of a 16-lane segment stores
       if (dst.p[i] != nullptr) WireLane16<C>::store16(dst.p[i], n_s, le, acc);
   }
-  __threadfence_system();
+  p2p_release(rel);
 }
 
 template <typename TOUT, int C>
@@ -371,10 +387,10 @@ void launch_wire_pack_to(int codec, int in_dtype, const void* in, const WirePtrs
   FAN_CODEC_SWITCH(codec, {
     if (in_dtype == kF32)
       hipLaunchKernelGGL((wire_pack_to_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in, dst, n_s,
-                         n_shards);
+                         n_shards, p2p_release_mode());
     else
       hipLaunchKernelGGL((wire_pack_to_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const bf16_t*)in, dst, n_s,
-                         n_shards);
+                         n_shards, p2p_release_mode());
   });
   FAN_HIP_CHECK(hipGetLastError());
 }
@@ -388,10 +404,10 @@ void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t
   FAN_CODEC_SWITCH(codec, {
     if (local_dtype == kF32)
       hipLaunchKernelGGL((wire_reduce_to_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,
-                         slot_stride, n_slots, self_pos, (const float*)local, dst, n_dst, n_s);
+                         slot_stride, n_slots, self_pos, (const float*)local, dst, n_dst, n_s, p2p_release_mode());
     else
       hipLaunchKernelGGL((wire_reduce_to_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,
-                         slot_stride, n_slots, self_pos, (const bf16_t*)local, dst, n_dst, n_s);
+                         slot_stride, n_slots, self_pos, (const bf16_t*)local, dst, n_dst, n_s, p2p_release_mode());
   });
   FAN_HIP_CHECK(hipGetLastError());
 }

@@ -1,6 +1,7 @@
 // Multi-segment copy: one launch moves every segment of a P2P round (one per peer), so all xGMI links carry
 // traffic at once instead of one hipMemcpyAsync after another. Each workgroup walks 16-B chunks of the
 // concatenated segments (grid-stride); stores to IPC-mapped peer pointers travel over xGMI.
+#include "bfp/bfp_format.h"
 #include "comm/p2p_comm.h"
 
 namespace fan {
@@ -16,7 +17,7 @@ struct Segs {
   int n;
 };
 
-__global__ void __launch_bounds__(256) multi_copy_kernel(Segs s) {
+__global__ void __launch_bounds__(256) multi_copy_kernel(Segs s, int rel) {
   const uint64_t total = s.end[s.n - 1] >> 4;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   int seg = 0;
@@ -28,8 +29,8 @@ __global__ void __launch_bounds__(256) multi_copy_kernel(Segs s) {
     *reinterpret_cast<uint4*>(s.dst[seg] + off) = v;
   }
   // peer stores are posted over xGMI: make them visible system-wide before the kernel retires, i.e. before
-  // the stream-ordered flag write that tells the peer to read them
-  __threadfence_system();
+  // the stream-ordered flag write that tells the peer to read them (bfp_format.h p2p_release)
+  p2p_release(rel);
 }
 
 }  // namespace
@@ -52,7 +53,7 @@ void launch_multi_copy(const std::vector<P2PCopy>& segs, hipStream_t stream) {
     }
     if (s.n == 0) continue;
     const int grid = stream_grid(acc / 16, 256);
-    hipLaunchKernelGGL(multi_copy_kernel, grid, 256, 0, stream, s);
+    hipLaunchKernelGGL(multi_copy_kernel, grid, 256, 0, stream, s, p2p_release_mode());
     FAN_HIP_CHECK(hipGetLastError());
   }
 }

@@ -49,18 +49,33 @@ def main():
 
     pack = lambda: C.wire_pack(x, out, n_s, codec)  # noqa: E731
     pack_to = lambda: C.wire_pack_to(x, dsts, n_s, codec)  # noqa: E731
-    tp, tt = [], []
+    flat = arena[: sb * a.shards]
+    wire_src = torch.randint(0, 255, (sb * a.shards,), dtype=torch.uint8, device="cuda")
+    copy_in = lambda: flat.copy_(wire_src)  # noqa: E731  (torch copy kernel into the arena: store-path reference)
+    modes = {"thread": 2, "block": 1, "none": 0}
+    m0 = C.p2p_release_mode()
+    tp, tc, tt = [], [], {k: [] for k in modes}
     for _ in range(a.rounds):
         tp.append(t(pack))
-        tt.append(t(pack_to))
+        tc.append(t(copy_in))
+        for k, m in modes.items():
+            C.set_p2p_release_mode(m)
+            tt[k].append(t(pack_to))
+    C.set_p2p_release_mode(m0)
+    pack_to()
     torch.cuda.synchronize()
     same = all(torch.equal(out[q * sb:(q + 1) * sb], dsts[q]) for q in range(a.shards))
     byt = x.numel() * 2 + sb * a.shards  # bf16 read + wire written
-    mp, mt = statistics.median(tp), statistics.median(tt)
-    print(json.dumps({"probe": "wire_store_bw", "arena_memory": comm.arena_memory, "shard_elems": n_s,
-                      "shards": a.shards, "pack_hbm_us": round(mp, 2), "pack_to_arena_us": round(mt, 2),
-                      "pack_hbm_GBps": round(byt / mp / 1e3, 1), "pack_to_arena_GBps": round(byt / mt / 1e3, 1),
-                      "arena_vs_hbm": round(mp / mt, 3), "bit_identical": same}), flush=True)
+    mp = statistics.median(tp)
+    rec = {"probe": "wire_store_bw", "arena_memory": comm.arena_memory, "shard_elems": n_s, "shards": a.shards,
+           "wire_bytes": sb * a.shards, "pack_hbm_us": round(mp, 2), "pack_hbm_GBps": round(byt / mp / 1e3, 1),
+           "torch_copy_into_arena_us": round(statistics.median(tc), 2), "default_release": m0,
+           "bit_identical": same}
+    for k in modes:
+        mt = statistics.median(tt[k])
+        rec[f"pack_to_arena_{k}_us"] = round(mt, 2)
+        rec[f"arena_vs_hbm_{k}"] = round(mp / mt, 3)
+    print(json.dumps(rec), flush=True)
     return 0 if same else 1
 
 
