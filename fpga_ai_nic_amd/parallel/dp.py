@@ -78,7 +78,7 @@ class DataParallelTrainer:
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
                  loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True,
                  commit_at_end: bool | None = None, panels: int | None = None, panel_submit: str = "split"):
-        """``panels`` (default env FAN_PANELS, else 4 at world > 1 and off at world 1; < 2 disables): the
+        """``panels`` (default env FAN_PANELS, else off; < 2 disables): the
         last-issued bucket (layer 0: no backward left to hide its exchange behind) is computed as row panels of dW,
         each submitted as a request of its own right after its GEMM (multi-rank C++ engine, mesh, GEMM-encoded
         wire only). ``panel_submit='whole'`` computes
@@ -106,9 +106,12 @@ class DataParallelTrainer:
                         and model.dtype == torch.bfloat16)
         self.panel_submit = panel_submit
         self.panel_plans: dict[int, dict] = {}
-        # default: 4 panels when there is a real exchange to hide (world > 1); a forced 1-rank path has none, and
-        # panels cost GEMM efficiency (smaller M per launch, more split-K slabs), so it opts in with FAN_PANELS
-        P = (int(os.environ.get("FAN_PANELS", "4" if self.world > 1 else "0")) if panels is None else int(panels))
+        # opt-in (FAN_PANELS=4): measured on the one-GPU pool the split costs more than it hides — each panel adds a
+        # GEMM launch at a quarter of the rows (more split-K slabs) and a request with two P2P rounds, and there the
+        # "exchange" it would hide is local (forced 1-rank path: 1.263 vs 1.127 ms/step; two ranks time-sharing one
+        # GPU: 5.06-5.30 vs 4.61-4.70 ms/step, profiles/r3_panels_ab.txt). It stays off until an 8-GPU run shows
+        # the layer-0 exchange it is built to overlap.
+        P = int(os.environ.get("FAN_PANELS", "0")) if panels is None else int(panels)
         if self.prepack and P >= 2 and hasattr(engine, "panel_plan"):
             l0 = model.layers[0]
             pp = engine.panel_plan(l0.cin, l0.cout, P)
