@@ -253,6 +253,8 @@ struct DenseLane16 {
 //   0 none: rely on the end-of-kernel release alone (diagnostic only).
 int p2p_release_mode();
 void set_p2p_release_mode(int mode);
+int p2p_grid_cap();  // workgroup cap of the peer-storing kernels (FAN_P2P_GRID)
+void set_p2p_grid_cap(int blocks);
 
 __device__ __forceinline__ void p2p_release(int mode) {
   if (mode == 2) {

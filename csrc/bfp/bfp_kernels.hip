@@ -14,6 +14,7 @@
 //                  into the all-gather epilogue so weights never take an extra HBM round trip.
 #include "bfp/bfp_format.h"
 
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 
@@ -36,6 +37,19 @@ static std::atomic<int>& release_mode_flag() {
 }
 int p2p_release_mode() { return release_mode_flag().load(std::memory_order_relaxed); }
 void set_p2p_release_mode(int mode) { release_mode_flag().store(mode < 0 ? 0 : mode > 2 ? 2 : mode); }
+
+// Grid cap of the kernels that store into peers' receive arenas (FAN_P2P_GRID, default 512): every workgroup ends
+// with one system-scope release, so fewer, longer-lived workgroups pay fewer of them (profiles/r3_wire_store_bw.txt).
+static std::atomic<int>& p2p_grid_flag() {
+  static std::atomic<int> g{[] {
+    const char* e = getenv("FAN_P2P_GRID");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : 512;
+  }()};
+  return g;
+}
+int p2p_grid_cap() { return p2p_grid_flag().load(std::memory_order_relaxed); }
+void set_p2p_grid_cap(int blocks) { p2p_grid_flag().store(blocks > 0 ? blocks : 512); }
 
 static int wire_max_blocks() {
   static const int v = [] {
@@ -383,7 +397,7 @@ void launch_wire_pack_to(int codec, int in_dtype, const void* in, const WirePtrs
   check_ns(n_s);
   FAN_CHECK(n_shards <= kMaxPeers, "pack_to: at most 16 destinations");
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, std::min(wire_max_blocks(), p2p_grid_cap()));
   FAN_CODEC_SWITCH(codec, {
     if (in_dtype == kF32)
       hipLaunchKernelGGL((wire_pack_to_kernel<float, C>), grid, kBlock, 0, stream, (const float*)in, dst, n_s,
@@ -400,7 +414,7 @@ void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t
   check_ns(n_s);
   FAN_CHECK(n_dst <= kMaxPeers && local != nullptr, "reduce_to: local operand and at most 16 destinations");
   if (n_s == 0) return;
-  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 16, kBlock, std::min(wire_max_blocks(), p2p_grid_cap()));
   FAN_CODEC_SWITCH(codec, {
     if (local_dtype == kF32)
       hipLaunchKernelGGL((wire_reduce_to_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,

@@ -52,7 +52,7 @@ void launch_multi_copy(const std::vector<P2PCopy>& segs, hipStream_t stream) {
       ++s.n;
     }
     if (s.n == 0) continue;
-    const int grid = stream_grid(acc / 16, 256);
+    const int grid = stream_grid(acc / 16, 256, p2p_grid_cap());
     hipLaunchKernelGGL(multi_copy_kernel, grid, 256, 0, stream, s, p2p_release_mode());
     FAN_HIP_CHECK(hipGetLastError());
   }

@@ -75,6 +75,17 @@ def main():
         mt = statistics.median(tt[k])
         rec[f"pack_to_arena_{k}_us"] = round(mt, 2)
         rec[f"arena_vs_hbm_{k}"] = round(mp / mt, 3)
+    # grid cap of the peer-storing kernels (one release per workgroup), default release form
+    g0 = C.p2p_grid_cap()
+    tg = {g: [] for g in (256, 512, 1024, 2048)}
+    for _ in range(a.rounds):
+        for g in tg:
+            C.set_p2p_grid_cap(g)
+            tg[g].append(t(pack_to))
+    C.set_p2p_grid_cap(g0)
+    rec["default_grid_cap"] = g0
+    rec["pack_to_arena_block_us_by_grid_cap"] = {g: round(statistics.median(v), 2) for g, v in tg.items()}
+    rec["arena_vs_hbm_by_grid_cap"] = {g: round(mp / statistics.median(v), 3) for g, v in tg.items()}
     print(json.dumps(rec), flush=True)
     return 0 if same else 1
 
