@@ -250,6 +250,8 @@ struct DenseLane16 {
 //   1 block (default): every wave drains its own stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier,
 //     then ONE lane issues the system-scope release (the valid form of MI355X_MICROARCH.md §Workgroup dispatch);
 //   2 thread: every wave issues __threadfence_system() (the round-2 form: one system fence per wave);
+//   3 cp: nothing in the kernel; the transport records a system-scope release event on the stream right before
+//     it writes the flags (ONE command-processor cache write-back per round instead of one per workgroup);
 //   0 none: rely on the end-of-kernel release alone (diagnostic only).
 int p2p_release_mode();
 void set_p2p_release_mode(int mode);

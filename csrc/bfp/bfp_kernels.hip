@@ -31,12 +31,13 @@ static std::atomic<int>& release_mode_flag() {
     if (!e) return 1;
     if (!strcmp(e, "thread")) return 2;
     if (!strcmp(e, "none")) return 0;
+    if (!strcmp(e, "cp")) return 3;
     return 1;
   }()};
   return m;
 }
 int p2p_release_mode() { return release_mode_flag().load(std::memory_order_relaxed); }
-void set_p2p_release_mode(int mode) { release_mode_flag().store(mode < 0 ? 0 : mode > 2 ? 2 : mode); }
+void set_p2p_release_mode(int mode) { release_mode_flag().store(mode < 0 ? 0 : mode > 3 ? 3 : mode); }
 
 // Grid cap of the kernels that store into peers' receive arenas (FAN_P2P_GRID, default 512): every workgroup ends
 // with one system-scope release, so fewer, longer-lived workgroups pay fewer of them (profiles/r3_wire_store_bw.txt).

@@ -1,6 +1,8 @@
 // Direct peer-to-peer transport. See p2p_comm.h.
 #include "comm/p2p_comm.h"
 
+#include "bfp/bfp_format.h"
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -61,6 +63,11 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
   last_sent_[0].assign(world, 0);
   last_sent_[1].assign(world, 0);
   bytes_to_peer_.assign(world, 0);
+  FAN_HIP_CHECK(hipEventCreateWithFlags(&rel_ev_, hipEventDisableTiming | hipEventReleaseToSystem));
+}
+
+void P2PComm::release_before_flags(hipStream_t s) {
+  if (p2p_release_mode() == 3) FAN_HIP_CHECK(hipEventRecord(rel_ev_, s));
 }
 
 void P2PComm::wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool credit) {
@@ -177,6 +184,7 @@ P2PComm::~P2PComm() {
     hipEventDestroy(t.ev[0]);
     hipEventDestroy(t.ev[1]);
   }
+  if (rel_ev_) hipEventDestroy(rel_ev_);
   hipFree(flags_);
   hipFree(arena_);
 }
@@ -245,6 +253,7 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
     }
   }
   copy(out, s);
+  release_before_flags(s);
   for (int p : dests) {
     FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, q, 0));  // "ready from rank_" at p
     last_sent_[par][p] = q;
@@ -287,6 +296,7 @@ P2PComm::Round P2PComm::begin(hipStream_t s) {
 
 void P2PComm::publish(const Round& r, hipStream_t s) {
   const int par = (int)(r.seq & 1);
+  release_before_flags(s);
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
     FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, r.seq, 0));  // "ready from rank_" at p

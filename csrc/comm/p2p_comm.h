@@ -147,6 +147,8 @@ class P2PComm : public Comm {
   std::vector<int64_t> bytes_to_peer_;
   bool uncached_ = false;
   std::string arena_mem_;
+  hipEvent_t rel_ev_ = nullptr;  // system-scope release before the flag writes (release mode "cp")
+  void release_before_flags(hipStream_t s);
 };
 
 }  // namespace fan
