@@ -14,8 +14,9 @@ Reported per (variant, size):
 * ``comm_us`` / ``comm_algo_bw_GBps``: device time of the communication phase only (request start on the comm
   stream -> end of the all-gather, from the engine's request trace, slowest rank), and the phase split;
 * ``wire_bytes_per_rank``: bytes one rank sends (BFP: 17 B per 16 values).
-Both variants start from f32 gradients (the mesh packs its shards, the ring packs per hop), so mesh vs ring is a
-like-for-like comparison; ``rccl`` is the uncompressed baseline (RCCL f32 all-reduce + a separate SGD kernel,
+Both variants start from f32 gradients (the mesh packs its shards, the ring packs per hop), or with
+``--prepacked`` both from the producer's BFP encoding (as in training, where the bwd-weight GEMM encodes), so mesh
+vs ring is a like-for-like comparison; ``rccl`` is the uncompressed baseline (RCCL f32 all-reduce + a separate SGD kernel,
 BASELINE config 2; the reference's commented MPI_Iallreduce path, sw:615-647).
 
 1 GPU:  python bench/allreduce_bw.py
@@ -58,6 +59,10 @@ def main():
     ap.add_argument("--transport", default="native", choices=["native", "torch", "p2p"])
     ap.add_argument("--local", action="store_true", help="world 1: inline engine (no collectives)")
     ap.add_argument("--grad-dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--prepacked", action="store_true",
+                    help="the gradient arrives already BFP-encoded by its producer (the training path: the bwd-weight "
+                         "GEMM's wire epilogue; encoded once here, outside the timed requests): the mesh skips its "
+                         "pack pass, the ring sends the producer's slices at every SEND_LOCAL hop")
     a = ap.parse_args()
     force = not a.local
     rank, world, _, dev = D.init_distributed(force=force)
@@ -83,8 +88,18 @@ def main():
             w = torch.randn(L.n_pad, device=dev)
             lp = w.to(torch.bfloat16)
 
+            kw = {}
+            if a.prepacked and hasattr(eng, "prepack_target") and gdt == torch.float32:
+                tgt = eng.prepack_target(g, n)
+                if tgt is not None:  # the "producer": encode the whole gradient once into the engine's wire layout
+                    n16 = n // 16 * 16
+                    from fpga_ai_nic_amd import _ext
+
+                    _ext.require().wire_pack_range(g, tgt[0], tgt[1], 0, n16, tgt[3])
+                    kw["prepacked"] = (tgt[0], n16)
+
             def once():
-                return eng.allreduce_sgd(g, w, lp, n_valid=n, lr=1e-6, grad_scale=1.0 / world)
+                return eng.allreduce_sgd(g, w, lp, n_valid=n, lr=1e-6, grad_scale=1.0 / world, **kw)
 
             once().synchronize()
             times, comm = [], []
@@ -110,7 +125,9 @@ def main():
                    "transport": (a.transport if impl == "native" else "torch") if multi else "none",
                    "n_gpus": world, "size_MB_f32": mb, "rings": eng.rings, "rings_requested": v["rings"],
                    "us": round(t * 1e6, 1), "algo_bw_GBps": round(algo_bw, 1), "bus_bw_GBps": round(bus_bw, 1),
-                   "wire_bytes_per_rank": eng.wire_bytes(L), "grad_dtype": a.grad_dtype}
+                   "wire_bytes_per_rank": eng.wire_bytes(L), "grad_dtype": a.grad_dtype,
+                   "input": "prepacked" if kw else "f32",
+                   "direct_rounds": eng.counters().get("direct_rounds", 0) if hasattr(eng, "counters") else 0}
             if comm:
                 tr = sorted(comm, key=lambda x: x["comm_ms"])[len(comm) // 2]  # median round
                 cus = tr["comm_ms"] * 1e3 / max(1, tr["requests"])

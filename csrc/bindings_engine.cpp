@@ -219,8 +219,10 @@ void register_engine(pybind11::module_& m) {
              if (prepacked && prepacked->defined()) {
                FAN_T_CUDA_CONTIG(*prepacked);
                TORCH_CHECK(e.prepack_shape(n_valid)[0] > 0, "this engine configuration cannot take prepacked input");
-               TORCH_CHECK(L.algo == 0 && prepacked->scalar_type() == at::kByte &&
-                               prepacked->numel() >= L.chunks * e.world() * (int64_t)wire_shard_bytes(e.codec(), L.shard),
+               const int64_t need = L.algo == 0
+                                        ? L.chunks * e.world() * (int64_t)wire_shard_bytes(e.codec(), L.shard)
+                                        : (int64_t)L.rings * L.blocks * e.world() * (int64_t)wire_shard_bytes(e.codec(), L.slice);
+               TORCH_CHECK(prepacked->scalar_type() == at::kByte && prepacked->numel() >= need,
                            "prepacked wire buffer too small");
                pre = prepacked->data_ptr<uint8_t>();
              }

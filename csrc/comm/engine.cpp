@@ -6,6 +6,7 @@
 
 #include "comm/p2p_comm.h"
 #include "common/roctx.h"
+#include "gemm/gemm.h"
 #include <functional>
 #include <sstream>
 #include <thread>
@@ -208,9 +209,12 @@ static void epilogue(int codec, hipStream_t st, const uint8_t* G, int64_t shard,
 }
 
 std::array<int64_t, 3> AllReduceEngine::prepack_shape(int64_t n) const {
-  if (cfg_.algo != 0 || (cfg_.codec != kBfpTrunc && cfg_.codec != kBfpRne)) return {0, 0, -1};
+  if (cfg_.codec != kBfpTrunc && cfg_.codec != kBfpRne) return {0, 0, -1};
   const EngineLayout L = layout(n);
   const bool local = (world_ == 1 && !cfg_.force_comm) || comm_ == nullptr;
+  if (cfg_.algo == 1)  // ring: one shard per slice, ring-major; every local slice is also needed in f32 (each reduce
+                       // hop adds the local contribution), except at world 1 where the encoding is the result
+    return {L.slice, (int64_t)L.rings * L.blocks * world_, world_ == 1 ? -1 : kWireOwnAll};
   // chunked buckets: the owner shard of chunk c is wire shard c*N + rank (owner = shard index mod N)
   return {L.shard, world_ * L.chunks, local ? -1 : rank_};
 }
@@ -482,7 +486,8 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
 
 std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const void* grad, int gdt,
                                                              float* master, bf16_t* lp, float* mom, int64_t n_valid,
-                                                             SgdParams p, bool update, float* out_sum) {
+                                                             SgdParams p, bool update, float* out_sum,
+                                                             const uint8_t* prepacked, int64_t prepacked_elems) {
   const int N = world_, c = cfg_.codec;
   const int64_t S = L.slice;
   const size_t sb = wire_shard_bytes(c, S);
@@ -490,6 +495,11 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
   const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
   hipStream_t st = run_stream_;
   const bool compat = cfg_.compat_owner_fp32 && N > 1 && update;
+  if (prepacked)  // encode what the producer did not (bias gradient + padding): slice-sized shards, ring-major
+    launch_wire_pack_range(c, gdt, grad, const_cast<uint8_t*>(prepacked), (size_t)S, (size_t)prepacked_elems,
+                           (size_t)L.n_pad, st);
+  if (P2PComm* d = comm_ ? comm_->direct() : nullptr; d && N > 1 && !compat && !verify_ && !fault_.active())
+    return run_ring_direct(d, L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked);
   struct RingState {
     int64_t off;
     int down, up, pos;
@@ -536,8 +546,14 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
         const RingRound& row = rs.plan[j];
         uint8_t* out = nullptr;
         if (row.send_src == kSendLocal) {
-          out = row.owned >= 0 ? rs.G + (size_t)row.send_slice * sb : rs.send;
-          launch_wire_pack(c, gdt, local(rs, row.send_slice), out, (size_t)S, 1, st);
+          if (prepacked) {  // the producer's encoding of this slice is the message
+            const uint8_t* pk = prepacked + ((size_t)(&rs - rings.data()) * nsl + row.send_slice) * sb;
+            if (row.owned >= 0) launch_multi_copy({{pk, rs.G + (size_t)row.send_slice * sb, sb}}, st);
+            out = const_cast<uint8_t*>(pk);
+          } else {
+            out = row.owned >= 0 ? rs.G + (size_t)row.send_slice * sb : rs.send;
+            launch_wire_pack(c, gdt, local(rs, row.send_slice), out, (size_t)S, 1, st);
+          }
         } else if (row.send_src == kSendReduce) {
           out = row.owned >= 0 ? rs.G + (size_t)row.send_slice * sb : rs.send;
           float* f32 = nullptr;
@@ -569,6 +585,7 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
         }
         for (size_t q = 0; q < nr; ++q) recvs.push_back({tag_region(1) + q * 4, 16, recvs[q].peer});
       }
+      // (fault injection corrupts a message in flight: on a producer-encoded slice that is the producer's buffer)
       for (size_t q = 0; q < nd; ++q) fault_.maybe_corrupt("ring_send", static_cast<uint8_t*>(sends[q].ptr), sb, st);
       if (counters_.peer_bytes.size() != (size_t)world_) counters_.peer_bytes.assign(world_, 0);
       for (const P2POp& op : sends) counters_.peer_bytes[op.peer] += (int64_t)op.bytes;
@@ -600,6 +617,143 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
     } else {
       thunks.push_back([=](hipStream_t es) { epilogue(c, es, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum); });
     }
+  }
+  return thunks;
+}
+
+// Ring over the direct P2P transport: the encoder is the sender. Every hop's fused decode + add + encode kernel
+// (wire_reduce_to) reads the upstream partial IN PLACE from this rank's receive arena and stores its encoded output
+// straight into the downstream neighbour's arena slot (the NIC pushes each reduced beat into send_fifo, through the
+// BFP TX framing and onto the link, hw/all_reduce.sv:1155-1166, hw/bfp_adapter.sv:279-379); SEND_LOCAL encodes
+// (or, for a producer-encoded bucket, copies) the local slice straight into that slot; a FORWARD hop copies the
+// received full slice arena -> downstream arena, and every received full slice is copied once into the gathered
+// wire the epilogue reads. Per round: credit waits for the downstream slots (P2PComm::begin_to), the kernels, ack
+// of the previous round's upstream slots, ready flags downstream, wait for upstream's. The schedule, sums and
+// summation order are those of run_ring's copying rounds (bit-identical; verify / fault / compat modes use that).
+std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineLayout& L, const void* grad, int gdt,
+                                                       float* master, bf16_t* lp, float* mom, int64_t n_valid,
+                                                       SgdParams p, bool update, float* out_sum,
+                                                       const uint8_t* prepacked) {
+  const int N = world_, c = cfg_.codec;
+  const int64_t S = L.slice;
+  const size_t sb = wire_shard_bytes(c, S);
+  const size_t msg = (sb + 255) / 256 * 256;  // message stride inside an arena slot (<= 2 messages per peer/round)
+  FAN_CHECK(2 * msg <= d->slot_bytes(), "p2p ring: two slices per round must fit an arena slot (lower max_slice_elems)");
+  const int64_t nsl = L.blocks * N;
+  const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
+  hipStream_t st = run_stream_;
+  struct RS {
+    int64_t off;
+    int down, up;
+    std::vector<RingRound> plan;
+    uint8_t* G;
+  };
+  struct Rx {
+    int64_t slice;
+    bool full;
+    const uint8_t* ptr;
+  };
+  std::vector<RS> rings;
+  std::vector<int> downs, ups;
+  const std::string k = std::to_string(sb) + "_" + std::to_string(nsl);
+  for (size_t i = 0; i < orders_.size(); ++i) {
+    const auto& o = orders_[i];
+    int pos = 0;
+    for (int q = 0; q < N; ++q)
+      if (o[q] == rank_) pos = q;
+    RS rs;
+    rs.off = (int64_t)i * L.part;
+    rs.down = o[(pos - 1 + N) % N];
+    rs.up = o[(pos + 1) % N];
+    rs.plan = ring_plan(N, pos, L.blocks);
+    rs.G = epi_scratch("ring_G" + std::to_string(i) + "_" + k, sb * nsl);
+    downs.push_back(rs.down);
+    ups.push_back(rs.up);
+    rings.push_back(rs);
+  }
+  const size_t nrows = rings[0].plan.size();
+  std::vector<std::vector<size_t>> rounds;
+  for (size_t j = 0; j < nrows; ++j) {  // a SEND_LOCAL row joins the previous round (OUTPUT_SEND overlap)
+    if (!rounds.empty() && j > 0 && rings[0].plan[j].send_src == kSendLocal) rounds.back().push_back(j);
+    else rounds.push_back({j});
+  }
+  auto local = [&](const RS& rs, int64_t x) { return g + (size_t)(rs.off + x * S) * esize(gdt); };
+  std::vector<std::vector<Rx>> prev(rings.size());
+  P2PComm::Round prev_round{0};
+  bool have_prev = false;
+  if (counters_.peer_bytes.size() != (size_t)world_) counters_.peer_bytes.assign(world_, 0);
+  for (const auto& rnd : rounds) {
+    RoctxRange rr_("fan/ring/direct_round");
+    const P2PComm::Round rr = d->begin_to(downs, st);
+    std::vector<P2PCopy> copies;  // forwards (arena -> downstream arena) and received full slices -> G
+    for (size_t i = 0; i < rings.size(); ++i) {
+      RS& rs = rings[i];
+      size_t kmsg = 0;
+      for (size_t j : rnd) {
+        const RingRound& row = rs.plan[j];
+        if (row.send_src == kSendNone) continue;
+        uint8_t* to = d->dst(rr, rs.down) + kmsg * msg;
+        ++kmsg;
+        counters_.peer_bytes[rs.down] += (int64_t)sb;
+        d->count_sent(rs.down, sb);
+        if (row.send_src == kSendLocal) {
+          if (prepacked) {
+            copies.push_back({prepacked + ((size_t)i * nsl + row.send_slice) * sb, to, sb});
+          } else {
+            WirePtrs w{};
+            w.p[0] = to;
+            launch_wire_pack_to(c, gdt, local(rs, row.send_slice), w, (size_t)S, 1, st);
+          }
+        } else if (row.send_src == kSendReduce) {
+          const Rx* part = nullptr;
+          for (const Rx& x : prev[i])
+            if (!x.full) part = &x;
+          FAN_CHECK(part != nullptr, "p2p ring: no upstream partial for a reduce hop");
+          WirePtrs w{};
+          w.p[0] = to;
+          int nd = 1;
+          if (row.owned >= 0) w.p[nd++] = rs.G + (size_t)row.send_slice * sb;  // this rank's fully reduced slice
+          launch_wire_reduce_to(c, gdt, part->ptr, 0, 2, 1, local(rs, row.send_slice), w, nd, (size_t)S, st);
+        } else {  // kSendForward: the full slice received last round goes on downstream
+          const Rx* full = nullptr;
+          for (const Rx& x : prev[i])
+            if (x.full && x.slice == row.send_slice) full = &x;
+          FAN_CHECK(full != nullptr, "p2p ring: forwarded slice not received");
+          copies.push_back({full->ptr, to, sb});
+        }
+      }
+      for (const Rx& x : prev[i])  // every received full slice lands once in the gathered wire
+        if (x.full) copies.push_back({x.ptr, rs.G + (size_t)x.slice * sb, sb});
+    }
+    if (!copies.empty()) launch_multi_copy(copies, st);
+    if (have_prev) d->release_from(prev_round, ups, st);  // the previous round's upstream slots are consumed
+    d->publish_to(rr, downs, st);
+    d->wait_from(rr, ups, st);
+    for (size_t i = 0; i < rings.size(); ++i) {
+      prev[i].clear();
+      size_t kmsg = 0;
+      for (size_t j : rnd) {
+        const RingRound& row = rings[i].plan[j];
+        if (row.recv_slice < 0) continue;
+        prev[i].push_back({row.recv_slice, row.recv_full != 0, d->src(rr, rings[i].up) + kmsg * msg});
+        ++kmsg;
+      }
+    }
+    prev_round = rr;
+    have_prev = true;
+    counters_.direct_rounds++;
+  }
+  std::vector<P2PCopy> tail;
+  for (size_t i = 0; i < rings.size(); ++i)
+    for (const Rx& x : prev[i])
+      if (x.full) tail.push_back({x.ptr, rings[i].G + (size_t)x.slice * sb, sb});
+  if (!tail.empty()) launch_multi_copy(tail, st);
+  if (have_prev) d->release_from(prev_round, ups, st);
+  std::vector<EpiThunk> thunks;
+  for (auto& rs : rings) {
+    const int64_t off = rs.off, part = L.part;
+    uint8_t* G = rs.G;
+    thunks.push_back([=](hipStream_t es) { epilogue(c, es, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum); });
   }
   return thunks;
 }
@@ -641,8 +795,7 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
     }
   }
   if (prepacked) {
-    FAN_CHECK(cfg_.algo == 0 && (cfg_.codec == kBfpTrunc || cfg_.codec == kBfpRne),
-              "prepacked input needs the mesh algorithm and a BFP codec");
+    FAN_CHECK(cfg_.codec == kBfpTrunc || cfg_.codec == kBfpRne, "prepacked input needs a BFP codec");
     FAN_CHECK(prepacked_elems % 16 == 0 && prepacked_elems <= L.n_pad, "bad prepacked_elems");
   }
   // buffers the deferred epilogue reads are per slot: a later request of the same size must not overwrite
@@ -653,7 +806,8 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   std::vector<EpiThunk> thunks =
       cfg_.algo == 0 ? run_mesh(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum, prepacked,
                                 prepacked_elems)
-                     : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum);
+                     : run_ring(L, grad, grad_dtype, master, lp, mom, n_valid, sgd, update, out_sum, prepacked,
+                                prepacked_elems);
   FAN_HIP_CHECK(hipGetLastError());
   // phases this schedule does not have (ring hops, the world-1 local path) collapse onto the end of comm
   for (int tp = kTpPacked; tp <= kTpCommEnd; ++tp)

@@ -145,9 +145,11 @@ class AllReduceEngine {
 
   // Enqueue the communication phase of a request. grad: padded flat buffer (f32 or bf16) ready on `producer`.
   // If `defer`, the weight update is enqueued later by commit(); otherwise immediately. Returns the slot.
-  // prepacked (mesh, BFP codecs): the producer already encoded flat elements [0, prepacked_elems) of the bucket
-  // into `prepacked` (mesh shard layout, prepack_shape()); the engine packs the rest (bias + padding) and skips
-  // the pack pass (and, at world 1, the reduce pass). The owner shard must also be present in f32 in `grad`.
+  // prepacked (BFP codecs): the producer already encoded flat elements [0, prepacked_elems) of the bucket into
+  // `prepacked` (shard layout of prepack_shape(): mesh shards, or ring slices ring-major); the engine packs the
+  // rest (bias + padding) and skips its own encode of them (mesh: the pack pass, and at world 1 the reduce pass;
+  // ring: every SEND_LOCAL). The shards prepack_shape() names as owned must also be present in f32 in `grad`
+  // (mesh: the owner shard; ring: all of them).
   int submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
              SgdParams sgd, hipStream_t producer, bool defer, bool update = true, float* out_sum = nullptr,
              const uint8_t* prepacked = nullptr, int64_t prepacked_elems = 0, int64_t layout_shard = 0,
@@ -238,7 +240,10 @@ class AllReduceEngine {
                                          float* out_sum, const uint8_t* prepacked, bool defer);
   std::vector<EpiThunk> run_ring(const EngineLayout& L, const void* grad, int gdt, float* master,
                                               bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
-                                              float* out_sum);
+                                              float* out_sum, const uint8_t* prepacked, int64_t prepacked_elems);
+  std::vector<EpiThunk> run_ring_direct(P2PComm* d, const EngineLayout& L, const void* grad, int gdt, float* master,
+                                        bf16_t* lp, float* mom, int64_t n_valid, SgdParams p, bool update,
+                                        float* out_sum, const uint8_t* prepacked);
 
   Comm* comm_;
   int rank_, world_, device_;

@@ -314,6 +314,35 @@ void P2PComm::release(const Round& r, hipStream_t s) {
     if (p != rank_) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + world_ + rank_, r.seq, 0));
 }
 
+P2PComm::Round P2PComm::begin_to(const std::vector<int>& to, hipStream_t s) {
+  FAN_CHECK(!aborted_, "p2p transport aborted");
+  Round r{++seq_};
+  const int par = (int)(r.seq & 1);
+  for (int p : to) {
+    FAN_CHECK(p != rank_ && p >= 0 && p < world_ && peer_arena_[p] != nullptr, "p2p: bad or unconnected peer");
+    const uint64_t prev = last_sent_[par][p];
+    if (prev) wait_flag(s, flags_ + world_ + p, prev, true);
+  }
+  return r;
+}
+
+void P2PComm::publish_to(const Round& r, const std::vector<int>& to, hipStream_t s) {
+  const int par = (int)(r.seq & 1);
+  release_before_flags(s);
+  for (int p : to) {
+    FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, r.seq, 0));
+    last_sent_[par][p] = r.seq;
+  }
+}
+
+void P2PComm::wait_from(const Round& r, const std::vector<int>& from, hipStream_t s) {
+  for (int p : from) wait_flag(s, flags_ + p, r.seq, false);
+}
+
+void P2PComm::release_from(const Round& r, const std::vector<int>& from, hipStream_t s) {
+  for (int p : from) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + world_ + rank_, r.seq, 0));
+}
+
 void P2PComm::copy(const std::vector<P2PCopy>& segs, hipStream_t s) {
   bool aligned = true;
   for (const P2PCopy& c : segs)

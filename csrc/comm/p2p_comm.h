@@ -83,6 +83,14 @@ class P2PComm : public Comm {
   const uint8_t* src_base(const Round& r) const { return arena_ + (r.seq & 1) * slot_; }
   size_t src_stride() const { return 2 * slot_; }
   void release(const Round& r, hipStream_t s);
+  // The same round protocol restricted to a peer subset (ring rounds: send to the downstream neighbours, receive
+  // from the upstream ones). Every rank must start the same number of rounds (begin / begin_to) in the same order.
+  Round begin_to(const std::vector<int>& to, hipStream_t s);
+  void publish_to(const Round& r, const std::vector<int>& to, hipStream_t s);
+  void wait_from(const Round& r, const std::vector<int>& from, hipStream_t s);
+  void release_from(const Round& r, const std::vector<int>& from, hipStream_t s);
+  // message from rank `src` in round r, in this rank's arena
+  const uint8_t* src(const Round& r, int from) const { return slot_ptr(arena_, from, r.seq); }
   void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s) override;
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override;
   std::string async_error() override { return aborted_ ? "p2p transport aborted" : ""; }

@@ -213,7 +213,7 @@ __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc
 struct WireOut {
   uint8_t* p;
   int64_t shard;  // elements per shard (multiple of 256)
-  int own;        // shard also written to C in f32 (-1: none)
+  int own;        // shard also written to C in f32 (-1: none; kWireOwnAll: every shard, e.g. the ring's inputs)
   int period;     // > 0: shards s with s % period == own are all written (chunked buckets: one owner shard per chunk)
   int codec;      // kBfpTrunc / kBfpRne
   float inv_shard;  // 1 / shard (shard index without a 64-bit integer division)
@@ -263,7 +263,7 @@ __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict_
                                            int row, int col) {
   const uint32_t f = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
   const int sh = wire_store16(v, f, wo);
-  if ((wo.period > 0 ? sh % wo.period : sh) == wo.own) {
+  if (wo.own == kWireOwnAll || (wo.period > 0 ? sh % wo.period : sh) == wo.own) {
 #pragma unroll
     for (int u = 0; u < 16; u += 4)
       *reinterpret_cast<float4*>(C + f + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);

@@ -272,13 +272,14 @@ class NativeAllReduce:
         return h if defer else h.commit(update_after)
 
     def allreduce(self, grad: torch.Tensor, out: torch.Tensor, *, n_valid: int | None = None,
-                  name: str = "bucket") -> NativeHandle:
+                  name: str = "bucket", prepacked=None) -> NativeHandle:
         """Sum-only all-reduce: decoded f32 result written to ``out`` (padded length)."""
         n_valid = int(n_valid if n_valid is not None else grad.numel())
         if out.dtype != torch.float32:
             raise TypeError("native allreduce writes f32 sums")
+        pre, pre_n = (None, 0) if prepacked is None else prepacked
         slot = self.C.submit(grad.view(-1), out.view(-1), None, None, n_valid, 0.0, 1.0, 0.0, 0.0, False, False,
-                             False, out.view(-1))
+                             False, out.view(-1), pre, int(pre_n))
         self._account(n_valid)
         return NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=False)
 

@@ -33,6 +33,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from fpga_ai_nic_amd import _ext
         from fpga_ai_nic_amd.parallel import sim
         from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce
         from fpga_ai_nic_amd.parallel.transport import make_p2p_comm
@@ -79,6 +80,15 @@ def _worker(rank, world, port, q):
                 sim.ring_allreduce(gin, eng.orders, L.slice_elems, L.blocks)[0]
             ok[f"engine_{algo}"] = bool(np.array_equal(out.cpu().numpy()[:m], ref[:m]))
             if algo != "mesh":
+                # the direct ring: every hop's reduce kernel stored into the downstream arena, one round per hop
+                ok["ring_direct_rounds"] = eng.counters()["direct_rounds"] >= 2 * L.blocks * (world - 1) - (L.blocks - 1)
+                # producer-encoded (prepacked) input on the direct ring: same sums
+                buf, shard, own, cid = eng.prepack_target(g, m)[:4]
+                _ext.require().wire_pack_range(g, buf, shard, 0, m // 16 * 16, cid)
+                out_p = torch.zeros(L.n_pad, device="cuda")
+                eng.allreduce(g, out_p, n_valid=m, prepacked=(buf, m // 16 * 16)).synchronize(30)
+                torch.cuda.synchronize()
+                ok["ring_direct_prepacked"] = bool(torch.equal(out_p, out))
                 continue
             # the mesh ran the DIRECT path (pack / reduce kernels stored into the peer's slots, reduce and epilogue
             # read this rank's slots in place); fused SGD immediate and deferred, and the copying path (verify

@@ -98,19 +98,20 @@ def _native_transport():  # one 1-rank RCCL communicator for the module
     return _NT["t"]
 
 
-def _engine_case(N, prepack, force=False, n=20000, codec="bfp_rne"):
+def _engine_case(N, prepack, force=False, n=20000, codec="bfp_rne", algo="mesh", rings=1):
     C = _ext.require()
     rng = np.random.default_rng(3)
     grads = [rng.standard_normal(n).astype(np.float32) for _ in range(N)]
     w0 = rng.standard_normal(n).astype(np.float32)
+    kw = dict(codec=codec, algo=algo, rings=rings, max_slice_elems=2048)
     if N > 1:
         fabric = C.LoopbackFabric(N, 60.0)
-        engines = [NativeAllReduce(None, codec=codec, comm=fabric.comm(r)) for r in range(N)]
+        engines = [NativeAllReduce(None, comm=fabric.comm(r), **kw) for r in range(N)]
     else:
         if force:
-            engines = [NativeAllReduce(_native_transport(), codec=codec, force_comm=True)]
+            engines = [NativeAllReduce(_native_transport(), force_comm=True, **kw)]
         else:
-            engines = [NativeAllReduce(ThreadFabric(1).transport(0), codec=codec)]
+            engines = [NativeAllReduce(ThreadFabric(1).transport(0), **kw)]
     L = engines[0].layout(n)
     w_elems = (n // 2) // 16 * 16  # pretend the producer encoded the first half
 
@@ -123,10 +124,12 @@ def _engine_case(N, prepack, force=False, n=20000, codec="bfp_rne"):
         kw = {}
         if prepack:
             buf, shard, own, cid = eng.prepack_target(g, n)[:4]
-            full = torch.zeros(shard * eng.world, device="cuda")
+            full = torch.zeros(L.n_pad, device="cuda")
             full[:n] = g[:n]
             _ext.require().wire_pack_range(full, buf, shard, 0, w_elems, cid)  # the "producer"
-            if own >= 0:  # the owner shard must be in f32 in grad (already true here); poison the rest
+            if own == -2:  # ring: every local slice is read in f32 too (each hop adds the local contribution)
+                pass
+            elif own >= 0:  # the owner shard must be in f32 in grad (already true here); poison the rest
                 keep = g[own * shard:(own + 1) * shard].clone()
                 g[:w_elems] = float("nan")
                 g[own * shard:(own + 1) * shard] = keep
@@ -164,6 +167,16 @@ def _engine_case(N, prepack, force=False, n=20000, codec="bfp_rne"):
 def test_engine_prepacked_equals_unpacked(N, force, codec):
     a = _engine_case(N, False, force, codec=codec)
     b = _engine_case(N, True, force, codec=codec)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("N,force,rings", [(1, True, 1), (3, False, 1), (3, False, 2), (8, False, 1), (8, False, 7)])
+def test_ring_prepacked_equals_unpacked(N, force, rings):
+    """The ring takes GEMM-encoded input too: each SEND_LOCAL hop sends the producer's encoding of the slice
+    instead of re-encoding it; the sums (and the trained weights) are bit-identical."""
+    a = _engine_case(N, False, force, algo="ring", rings=rings)
+    b = _engine_case(N, True, force, algo="ring", rings=rings)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
 
