@@ -74,7 +74,7 @@ def main():
         impl = a.engine if v["kind"] != "rccl" else "python"
         if not multi:
             transport = ThreadFabric(1).transport(0)
-        elif v["kind"] == "rccl" or impl == "python" or a.transport == "torch":
+        elif v["kind"] == "rccl" or impl == "python" or a.transport in ("torch", "p2p"):  # p2p: gloo/RCCL control
             transport = TorchDistTransport(force_collectives=force)
         else:
             transport = NativeTransport(force_collectives=force)
