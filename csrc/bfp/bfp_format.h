@@ -247,11 +247,13 @@ struct DenseLane16 {
 // A kernel that stores into peers' receive arenas (direct P2P transport) must have every store performed before the
 // stream-ordered flag write that tells the peer to read them (p2p_comm.h, memory ordering). Modes (FAN_P2P_RELEASE,
 // settable at run time for A/B: p2p_release_mode()):
-//   1 block (default): every wave drains its own stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier,
+//   3 cp (default): nothing in the kernel; the transport records a system-scope release event
+//     (hipEventReleaseToSystem) on the stream right before it writes the flags: ONE command-processor release
+//     per round, ordered after every kernel of the round (2-rank flagship 2.25 vs 2.59 ms/step with "block",
+//     profiles/r3_p2p_release_ab.txt);
+//   1 block: every wave drains its own stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier,
 //     then ONE lane issues the system-scope release (the valid form of MI355X_MICROARCH.md §Workgroup dispatch);
-//   2 thread: every wave issues __threadfence_system() (the round-2 form: one system fence per wave);
-//   3 cp: nothing in the kernel; the transport records a system-scope release event on the stream right before
-//     it writes the flags (ONE command-processor cache write-back per round instead of one per workgroup);
+//   2 thread: every wave issues __threadfence_system() (the round-2 form: one system fence per wave, 4.9 ms/step);
 //   0 none: rely on the end-of-kernel release alone (diagnostic only).
 int p2p_release_mode();
 void set_p2p_release_mode(int mode);

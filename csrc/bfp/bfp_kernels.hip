@@ -28,11 +28,11 @@ namespace fan {
 static std::atomic<int>& release_mode_flag() {
   static std::atomic<int> m{[] {
     const char* e = getenv("FAN_P2P_RELEASE");
-    if (!e) return 1;
+    if (!e) return 3;
     if (!strcmp(e, "thread")) return 2;
     if (!strcmp(e, "none")) return 0;
-    if (!strcmp(e, "cp")) return 3;
-    return 1;
+    if (!strcmp(e, "block")) return 1;
+    return 3;
   }()};
   return m;
 }

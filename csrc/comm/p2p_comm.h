@@ -13,10 +13,12 @@
 // done-flag writes (hw/all_reduce.sv:1368-1375); here sequence numbers play the role of both.
 //
 // Memory ordering (why a reader never sees a stale payload, across GPUs whose per-XCD L2s are not coherent):
-//   1. writer: the copy kernel stores the payload into the peer's arena (stores over xGMI land in the peer's HBM;
-//      the writer's own L2 does not keep remote lines), then __threadfence_system() and kernel end (release at
-//      system scope) — every payload store is performed before the kernel's completion is signalled;
-//   2. the flag write (hipStreamWriteValue64) is stream-ordered after that completion, so it becomes visible to the
+//   1. writer: the producing kernels store the payload into the peer's arena (stores over xGMI land in the peer's
+//      HBM; the writer's own L2 does not keep remote lines); before the flag writes the stream records a system-scope
+//      release event (hipEventReleaseToSystem: the command processor waits for the round's kernels and writes back
+//      / makes their stores visible at system scope) — FAN_P2P_RELEASE=block|thread put the release inside the
+//      kernels instead (bfp_format.h p2p_release);
+//   2. the flag write (hipStreamWriteValue64) is stream-ordered after that release, so it becomes visible to the
 //      peer only after the payload;
 //   3. reader: its stream's hipStreamWaitValue64 (the command processor polls the flag in memory, not a cache)
 //      releases the copy-out kernel only once the flag carries the message's sequence number;
