@@ -20,11 +20,8 @@
 
 namespace fan {
 
-// Upper bound on the workgroups of one wire kernel (env FAN_WIRE_MAX_BLOCKS, default 2048): these memory-bound
-// kernels run on the comm stream beside the GEMMs at world > 1, and every CU they occupy cannot host a GEMM
-// workgroup (profiles/r1_gemm_cu_contention_probe.txt), so the footprint is a tunable. Measured at world 1 through
-// the multi-rank path: capping it at 512 / 128 / 64 made the step 0.4 / 4 / 11 % slower
-// (profiles/r1_wire_grid_cap_ab.txt) — the kernels are on the critical path more than they crowd the GEMMs.
+static int wire_max_blocks();
+
 static std::atomic<int>& release_mode_flag() {
   static std::atomic<int> m{[] {
     const char* e = getenv("FAN_P2P_RELEASE");
@@ -39,19 +36,30 @@ static std::atomic<int>& release_mode_flag() {
 int p2p_release_mode() { return release_mode_flag().load(std::memory_order_relaxed); }
 void set_p2p_release_mode(int mode) { release_mode_flag().store(mode < 0 ? 0 : mode > 3 ? 3 : mode); }
 
-// Grid cap of the kernels that store into peers' receive arenas (FAN_P2P_GRID, default 512): every workgroup ends
-// with one system-scope release, so fewer, longer-lived workgroups pay fewer of them (profiles/r3_wire_store_bw.txt).
+// Grid cap of the kernels that store into peers' receive arenas (FAN_P2P_GRID; 0 = auto): with the in-kernel
+// release forms every workgroup ends with one system-scope release, so fewer, longer-lived workgroups pay fewer of
+// them (512); with the command-processor release (default) nothing is paid per workgroup and the cap is the
+// ordinary one (profiles/r3_wire_store_bw.jsonl: 8 shards packed into the arena 18.95 us at 512 vs 17.39 at 2048).
 static std::atomic<int>& p2p_grid_flag() {
   static std::atomic<int> g{[] {
     const char* e = getenv("FAN_P2P_GRID");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 ? x : 512;
+    return e ? atoi(e) : 0;
   }()};
   return g;
 }
-int p2p_grid_cap() { return p2p_grid_flag().load(std::memory_order_relaxed); }
-void set_p2p_grid_cap(int blocks) { p2p_grid_flag().store(blocks > 0 ? blocks : 512); }
+int p2p_grid_cap() {
+  const int g = p2p_grid_flag().load(std::memory_order_relaxed);
+  if (g > 0) return g;
+  const int m = p2p_release_mode();
+  return m == 1 || m == 2 ? 512 : wire_max_blocks();
+}
+void set_p2p_grid_cap(int blocks) { p2p_grid_flag().store(blocks > 0 ? blocks : 0); }
 
+// Upper bound on the workgroups of one wire kernel (env FAN_WIRE_MAX_BLOCKS, default 2048): these memory-bound
+// kernels run on the comm stream beside the GEMMs at world > 1, and every CU they occupy cannot host a GEMM
+// workgroup (profiles/r1_gemm_cu_contention_probe.txt), so the footprint is a tunable. Measured at world 1 through
+// the multi-rank path: capping it at 512 / 128 / 64 made the step 0.4 / 4 / 11 % slower
+// (profiles/r1_wire_grid_cap_ab.txt) — the kernels are on the critical path more than they crowd the GEMMs.
 static int wire_max_blocks() {
   static const int v = [] {
     const char* e = getenv("FAN_WIRE_MAX_BLOCKS");
