@@ -217,22 +217,24 @@ __global__ void __launch_bounds__(kBlock)
     wire_sgd_kernel(const uint8_t* __restrict__ wire, size_t n_s, int n_shards, int skip_shard, int skip_period,
                     float* __restrict__ master, bf16_t* __restrict__ lp, float* __restrict__ mom, SgdParams p,
                     size_t n_valid, size_t sb) {
-  const size_t tasks = n_s >> 4;
+  // 8 elements per lane here (a read-only wire: the 16-per-lane store layout buys nothing, and the smaller
+  // register footprint streams master / lp faster: 33.5 vs 42.5 us on a 16.8 M bucket in the flagship step)
+  const size_t tasks = n_s >> 3;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (int s = 0; s < n_shards; ++s) {
     if (skip_shard >= 0 && (s % skip_period) == skip_shard) continue;
     const uint8_t* src = wire + (size_t)s * sb;
     const size_t base = (size_t)s * n_s;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
-      const size_t e = base + (t << 4);
+      const size_t e = base + (t << 3);
       if (e >= n_valid) continue;
-      float g[16], w[16];
-      WireLane16<C>::load16(src, n_s, t << 4, g);
-      DenseLane16<float>::load16(master, e, w);
-      float m[16];
-      if (HAS_MOM) DenseLane16<float>::load16(mom, e, m);
+      float g[8], w[8];
+      WireLane<C>::load8(src, n_s, t << 3, g);
+      DenseLane<float>::load8(master, e, w);
+      float m[8];
+      if (HAS_MOM) DenseLane<float>::load8(mom, e, m);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < 8; ++j) {
         float gj = g[j] * p.grad_scale;
         if (p.weight_decay != 0.0f) gj = fmaf(p.weight_decay, w[j], gj);
         if (HAS_MOM) {
@@ -241,13 +243,13 @@ __global__ void __launch_bounds__(kBlock)
         }
         w[j] = fmaf(-p.lr, gj, w[j]);
       }
-      const bool full = e + 16 <= n_valid;
+      const bool full = e + 8 <= n_valid;
       if (full) {
-        DenseLane16<float>::store16(master, e, w);
-        if (HAS_MOM) DenseLane16<float>::store16(mom, e, m);
-        if (HAS_LP) DenseLane16<bf16_t>::store16(lp, e, w);
+        DenseLane<float>::store8(master, e, w);
+        if (HAS_MOM) DenseLane<float>::store8(mom, e, m);
+        if (HAS_LP) DenseLane<bf16_t>::store8(lp, e, w);
       } else {
-        for (int j = 0; j < 16 && e + j < n_valid; ++j) {
+        for (int j = 0; j < 8 && e + j < n_valid; ++j) {
           master[e + j] = w[j];
           if (HAS_MOM) mom[e + j] = m[j];
           if (HAS_LP) lp[e + j] = f32_to_bf16(w[j]);
@@ -365,7 +367,7 @@ void launch_wire_sgd(int codec, const void* wire, size_t n_s, int n_shards, int 
   if (skip_period < 1) skip_period = 1 << 30;
   check_ns(n_s);
   if (n_s == 0 || n_shards == 0) return;
-  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
+  const int grid = stream_grid(n_s / 8, kBlock, wire_max_blocks());
   const uint8_t* w = (const uint8_t*)wire;
   FAN_CODEC_SWITCH(codec, {
     const size_t sb = shard_stride ? shard_stride : wire_shard_bytes(C, n_s);

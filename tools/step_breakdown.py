@@ -24,24 +24,19 @@ def short_name(n: str) -> str:
     return n[:110]
 
 
-def _period(keys, max_p=400):
-    """Smallest P for which >= 90 % of dispatches equal the one P later (kernels per training step)."""
+def _steady_window(keys, steps, max_p=400):
+    """(P, start) of the LAST window of steps*P dispatches that repeats with period P, for the smallest such P
+    (kernels per training step): the timed steps, wherever warmup / plan-tuning launches before them and the
+    run's own bookkeeping after them sit in the trace. (0, 0) if none."""
     n = len(keys)
-    for p in range(1, min(max_p, n // 3) + 1):
-        if sum(keys[i] == keys[i + p] for i in range(n - p)) >= 0.9 * (n - p):
-            return p
-    return 0
-
-
-def _last_periodic_window(keys, P, steps):
-    """Start of the last window of steps*P dispatches that repeats with period P (the timed steps, followed in
-    the trace by whatever non-periodic work the run does after them)."""
-    need = P * steps
-    for end in range(len(keys), need - 1, -1):
-        lo = end - need
-        if all(keys[i] == keys[i + P] for i in range(lo, end - P)):
-            return lo
-    return max(0, len(keys) - need)
+    for p in range(1, min(max_p, n // max(steps, 2)) + 1):
+        need = (steps - 1) * p  # consecutive positions i with keys[i] == keys[i + p]
+        run = 0
+        for i in range(n - p - 1, -1, -1):  # scan from the end: the last such window
+            run = run + 1 if keys[i] == keys[i + p] else 0
+            if run >= need and need > 0:
+                return p, i
+    return 0, 0
 
 
 def breakdown(path: str, steps: int):
@@ -55,10 +50,9 @@ def breakdown(path: str, steps: int):
             disp.append((int(r["Start_Timestamp"]), key, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     disp.sort()
     keys = [k for _, k, _ in disp]
-    P = _period(keys)
+    P, lo = _steady_window(keys, steps)
     rows = OrderedDict()
     if P:
-        lo = _last_periodic_window(keys, P, steps)
         disp = disp[lo:lo + P * steps]
     for i, (_, key, d) in enumerate(disp):
         k = ((i % P) if P else -1,) + key
