@@ -140,6 +140,8 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
         return
     k = T.key(M, N, K, a_t, b_t, epilogue, colsum is not None, wire is not None, C.device)
     plan = T.lookup(k)
+    if plan is None and not T.worth_tuning(M, N, static, C.device):
+        plan = T.keep_static(k, static)
     if plan is None:
         T.tune(k, static, T.candidates(Cx, M, N, K), run)
     else:

@@ -8,6 +8,8 @@ tiles without a split take 55-59 µs (profiles/r3_gemm_sweep_mb1792.jsonl). Rath
 the first call of every (shape, layout, epilogue) times the candidate plans on the device, in place, on the call's
 own operands, and keeps the fastest:
 
+* only shapes whose static plan leaves the last wave of workgroups part-empty are tuned (whole-wave plans were
+  chosen by in-step A/B and are kept);
 * candidates: BM x BN in {256, 128}^2 x split-K in {1, 2, 3, 4, 6, 8}, those the planner accepts for the shape,
   with at most 4 waves of workgroups and at least 256 K-elements per split;
 * two interleaved rounds of 3 timed launches each (hip events), a candidate's score is its best round median;
@@ -25,7 +27,6 @@ from __future__ import annotations
 
 import json
 import os
-import statistics
 import threading
 
 import torch
@@ -72,6 +73,20 @@ class GemmTuner:
 
     def lookup(self, k):
         return self.plans.get(k)
+
+    @staticmethod
+    def worth_tuning(M, N, static, dev) -> bool:
+        """Only grids that leave part of the last wave of workgroups idle: the static plans of whole-wave grids were
+        chosen by in-step A/B (round 2) and a micro-benchmark in place, with cache-warm operands, can misrank them
+        (a profiled run once swapped the MB-8192 forward's 256x256 tiles for 256x128: 76 vs 64.5 us in the step)."""
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count if torch.cuda.is_available() else 256
+        wgs = -(-M // static[0]) * -(-N // static[1]) * static[2]
+        return wgs % cus != 0
+
+    def keep_static(self, k, static):
+        with self._lock:
+            self.plans[k] = tuple(static[:3])
+        return tuple(static[:3])
 
     def tune(self, k, static_plan, cands, run):
         """run(plan) launches the GEMM with that (bm, bn, sk) plan on the current stream. Returns the winner (which

@@ -18,7 +18,7 @@ def _ref(A, B, a_t, b_t):
 
 
 @pytest.mark.parametrize("M,N,K,a_t,b_t", [(1792, 4096, 1024, False, False), (1792, 1024, 2048, False, True),
-                                           (1024, 2048, 1792, True, False)])
+                                           (1024, 1536, 1792, True, False)])
 def test_tuned_plan_same_product(M, N, K, a_t, b_t):
     T = gemm_tune.reset(enabled=True)
     torch.manual_seed(0)
@@ -36,6 +36,18 @@ def test_tuned_plan_same_product(M, N, K, a_t, b_t):
     G.gemm(A, a_t, B, b_t, C2)  # cached decision, same plan -> bit-identical
     torch.cuda.synchronize()
     assert len(T.log) == 1 and torch.equal(C, C2)
+
+
+def test_whole_wave_static_plans_are_kept():
+    """A static plan that fills whole waves of the 256 CUs (chosen by in-step A/B) is not re-tuned."""
+    T = gemm_tune.reset(enabled=True)
+    A = (torch.rand(8192, 1024, device="cuda") - 0.5).to(torch.bfloat16)
+    B = (torch.rand(1024, 4096, device="cuda") - 0.5).to(torch.bfloat16)
+    C = torch.empty(8192, 4096, device="cuda")
+    G.gemm(A, False, B, False, C)  # 256x256 tiles: 512 workgroups = 2 waves
+    torch.cuda.synchronize()
+    assert T.log == [] and len(T.plans) == 1
+    gemm_tune.reset()
 
 
 def test_untunable_calls_use_the_static_plan():
