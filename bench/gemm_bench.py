@@ -88,6 +88,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--shapes", default="")
     ap.add_argument("--sweep", action="store_true", help="time every tile/split-K plan per shape")
+    ap.add_argument("--sweep-wire", action="store_true",
+                    help="bwd-weight shapes: sweep with the BFP wire epilogue the training step runs (split plans then "
+                         "include splitk_reduce_wire instead of the f32 reduce)")
     ap.add_argument("--mb", type=int, default=2048, help="MLP minibatch of the shape set")
     ap.add_argument("--set", default="mlp", choices=["mlp", "bert", "ref", "ragged"])
     ap.add_argument("--loops", default="",
@@ -132,6 +135,13 @@ def main():
         def ref_mm_only():
             torch.matmul(Am, Bm)
 
+        wire_sweep = a.sweep_wire and a_t and not b_t
+        if wire_sweep:
+            from fpga_ai_nic_amd.ops import wire as W
+
+            shard_w = (M * N + N + 255) // 256 * 256
+            wbuf_s = torch.empty(W.shard_bytes("bfp_rne", shard_w), dtype=torch.uint8, device="cuda")
+            wt_s = (wbuf_s, shard_w, -1, W.codec_id("bfp_rne"))
         if a.sweep and dt == torch.bfloat16:
             res = {}
             for tile in ((256, 256), (256, 128), (128, 256), (128, 128)):
@@ -145,11 +155,14 @@ def main():
                         torch.cuda.synchronize()
                         ref_out = ref().float() * ((aux > 0) if epi == G.EPI_RELU_MASK else 1)
                         ok = (C.float() - ref_out).abs().max().item() < 1.0
+                        if wire_sweep:  # the plan is checked above with the f32 epilogue; time the wire one
+                            fn = lambda t=t3, s=sk: G.gemm(A, a_t, B, b_t, C, G.EPI_WIRE, split_k=s, tile=t,  # noqa: E731
+                                                           wire=wt_s)
                         res[f"{tile[0]}x{tile[1]}w{waves}/s{sk}"] = round(
                             statistics.median(time_fn(fn, a.iters) for _ in range(3)), 2) if ok else "WRONG"
             valid = {k: v for k, v in res.items() if v != "WRONG"}
             best = min(valid, key=valid.get) if valid else None
-            print(json.dumps({"shape": name, "sweep_us": res, "best": best,
+            print(json.dumps({"shape": name, "epi": "wire" if wire_sweep else epi, "sweep_us": res, "best": best,
                               "auto_plan": G._ext.require().gemm_plan(M, N, K)}), flush=True)
         mine(); ref(); torch.cuda.synchronize()
         err = (C.float() - (ref().float() * ((aux > 0) if epi == G.EPI_RELU_MASK else 1))).abs().max().item()
