@@ -55,12 +55,15 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
   void* d = nullptr;
   FAN_HIP_CHECK(hipHostGetDevicePointer(&d, h, 0));
   flags_dev_ = reinterpret_cast<uint32_t*>(d);
-  // Cross-stream events: FAN_EVENT_FENCE=system|device selects the release scope of the event marker
-  // (diagnostic for the comm-stream epilogue ordering issue, profiles/r1_comm_epilogue_discrepancy.txt).
-  unsigned evf = hipEventDisableTiming;
+  // Cross-stream events order kernels of this device's own streams, so a device-scope release (every XCD's L2
+  // written back for the other streams' kernels) is enough; what leaves the device is released by its own path
+  // (RCCL's kernels, the P2P transport's system-scope round event). Device scope measured 1 % faster on the forced
+  // multi-rank path (1.151-1.153 vs 1.160-1.176 ms/step, same box, profiles/r3_event_fence_ab.txt).
+  // FAN_EVENT_FENCE=system|default: system-scope release / HIP's default marker.
+  unsigned evf = hipEventDisableTiming | hipEventReleaseToDevice;
   if (const char* f = std::getenv("FAN_EVENT_FENCE")) {
-    if (!std::strcmp(f, "system")) evf |= hipEventReleaseToSystem;
-    else if (!std::strcmp(f, "device")) evf |= hipEventReleaseToDevice;
+    if (!std::strcmp(f, "system")) evf = hipEventDisableTiming | hipEventReleaseToSystem;
+    else if (!std::strcmp(f, "default")) evf = hipEventDisableTiming;
   }
   bool lazy_done = true;
   if (const char* ld = std::getenv("FAN_LAZY_DONE")) lazy_done = ld[0] != '0';

@@ -23,10 +23,13 @@ _ws: dict = {}
 
 
 def _workspace(device, numel):
-    t = _ws.get(device)
+    """Split-K slab / bias-partial workspace, one per (device, stream): GEMMs issued on different streams (virtual
+    ranks on one GPU, side streams) may run at the same time and must not share slabs."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream if device.type == "cuda" else 0)
+    t = _ws.get(key)
     if t is None or t.numel() < numel:
         t = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
-        _ws[device] = t
+        _ws[key] = t
     return t
 
 

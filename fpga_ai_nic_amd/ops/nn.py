@@ -28,10 +28,11 @@ def col_sum(x: torch.Tensor, out: torch.Tensor, scale: float = 1.0, accumulate: 
         C = _ext.require()
         M, N = x.shape
         need = C.col_sum_workspace_floats(M, N)
-        ws = _ws.get(x.device)
+        key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)  # per stream: concurrent callers
+        ws = _ws.get(key)
         if ws is None or ws.numel() < need:
             ws = torch.empty(max(need, 1 << 16), dtype=torch.float32, device=x.device)
-            _ws[x.device] = ws
+            _ws[key] = ws
         C.col_sum(x, out, float(scale), bool(accumulate), ws)
         return out
     s = x.float().sum(0) * scale
