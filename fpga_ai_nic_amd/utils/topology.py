@@ -94,6 +94,11 @@ def device_bus_id(index: int) -> str | None:
         return None
 
 
+def own_bus_id() -> str | None:
+    """PCI bus id of this process's current HIP device (None without a GPU)."""
+    return device_bus_id(torch.cuda.current_device()) if torch.cuda.is_available() else None
+
+
 def link_matrix_for(bus_ids, peer=None, types=None, smi_bus=None):
     """Direct-link matrix between the GPUs of the ranks (rank r runs on the GPU with PCI bus id ``bus_ids[r]``):
     links[a][b] = 1 when a reaches b over xGMI — rocm-smi's link type when it reports one for that pair (XGMI),
@@ -146,7 +151,7 @@ def agreed_link_matrix(world: int):
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() == world):
         return link_matrix(world)
     bus = [None] * world
-    dist.all_gather_object(bus, device_bus_id(torch.cuda.current_device()) if torch.cuda.is_available() else None)
+    dist.all_gather_object(bus, own_bus_id())
     obj = [None]
     if dist.get_rank() == 0:
         peer = None
