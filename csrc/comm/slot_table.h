@@ -201,11 +201,13 @@ class SlotTable {
     Slot& sl = slots_[s];
     if (!sl.pending) return;
     sl.epi_stream = sl.stream;
+    bool on_producer = false;
     if (cfg_.epi_on_producer && !cfg_.inline_mode && after_producer && !(producer == sl.stream)) {
       // epilogue on the producer (compute) stream, after the request's communication phase: it runs after
       // everything already enqueued there and never concurrently with the producer's GEMMs
       dev_.wait(producer, sl.comm_done);
       sl.epi_stream = producer;
+      on_producer = true;
     } else if (cfg_.side_epi && after_producer) {
       // world 1: no communication phase; decode + SGD on the side stream after the producer's enqueued work and
       // after the request's own inline work (on the stream it was submitted from, when another stream commits)
@@ -226,7 +228,11 @@ class SlotTable {
     // multi-rank requests finishing on the comm stream: the GPU writes the done word ("write 1 to done_addr +
     // done_id"); requests finishing on the critical compute stream skip that packet: their completion is the event
     if (sl.epi_stream == sl.stream && !cfg_.inline_mode) dev_.write_done(sl.stream, s, sl.seq);
-    sl.done_lazy = cfg_.lazy_done && cfg_.inline_mode && sl.epi_stream == sl.stream && !sl.keep_done;
+    // Lazy done event: the epilogue ran in its own stream's order (inline requests; multi-rank epilogues on the
+    // producer stream), so nothing needs the event unless the host polls the request or another stream waits on
+    // it; ensure_done() records it then. Each eager record is a marker packet on the critical compute stream.
+    sl.done_lazy = cfg_.lazy_done && !sl.keep_done &&
+                   ((cfg_.inline_mode && sl.epi_stream == sl.stream) || on_producer);
     if (!sl.done_lazy) dev_.record(sl.done, sl.epi_stream);
     sl.pending = false;
   }

@@ -8,7 +8,8 @@
 // deferred requests, more than 8 deferred at once, commits after the producer, GPU-side waits, host queries of
 // current and superseded handles, two producer streams one of which is the null stream 0, sequence numbers that
 // wrap around 2^32) is driven through every engine mode (inline with lazy / eager done events, inline with side
-// epilogues, multi-rank with the epilogue on the comm stream or on the producer). Checked on every run:
+// epilogues, multi-rank with the epilogue on the comm stream or on the producer with lazy / eager done events).
+// Checked on every run:
 //   I1 epilogue after its own communication phase, and after all producer work enqueued before its commit;
 //   I2 a slot's buffer is not rewritten by the next request before the previous epilogue on that slot has read it;
 //   I3 a handle that query() reports done has its epilogue executed; work a stream enqueues after wait_stream()
@@ -134,9 +135,9 @@ static void run_case(int mode, unsigned seed, bool wrap) {
   SimDevice dev(5);
   SlotTable<SimDevice>::Config cfg;
   cfg.inline_mode = mode <= 2;
-  cfg.lazy_done = mode != 1;
+  cfg.lazy_done = mode != 1 && mode != 5;
   cfg.side_epi = mode == 2;
-  cfg.epi_on_producer = mode == 4;
+  cfg.epi_on_producer = mode >= 4;
   cfg.comm = COMM;
   cfg.side = SIDE;
   std::vector<int> evs;
@@ -250,7 +251,7 @@ static void run_case(int mode, unsigned seed, bool wrap) {
 
 int main() {
   int cases = 0;
-  for (int mode = 0; mode <= 4; ++mode)
+  for (int mode = 0; mode <= 5; ++mode)
     for (unsigned seed = 1; seed <= 150; ++seed) {
       run_case(mode, seed, seed % 5 == 0);
       ++cases;
