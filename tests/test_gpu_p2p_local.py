@@ -1,0 +1,118 @@
+"""Direct P2P schedules at world 3, 4 and 8 on ONE GPU: N virtual ranks in one process, each with its own P2PComm
+(receive arena + flag block) wired to the others with ``P2PComm.connect_local`` (no IPC), one host thread and one
+stream per rank. The two-process test (test_gpu_p2p.py) covers the IPC bootstrap at world 2, where a ring has one
+neighbour each way; here the direct ring runs over several arc-disjoint rings at once (every rank a different
+downstream peer per ring, hw/all_reduce.sv's single ring generalised: sw/setup_route.sh), and the direct mesh over
+N - 1 peers. Each schedule is bit-exact against the spec simulator, from f32 and from producer-encoded (prepacked)
+input, and counts its direct rounds.
+
+The ranks' flag waits are command-processor waits (hipStreamWaitValue64): a stream parked on a peer's flag blocks the
+hardware queue it runs on. HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES queues (4 by default), so N
+ranks' 2N+ streams in ONE process can park one rank behind another's wait (a deadlock a one-process-per-GPU job
+cannot have). Each case therefore runs in a child process with one hardware queue per stream (GPU_MAX_HW_QUEUES=32,
+the pool's limit) under its own time limit."""
+import json
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fpga_ai_nic_amd import _ext  # noqa: E402
+from fpga_ai_nic_amd.parallel import sim  # noqa: E402
+from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(world, algo, rings, m=40000, max_slice=2048):
+    C = _ext.require()
+    comms = [C.P2PComm(r, world, 0, 2 << 20) for r in range(world)]
+    C.P2PComm.connect_local(comms)
+    rng = np.random.default_rng(100 + world)
+    grads = [rng.standard_normal(m).astype(np.float32) for _ in range(world)]
+    res, errs = [None] * world, [None] * world
+    engines = [NativeAllReduce(None, codec="bfp_rne", algo=algo, rings=rings, max_slice_elems=max_slice,
+                               comm=comms[r]) for r in range(world)]
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                eng = engines[r]
+                L = eng.layout(m)
+                g = torch.zeros(L.n_pad, device="cuda")
+                g[:m] = torch.from_numpy(grads[r]).cuda()
+                out = torch.zeros(L.n_pad, device="cuda")
+                eng.allreduce(g, out, n_valid=m).synchronize(60)
+                tgt = eng.prepack_target(g, m)
+                out_p = None
+                if tgt is not None:  # the producer's encoding as the input
+                    buf, shard, own, cid = tgt[:4]
+                    C.wire_pack_range(g, buf, shard, 0, m // 16 * 16, cid)
+                    out_p = torch.zeros(L.n_pad, device="cuda")
+                    eng.allreduce(g, out_p, n_valid=m, prepacked=(buf, m // 16 * 16)).synchronize(60)
+                s.synchronize()
+                res[r] = (out.cpu().numpy(), None if out_p is None else out_p.cpu().numpy(), L,
+                          eng.counters()["direct_rounds"], [list(o) for o in eng.orders])
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(180)
+    assert not any(t.is_alive() for t in ts), "virtual rank thread hung"
+    assert not any(errs), errs
+    L = res[0][2]
+    gin = [np.pad(x, (0, L.n_pad - m)) for x in grads]
+    if algo == "mesh":
+        ref = sim.mesh_allreduce(gin, L.shard)
+    else:
+        ref = sim.ring_allreduce(gin, res[0][4], L.slice_elems, L.blocks)[0]
+    return res, ref, L
+
+
+def _check(world, algo, rings):
+    res, ref, L = _run(world, algo, rings)
+    m = 40000
+    out = {"ok": True, "why": [], "rings": len(res[0][4])}
+    for r in range(world):
+        o, o_p, _, direct, orders = res[r]
+        if not np.array_equal(o[:m], ref[:m]):
+            out["why"].append(f"rank {r}: {algo} x{rings} differs from the simulator")
+        if o_p is not None and not np.array_equal(o_p, o):
+            out["why"].append(f"rank {r}: prepacked input differs")
+        if direct <= 0:
+            out["why"].append(f"rank {r}: the direct path did not run")
+        if orders != res[0][4]:
+            out["why"].append(f"rank {r}: ring orders differ")
+    out["ok"] = not out["why"]
+    return out
+
+
+@pytest.mark.parametrize("world,algo,rings", [(3, "ring", 2), (4, "ring", 3), (8, "ring", 7), (3, "mesh", 1),
+                                              (8, "mesh", 1)])
+def test_direct_p2p_schedules_bit_exact(world, algo, rings):
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="32")
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), str(world), algo, str(rings)], env=env,
+                           capture_output=True, text=True, timeout=150)
+    except subprocess.TimeoutExpired as e:
+        pytest.fail(f"world {world} {algo}: child timed out\n{(e.stderr or '')[-3000:]}")
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(recs) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    rec = recs[0]
+    assert rec["ok"], rec["why"]
+    if algo == "ring":
+        assert rec["rings"] >= min(rings, 2)  # several arc-disjoint rings at once (N = 4 has 2, not 3)
+
+
+if __name__ == "__main__":
+    print(json.dumps(_check(int(sys.argv[1]), sys.argv[2], int(sys.argv[3]))), flush=True)
