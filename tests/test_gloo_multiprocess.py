@@ -55,7 +55,8 @@ def _engine_worker(rank, world, port, algo, rings, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,algo,rings", [(2, "mesh", 1), (3, "ring", 2), (4, "mesh", 1), (4, "ring", 2)])
+@pytest.mark.parametrize("world,algo,rings", [(2, "mesh", 1), (3, "ring", 2), (4, "mesh", 1), (4, "ring", 2),
+                                              (8, "ring", 7), (8, "mesh", 1)])
 def test_engine_over_gloo(world, algo, rings):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
