@@ -144,8 +144,9 @@ def main():
             wt_s = (wbuf_s, shard_w, -1, W.codec_id("bfp_rne"))
         if a.sweep and dt == torch.bfloat16:
             res = {}
-            for tile in ((256, 256), (256, 128), (128, 256), (128, 128)):
-                for waves in (8, 4):
+            tiles = ((256, 256), (256, 128), (128, 256), (128, 128)) + (((224, 128),) if not a_t else ())
+            for tile in tiles:
+                for waves in (8, 4) if tile[0] != 224 else (4,):
                     for sk in (1, 2, 3, 4, 6, 8):
                         if M % tile[0] or N % tile[1] or K % (64 * sk):
                             continue

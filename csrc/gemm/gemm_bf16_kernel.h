@@ -819,20 +819,26 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
-template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256>
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
+          int BM_ = 256>
 __global__ void __launch_bounds__(256, 1)
     gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
                     float* __restrict__ colsum, WireOut wo) {
-  constexpr int BM = 256, BN = BN_, NT = 256;
+  constexpr int BM = BM_, BN = BN_, NT = 256;
   constexpr int A_BYTES = OpTile<BM, NT>::BYTES;
   constexpr int STAGE = A_BYTES + OpTile<BN, NT>::BYTES;
-  constexpr int GA = OpTile<BM, NT>::GLDS, G = GA + OpTile<BN, NT>::GLDS;  // 8 + 8 (BN 128: 8 + 4) pieces per wave
-  constexpr int WTM = 128, WTN = BN / 2, MI = 8, NJ = WTN / 16;
+  constexpr int GA = OpTile<BM, NT>::GLDS, G = GA + OpTile<BN, NT>::GLDS;  // 8 + 8 (BN 128: 8 + 4; BM 224: 7 + 4)
+  constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NJ = WTN / 16;
   constexpr int Q = MI * NJ, R = MI + NJ;  // MFMAs and fragment reads per k-step and wave
   constexpr int RSP = (Q * 3 / 4) / R, DSP = Q / G;  // read / DMA spacing in MFMAs (64 MFMAs: 3 / 4; 32: 2 / 2)
   static_assert(BN == 256 || BN == 128, "256x256 or 256x128 tiles");
+  // 224x128 tiles: 1792 rows (the reference's per-rank batch, sw/run.sh:16) are 8 row tiles, so a 1792 x 4096 output
+  // is 8 x 32 = 256 workgroups, one per CU (256-row tiles give 7 x 32 = 224 and leave 32 CUs idle). The A image is
+  // K-contiguous ([rows][64 k], 32 rows per glds piece: 7 pieces); an MN-contiguous A stages 128-column halves.
+  static_assert(BM == 256 || (BM == 224 && BN == 128 && AK && !COLSUM), "224-row tiles: K-contiguous A, BN 128");
+  static_assert(OpTile<BM, NT>::BYTES % OpTile<BM, NT>::IB == 0, "whole glds pieces");
   // 256x128 tiles fit 3 operand stages in the LDS (144 KB): K-tile kt + 2 is then fetched during k-step 0 of kt
   // (its stage was consumed in kt - 1) instead of k-step 1, so 1.5 K-tiles of fetch latency are covered (the
   // classifier forward reads a 64 MB activation straight from HBM inside the step: 76 vs 63 us from the MALL).
@@ -1187,6 +1193,21 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
       return 0;
     }
   }
+  if constexpr (BM == 224) {
+    // 224x128 tiles (1792 rows = 8 row tiles: one workgroup per CU on 4096-wide outputs), 4-wave pipelined loop with
+    // 112x64 per wave and 3 LDS stages; aligned shapes with a K-contiguous A only (the planner's condition)
+    FAN_CHECK(AK && a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0 && !a.colsum,
+              "224x128 GEMM tiles: K-contiguous A, M % 224 == 0, N % 128 == 0, no fused bias gradient");
+    if constexpr (AK && BN == 128) {
+      constexpr int lds = 3 * (BM + BN) * BK * 2;
+      auto k = gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false, 128, 224>;
+      FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+      hipLaunchKernelGGL(k, persist_grid(grid), 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
+                         (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
+                         (float*)a.workspace, a.colsum, wo);
+    }
+    return 0;
+  } else {
   constexpr int lds = lds_bytes<BM, BN>();
   // bwd-weight layout (both operands MN-contiguous): next stage's DMA by one wave per SIMD; the other layouts issue
   // it from every wave right after the barrier. (Issuing it between the two k-steps' MFMA clusters made fwd1 5 %
@@ -1200,6 +1221,7 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
                      a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace,
                      a.colsum, wo);
   return SPLIT && a.colsum ? sk : 0;
+  }
 }
 
 template <bool WIRE>
@@ -1280,6 +1302,10 @@ void launch_tile(const GemmArgs& a, int bm, int bn, int waves, int sk, hipStream
   (void)waves;
   if (bm == 256 && bn == 256) launch_epi<256, 256, 2, 4, AK, BKC>(a, sk, s);
   else if (bm == 256 && bn == 128) launch_epi<256, 128, 4, 2, AK, BKC>(a, sk, s);
+  else if (bm == 224 && bn == 128) {
+    if constexpr (AK) launch_epi<224, 128, 2, 2, AK, BKC>(a, sk, s);
+    else FAN_CHECK(false, "224x128 GEMM tiles need a K-contiguous A");
+  }
   else if (bm == 128 && bn == 256) launch_epi<128, 256, 2, 4, AK, BKC>(a, sk, s);
   else launch_epi<128, 128, 2, 4, AK, BKC>(a, sk, s);
 }

@@ -77,7 +77,8 @@ static const EnvPlans& env_plans() {
       TunedPlan t{};
       int used = 0;
       if (sscanf(q, "%dx%dx%d=%d,%d,%d%n", &t.M, &t.N, &t.K, &t.bm, &t.bn, &t.sk, &used) != 6 ||
-          (t.bm != 128 && t.bm != 256) || (t.bn != 128 && t.bn != 256) || t.sk < 1) {
+          (t.bm != 128 && t.bm != 256 && t.bm != 224) || (t.bn != 128 && t.bn != 256) ||
+          (t.bm == 224 && t.bn != 128) || t.sk < 1) {
         r.bad = true;
         break;
       }
@@ -87,7 +88,7 @@ static const EnvPlans& env_plans() {
     }
     return r;
   }();
-  FAN_CHECK(!ep.bad, "FAN_GEMM_PLAN: expected MxNxK=bm,bn,sk[;...] with bm, bn in {128, 256}");
+  FAN_CHECK(!ep.bad, "FAN_GEMM_PLAN: expected MxNxK=bm,bn,sk[;...] with bm, bn in {128, 256} (or 224x128)");
   return ep;
 }
 
@@ -130,7 +131,16 @@ static GemmPlan plan_ragged(int M, int N, int K, int split_k, int tile_bm, int t
 GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_bn, int tile_waves) {
   GemmPlan p{0, 0, 1, 8};
   if (M <= 0 || N <= 0 || K <= 0 || M % 8 || N % 8 || K % 8) return p;
+  if (tile_bm == 224) {  // 224x128 tiles, explicit only (the plan tuner's candidate for M % 224 == 0): aligned shapes
+    const int sk = split_k > 0 ? split_k : 1;
+    if (tile_bn != 128 || M % 224 || N % 128 || K % (BK * sk)) return p;
+    return GemmPlan{224, 128, sk, kDefaultWaves};
+  }
   if (tile_bm != 0 && ((tile_bm != 128 && tile_bm != 256) || (tile_bn != 128 && tile_bn != 256))) return p;
+  if (tile_bm == 0 && split_k <= 0) {
+    for (const TunedPlan& t : env_plans().plans)
+      if (t.bm == 224 && t.M == M && t.N == N && t.K == K) return gemm_bf16_plan(M, N, K, t.sk, 224, 128, 0);
+  }
   if (M % 128 || N % 128 || K % BK ||
       (tile_bm > 0 && (M % tile_bm || N % tile_bn)) || (split_k > 1 && K % (BK * split_k)))
     return plan_ragged(M, N, K, split_k, tile_bm, tile_bn);
@@ -217,6 +227,7 @@ bool gemm_bf16_supported(const GemmArgs& a) {
   if (a.accumulate && a.c_bf16) return false;
   if (p.split_k > 1 && a.workspace == nullptr) return false;
   if (a.colsum && a.b_kcontig) return false;
+  if (p.bm == 224 && (!a.a_kcontig || a.colsum)) return false;  // 224-row tiles: K-contiguous A image only
   if (a.epilogue == kEpiWire) {
     if (a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire || a.N % 16) return false;
     if (a.wire_shard <= 0 || a.wire_shard % 256 || a.ldc % 16) return false;

@@ -146,7 +146,7 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
     if plan is None and not T.worth_tuning(M, N, static, C.device):
         plan = T.keep_static(k, static)
     if plan is None:
-        T.tune(k, static, T.candidates(Cx, M, N, K), run)
+        T.tune(k, static, T.candidates(Cx, M, N, K, a_kcontig=not a_t, colsum=colsum is not None), run)
     else:
         run(plan)
 

@@ -10,8 +10,9 @@ own operands, and keeps the fastest:
 
 * only shapes whose static plan leaves the last wave of workgroups part-empty are tuned (whole-wave plans were
   chosen by in-step A/B and are kept);
-* candidates: BM x BN in {256, 128}^2 x split-K in {1, 2, 3, 4, 6, 8}, those the planner accepts for the shape,
-  with at most 4 waves of workgroups and at least 256 K-elements per split;
+* candidates: BM x BN in {256, 128}^2 (plus 224x128 for a K-contiguous A: 1792 = 8 x 224 rows) x split-K in
+  {1, 2, 3, 4, 6, 8}, those the planner accepts for the shape, with at most 4 waves of workgroups and at least 256
+  K-elements per split;
 * two interleaved rounds of 3 timed launches each (hip events), a candidate's score is its best round median;
   the static plan keeps the shape unless a candidate beats it by more than ``margin`` (5 %);
 * the winner runs last, so the caller's outputs are the winner's (every candidate computes the same product, and
@@ -32,6 +33,9 @@ import threading
 import torch
 
 TILES = ((256, 256), (256, 128), (128, 256), (128, 128))
+# 224x128: 1792 rows (the reference's per-rank batch) in 8 row tiles -> one workgroup per CU on 4096-wide outputs;
+# K-contiguous A only (the planner refuses it otherwise), no fused bias gradient
+TILES_KA = ((224, 128),)
 SPLITS = (1, 2, 3, 4, 6, 8)
 
 
@@ -55,9 +59,9 @@ class GemmTuner:
         name = torch.cuda.get_device_properties(dev).gcnArchName.split(":")[0] if torch.cuda.is_available() else ""
         return f"{name}|{M}x{N}x{K}|{int(a_t)}{int(b_t)}|e{epilogue}|c{int(colsum)}|w{int(wire)}"
 
-    def candidates(self, Cx, M, N, K):
+    def candidates(self, Cx, M, N, K, a_kcontig=False, colsum=False):
         out, seen = [], set()
-        for bm, bn in TILES:
+        for bm, bn in TILES + (TILES_KA if a_kcontig and not colsum else ()):
             for sk in SPLITS:
                 if sk > 1 and K // sk < 256:
                     continue

@@ -336,3 +336,43 @@ def test_gemm_persistent_grid_bit_identical(persist_cap, tile, cap):
                     assert (outs[1].double() - ref).abs().max().item() < 0.02 * (1 + ref.abs().max().item())
     finally:
         C.gemm_set_main_loop(mode0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1792, 512, 1024), (672, 384, 2048), (224, 128, 64)])
+def test_gemm_224x128_tile(C, M, N, K):
+    """224x128 tiles (M % 224 == 0: the reference's per-rank batch 1792 = 8 x 224 rows fills 256 CUs on 4096-wide
+    outputs; 672 = 5376 / 8 ranks), K-contiguous A on both B layouts, with and without split-K, bias / ReLU /
+    ReLU-mask epilogues, persistent grids capped below the tile count: vs an fp64 reference."""
+    torch.manual_seed(M + K)
+    A = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    Bkn = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    ref = _ref_mm(A.float(), Bkn.float())
+    bound = _elem_bound(A.float(), Bkn.float())
+    assert tuple(C.gemm_plan(M, N, K, 1, 224, 128, 0))[:3] == (224, 128, 1)
+    assert C.gemm_plan(M, N, K, 1, 224, 256, 0)[0] == 0  # 224 rows pair with 128 columns only
+    cap0 = C.gemm_persist()
+    try:
+        for b_t in (False, True):
+            Bin = Bkn.t().contiguous() if b_t else Bkn
+            for sk in (1, 2) if K % 128 == 0 else (1,):
+                for cap in (cap0, 3):
+                    C.gemm_set_persist(cap)
+                    Cout = torch.full((M, N), float("nan"), device=DEV)
+                    G.gemm(A, False, Bin, b_t, Cout, split_k=sk, tile=(224, 128))
+                    err = (Cout.double() - ref).abs()
+                    assert bool((err <= bound).all()), f"b_t={b_t} split_k={sk} cap={cap}: max err {err.max().item()}"
+    finally:
+        C.gemm_set_persist(cap0)
+    bias = torch.randn(N, device=DEV).to(torch.bfloat16)
+    Y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm(A, False, Bkn, False, Y, G.EPI_BIAS_RELU, bias=bias, split_k=1, tile=(224, 128))
+    want = torch.relu(ref + bias.double())
+    assert (Y.double() - want).abs().max().item() <= (bound.max().item() + 1e-2 * want.abs().max().item())
+    act = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    Bnk = Bkn.t().contiguous()
+    dX = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    G.gemm(A, False, Bnk, True, dX, G.EPI_RELU_MASK, aux=act, split_k=1, tile=(224, 128))
+    want = ref * (act.double() > 0)
+    assert (dX.double() - want).abs().max().item() <= (bound.max().item() + 1e-2 * want.abs().max().item())
+    with pytest.raises(Exception):  # an MN-contiguous A has no 224-row image
+        G.gemm(A.t().contiguous(), True, Bkn, False, torch.empty(M, N, device=DEV), split_k=1, tile=(224, 128))
