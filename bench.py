@@ -316,6 +316,8 @@ def main(argv=None):
                 "engine": impl,
                 "hip_graph": graphed,
                 "fused_sgd": True,
+                # world 1: dW's BFP round trip + SGD inside the bwd-weight GEMM epilogue (no separate update pass)
+                "fused_update_in_gemm": bool(getattr(trainer, "fused_update", False)),
                 "epilogue_stream": ("compute" if getattr(engine, "epilogue_on_producer", False) else "comm")
                 if engine is not None and not getattr(engine, "inline", True) else "inline",
             },

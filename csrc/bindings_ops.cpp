@@ -29,7 +29,10 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux, bool accumulate,
           int64_t split_k, const c10::optional<at::Tensor>& workspace, int64_t tile_bm, int64_t tile_bn,
           const c10::optional<at::Tensor>& colsum, int64_t tile_waves, const c10::optional<at::Tensor>& wire,
-          int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period) {
+          int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period,
+          const c10::optional<at::Tensor>& upd_master, const c10::optional<at::Tensor>& upd_lp,
+          const c10::optional<at::Tensor>& upd_mom, double upd_lr, double upd_grad_scale, double upd_weight_decay,
+          double upd_momentum, bool upd_nesterov) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "A and B dtype mismatch");
   GemmArgs g{};
@@ -83,6 +86,27 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     g.wire_own = (int)wire_own;
     g.wire_period = (int)wire_period;
     g.wire_codec = (int)wire_codec;
+    if (upd_master) {  // fused local update: the bucket planes cover every flat index the epilogue touches
+      auto plane = [&](const at::Tensor& t, at::ScalarType st, const char* what) {
+        TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == st && t.numel() > last &&
+                        t.data_ptr() != nullptr && (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0,
+                    "fused update: ", what, " must be a contiguous, 16-B aligned GPU plane covering the bucket");
+      };
+      TORCH_CHECK(wire_own == -1, "fused update: no owner shard (single-rank engine)");
+      TORCH_CHECK(wire_codec == kBfpRne, "fused update: rne codec only");
+      plane(*upd_master, at::kFloat, "master");
+      g.upd_master = upd_master->data_ptr<float>();
+      if (upd_lp) {
+        plane(*upd_lp, at::kBFloat16, "lp");
+        g.upd_lp = reinterpret_cast<bf16_t*>(upd_lp->data_ptr());
+      }
+      if (upd_mom) {
+        plane(*upd_mom, at::kFloat, "mom");
+        g.upd_mom = upd_mom->data_ptr<float>();
+      }
+      g.upd = SgdParams{(float)upd_lr, (float)upd_grad_scale, (float)upd_weight_decay, (float)upd_momentum,
+                        upd_nesterov ? 1 : 0};
+    }
   }
   if (A.scalar_type() == at::kBFloat16) {
     TORCH_CHECK(bias ? bias->scalar_type() == at::kBFloat16 : true, "bias must be bf16");
@@ -162,7 +186,11 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("workspace") = pybind11::none(), pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0,
         pybind11::arg("colsum") = pybind11::none(), pybind11::arg("tile_waves") = 0,
         pybind11::arg("wire") = pybind11::none(), pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1,
-        pybind11::arg("wire_codec") = 1, pybind11::arg("wire_period") = 0);
+        pybind11::arg("wire_codec") = 1, pybind11::arg("wire_period") = 0,
+        pybind11::arg("upd_master") = pybind11::none(), pybind11::arg("upd_lp") = pybind11::none(),
+        pybind11::arg("upd_mom") = pybind11::none(), pybind11::arg("upd_lr") = 0.0,
+        pybind11::arg("upd_grad_scale") = 1.0, pybind11::arg("upd_weight_decay") = 0.0,
+        pybind11::arg("upd_momentum") = 0.0, pybind11::arg("upd_nesterov") = false);
   m.def("gemm_supported", &gemm_supported);
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);

@@ -8,6 +8,7 @@
 #pragma once
 #include <atomic>
 
+#include "bfp/bfp_format.h"  // SgdParams (fused local update)
 #include "common/hip_common.h"
 
 namespace fan {
@@ -18,7 +19,9 @@ enum GemmEpilogue : int {
   kEpiBiasRelu = 2,   // relu(x + bias[n])
   kEpiReluMask = 3,   // x * (aux[m][n] > 0)   (ReLU backward fused into the bwd-data GEMM)
   kEpiWire = 4,       // BFP-encode the f32 result straight into all-reduce wire shards (see GemmArgs::wire)
+  kEpiWireUpd = 5,    // kernel-internal: kEpiWire with the fused local update (GemmArgs::upd_master set)
 };
+constexpr bool is_wire_epi(int e) { return e == kEpiWire || e == kEpiWireUpd; }
 
 // GemmArgs::wire_own value: every shard is also written to C in f32 (the ring needs every local slice in f32:
 // each reduce hop adds the local f32 contribution, hw/all_reduce.sv:1168-1183)
@@ -54,6 +57,13 @@ struct GemmArgs {
   int wire_own = -1;
   int wire_period = 0;  // > 0: every shard s with s % wire_period == wire_own is owned (chunked mesh buckets)
   int wire_codec = 1;  // kBfpTrunc or kBfpRne
+  // kEpiWire fused local update (single-rank engine): instead of storing the wire, every encoded group is decoded
+  // in registers and applied by SGD to the bucket planes at the same flat indices (upd_master f32, upd_lp bf16
+  // copy, upd_mom optional; wire_own must be -1). See WireOut::um (gemm_bf16_kernel.h).
+  float* upd_master = nullptr;
+  bf16_t* upd_lp = nullptr;
+  float* upd_mom = nullptr;
+  SgdParams upd{};
 };
 
 struct GemmPlan {

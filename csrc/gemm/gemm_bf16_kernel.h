@@ -218,6 +218,15 @@ struct WireOut {
   int codec;      // kBfpTrunc / kBfpRne
   float inv_shard;  // 1 / shard (shard index without a 64-bit integer division)
   int bias_off;     // > 0: flat offset of the bias segment, encoded from the fused column sum
+  // Fused local update (single-rank engine: the all-reduce of one rank is the identity): um != nullptr replaces the
+  // wire stores by the SGD update of the bucket in place — each 16-value group takes its BFP round trip in registers
+  // (encode -> decode: exactly the values the one-rank all-reduce hands its decode + SGD epilogue) and updates
+  // master (f32), lp (bf16 copy) and mom at the same flat indices. The NIC's weight-update unit consumes the
+  // all-reduce output stream the same way, without a round trip through host memory (hw/weight_update.sv:433-452).
+  float* um;
+  bf16_t* ulp;
+  float* umom;
+  SgdParams up;
 #ifdef FAN_GEMM_STAMPS
   unsigned long long* stamps;  // diagnostic builds: s_memtime stamp buffer (see FAN_STAMP)
 #endif
@@ -240,15 +249,74 @@ __device__ __forceinline__ int32_t wire_encode(float x, uint32_t E, int codec) {
   return codec == kBfpTrunc ? bfp_encode_trunc(__float_as_uint(x), E) : bfp_encode_rne(x, E);
 }
 
+// BFP round trip of one value of a group with shared exponent E, as the single-rank all-reduce delivers it to its
+// decode + SGD epilogue (framework codec only: the fused update is built for rne — with both codecs' branches the
+// epilogue grows past the unroller's limit and the accumulator array lands in scratch memory).
+__device__ __forceinline__ float wire_roundtrip_rne(float x, uint32_t E) {
+  return bfp_decode_rne(bfp_encode_rne(x, E), E);  // |q| <= 127: the stored byte decodes to q
+}
+
+// One element of the fused update: the same operations, in the same order, as wire_sgd_kernel (bfp_kernels.hip), so
+// the fused and the unfused single-rank step produce bit-identical weights.
+__device__ __forceinline__ float sgd_apply(float g, float& w, float& m, bool has_mom, const SgdParams& p) {
+  float gj = g * p.grad_scale;
+  if (p.weight_decay != 0.0f) gj = fmaf(p.weight_decay, w, gj);
+  if (has_mom) {
+    m = fmaf(p.momentum, m, gj);
+    gj = p.nesterov ? fmaf(p.momentum, m, gj) : m;
+  }
+  w = fmaf(-p.lr, gj, w);
+  return w;
+}
+
+// Fused update of the 16-value group at flat index f (shared exponent E already computed): 16-B master / mom
+// loads and stores, one 32-B bf16 store.
+__device__ __forceinline__ void local_update16(const float v[16], uint32_t E, uint32_t f, const WireOut& wo) {
+  float w[16], m[16];
+#pragma unroll
+  for (int u = 0; u < 16; u += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(wo.um + f + u);
+    w[u] = a.x; w[u + 1] = a.y; w[u + 2] = a.z; w[u + 3] = a.w;
+  }
+  const bool hm = wo.umom != nullptr;
+  if (hm) {
+#pragma unroll
+    for (int u = 0; u < 16; u += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(wo.umom + f + u);
+      m[u] = a.x; m[u + 1] = a.y; m[u + 2] = a.z; m[u + 3] = a.w;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) sgd_apply(wire_roundtrip_rne(v[u], E), w[u], m[u], hm, wo.up);
+#pragma unroll
+  for (int u = 0; u < 16; u += 4) {
+    *reinterpret_cast<float4*>(wo.um + f + u) = make_float4(w[u], w[u + 1], w[u + 2], w[u + 3]);
+    if (hm) *reinterpret_cast<float4*>(wo.umom + f + u) = make_float4(m[u], m[u + 1], m[u + 2], m[u + 3]);
+  }
+  if (wo.ulp) {
+    uint4* d = reinterpret_cast<uint4*>(wo.ulp + f);
+    d[0] = make_uint4(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                      pack_bf16x2(w[6], w[7]));
+    d[1] = make_uint4(pack_bf16x2(w[8], w[9]), pack_bf16x2(w[10], w[11]), pack_bf16x2(w[12], w[13]),
+                      pack_bf16x2(w[14], w[15]));
+  }
+}
+
 // Encode the 16-value group at flat bucket index f (f % 16 == 0) held by this lane: 16-B mantissa store +
-// 1 exponent byte. Returns the shard it landed in.
+// 1 exponent byte (or, with the fused local update, the update of the group in place). Returns the shard it
+// landed in (-1: updated in place).
+template <bool UPD = false>
 __device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const WireOut& wo) {
-  const int sh = wire_shard_of(f, wo);
-  const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
   uint32_t mx = 0;
 #pragma unroll
   for (int u = 0; u < 16; ++u) mx = max(mx, __float_as_uint(v[u]) & 0x7FFFFFFFu);
   const uint32_t E = mx >> 23;
+  if constexpr (UPD) {
+    local_update16(v, E, f, wo);
+    return -1;
+  }
+  const int sh = wire_shard_of(f, wo);
+  const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
   uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int u = 0; u < 16; ++u) w[u >> 2] |= ((uint32_t)wire_encode(v[u], E, wo.codec) & 0xFFu) << (8 * (u & 3));
@@ -259,11 +327,12 @@ __device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const
 }
 
 // Encode one whole 16-column group of C(row, col..col+15); the owner shard is also written to C in f32.
+template <bool UPD = false>
 __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
                                            int row, int col) {
   const uint32_t f = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
-  const int sh = wire_store16(v, f, wo);
-  if (wo.own == kWireOwnAll || (wo.period > 0 ? sh % wo.period : sh) == wo.own) {
+  const int sh = wire_store16<UPD>(v, f, wo);
+  if (sh >= 0 && (wo.own == kWireOwnAll || (wo.period > 0 ? sh % wo.period : sh) == wo.own)) {
 #pragma unroll
     for (int u = 0; u < 16; u += 4)
       *reinterpret_cast<float4*>(C + f + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
@@ -283,13 +352,23 @@ __device__ __forceinline__ void colsum_finish(float (&cs)[NJ], int lane, int col
     v += __shfl_xor(v, 32);
     const int col = col0 + j * 16 + (lane & 15);
     if (lane < 16 && col < N) out[col] = v;
-    if constexpr (EPI == kEpiWire && !SPLIT) {
+    if constexpr (is_wire_epi(EPI) && !SPLIT) {
       if (wo.bias_off > 0 && col0 + j * 16 < N) {  // N % 16 == 0: the 16-column group is wholly in range
         uint32_t mx = __float_as_uint(v) & 0x7FFFFFFFu;
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
         const uint32_t E = mx >> 23;
         const uint32_t f = (uint32_t)wo.bias_off + (uint32_t)col;
+        if constexpr (EPI == kEpiWireUpd) {  // fused local update of the bias segment, one element per lane
+          if (lane < 16) {
+            float w = wo.um[f], m = wo.umom ? wo.umom[f] : 0.f;
+            sgd_apply(wire_roundtrip_rne(v, E), w, m, wo.umom != nullptr, wo.up);
+            wo.um[f] = w;
+            if (wo.umom) wo.umom[f] = m;
+            if (wo.ulp) wo.ulp[f] = f32_to_bf16(w);
+          }
+          continue;
+        }
         const int sh = wire_shard_of(f, wo);
         const uint32_t pos = f - (uint32_t)sh * (uint32_t)wo.shard;
         uint8_t* base = wire_shard_base(sh, wo);
@@ -345,7 +424,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
 #pragma unroll
       for (int r = 0; r < 4; ++r) stg[(row_l + r) * EW + j * 16 + col_l] = acc[i][j][r];
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own LDS writes landed (wave-private region)
-    if constexpr (EPI == kEpiWire && !SPLIT) {
+    if constexpr (is_wire_epi(EPI) && !SPLIT) {
       constexpr int G16 = WTN / 16;  // groups per staged row
       constexpr int RPG = 64 / G16;  // rows per pass (lanes beyond 16 rows idle)
       constexpr int PASSES = RPG >= 16 ? 1 : 16 / RPG;
@@ -361,7 +440,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
             v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
           }
           if (!mn_edge || (row0 + i * 16 + rr < M && col0 + cc < N))
-            wire_epi16(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr, col0 + cc);
+            wire_epi16<EPI == kEpiWireUpd>(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr, col0 + cc);
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -1021,7 +1100,7 @@ __global__ void __launch_bounds__(256)
 // encodes the group into the all-reduce wire (owner shard also in f32). With colsum, the threads past the
 // M*N/16 groups reduce the split_k bias partial sums (ws[split_k * M * N + k * N]), write colsum[] and encode the
 // bias segment of the [W | b] bucket.
-template <int kUnused = 0>
+template <bool UPD>
 __global__ void __launch_bounds__(256)
     splitk_reduce_wire_kernel(const float* __restrict__ ws, int split_k, float* __restrict__ C, int64_t ldc, int M,
                               int N, float* __restrict__ colsum, WireOut wo) {
@@ -1049,11 +1128,11 @@ __global__ void __launch_bounds__(256)
       }
     }
     if (!bias) {
-      wire_epi16(v, C, ldc, wo, row, col);
+      wire_epi16<UPD>(v, C, ldc, wo, row, col);
     } else {
 #pragma unroll
       for (int u = 0; u < 16; ++u) colsum[col + u] = v[u];
-      if (wo.bias_off > 0) wire_store16(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
+      if (wo.bias_off > 0) wire_store16<UPD>(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
     }
   }
 }
@@ -1061,7 +1140,7 @@ __global__ void __launch_bounds__(256)
 // Ordered reduce of bias-gradient partial slabs part[p * N + n], p < parts, into colsum[n]; WIRE: also encodes the
 // bias segment of the [W | b] bucket (flat wo.bias_off + n). One block per 64 columns: 16 lanes x float4 columns by
 // 16 part classes (p % 16), each summed in p order, then the classes summed in class order (deterministic).
-template <bool WIRE>
+template <bool WIRE, bool UPD = false>
 __global__ void __launch_bounds__(256)
     colsum_reduce_kernel(const float* __restrict__ part, int parts, float* __restrict__ colsum, int N, WireOut wo) {
   __shared__ float4 red[16][16];
@@ -1093,7 +1172,7 @@ __global__ void __launch_bounds__(256)
       float v[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) v[u] = fin[t * 16 + u];
-      wire_store16(v, (uint32_t)wo.bias_off + (uint32_t)c16, wo);
+      wire_store16<UPD>(v, (uint32_t)wo.bias_off + (uint32_t)c16, wo);
     }
   }
 }
@@ -1224,16 +1303,17 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
   }
 }
 
-template <bool WIRE>
+template <bool WIRE, bool UPD = false>
 void launch_colsum_reduce(const float* part, int parts, const GemmArgs& a, const WireOut& wo, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_reduce_kernel<WIRE>, cdiv_i(a.N, 64), 256, 0, s, part, parts, a.colsum, a.N, wo);
+  hipLaunchKernelGGL((colsum_reduce_kernel<WIRE, UPD>), cdiv_i(a.N, 64), 256, 0, s, part, parts, a.colsum, a.N, wo);
 }
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
 void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_period, a.wire_codec,
                    a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
-                   a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0
+                   a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0,
+                   a.upd_master, a.upd_lp, a.upd_mom, a.upd
 #ifdef FAN_GEMM_STAMPS
                    , (unsigned long long*)gemm_stamp_buffer()
 #endif
@@ -1241,10 +1321,12 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   if (sk > 1) {
     // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + p*N]), then an ordered reduce that
     // applies the epilogue (deterministic: slabs summed in split order)
-    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, true>(a, sk, wo, s);
-    if constexpr (EPI == kEpiWire) {
+    // (the split main loop only writes slabs: the wire / update variants share one kernel)
+    constexpr int kMainEpi = EPI == kEpiWireUpd ? kEpiWire : EPI;
+    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, kMainEpi, TC, ACCUM, true>(a, sk, wo, s);
+    if constexpr (is_wire_epi(EPI)) {
       const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
-      hipLaunchKernelGGL(splitk_reduce_wire_kernel<0>, stream_grid(items), 256, 0, s, (const float*)a.workspace, sk,
+      hipLaunchKernelGGL(splitk_reduce_wire_kernel<EPI == kEpiWireUpd>, stream_grid(items), 256, 0, s, (const float*)a.workspace, sk,
                          (float*)a.C, a.ldc, a.M, a.N, a.colsum, wo);
     } else {
       hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
@@ -1256,7 +1338,8 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   } else {
     // bias-gradient partials at ws[p * N] (pipelined loop): ordered reduce (+ the bias segment's wire encode)
     const int parts = launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>(a, sk, wo, s);
-    if (parts > 0) launch_colsum_reduce<EPI == kEpiWire>((const float*)a.workspace, parts, a, wo, s);
+    if (parts > 0)
+      launch_colsum_reduce<is_wire_epi(EPI), EPI == kEpiWireUpd>((const float*)a.workspace, parts, a, wo, s);
   }
 }
 
@@ -1276,7 +1359,8 @@ void launch_epi(const GemmArgs& a, int sk, hipStream_t s) {
     case kEpiWire:  // only the bwd-weight layout (A and B MN-contiguous) produces wire-ready gradients
       if constexpr (!AK && !BKC) {
         FAN_CHECK(!a.c_bf16 && !a.accumulate, "wire epilogue: f32, no accumulate");
-        launch_typed<BM, BN, WM, WN, AK, BKC, kEpiWire, float, false>(a, sk, s);
+        if (a.upd_master) launch_typed<BM, BN, WM, WN, AK, BKC, kEpiWireUpd, float, false>(a, sk, s);
+        else launch_typed<BM, BN, WM, WN, AK, BKC, kEpiWire, float, false>(a, sk, s);
         break;
       }
       FAN_CHECK(false, "wire epilogue needs A and B MN-contiguous (bwd-weight layout)");

@@ -53,18 +53,23 @@ def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
 
 
 def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux=None, accumulate=False,
-         split_k: int | None = None, tile: tuple | None = None, colsum=None, wire=None):
+         split_k: int | None = None, tile: tuple | None = None, colsum=None, wire=None, update=None):
     """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
     ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only).
     ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N]).
     ``wire=(buf_u8, shard_elems, own_shard, codec_id[, period])``: BFP-encode the f32 result straight into all-reduce
     wire shards (flat index m*ldc + n; shard ``own_shard`` — with ``period``, every shard s with s % period ==
-    own_shard — is also written to C) — bf16 bwd-weight only."""
+    own_shard — is also written to C) — bf16 bwd-weight only.
+    ``update`` (with ``wire``, single-rank engine): a :class:`LocalUpdate` — the encoded groups are not stored but
+    decoded in registers and applied by SGD to the bucket planes in place (the fused local update, see
+    csrc/gemm/gemm_bf16_kernel.h WireOut::um)."""
     if wire is not None:
         if not C.is_cuda or A.dtype != torch.bfloat16 or not a_t or b_t:
             raise ValueError("wire epilogue: bf16 GPU bwd-weight layout only")
-        _bf16(_ext.require(), A, a_t, B, b_t, C, EPI_WIRE, None, None, False, split_k, tile, colsum, wire)
+        _bf16(_ext.require(), A, a_t, B, b_t, C, EPI_WIRE, None, None, False, split_k, tile, colsum, wire, update)
         return C
+    if update is not None:
+        raise ValueError("update needs the wire epilogue")
     if C.is_cuda:
         Cx = _ext.require()
         if colsum is not None and (A.dtype != torch.bfloat16 or b_t):
@@ -109,9 +114,28 @@ def _shares_storage(C, *ts) -> bool:
     return any(t is not None and t.untyped_storage().data_ptr() == c for t in ts)
 
 
-def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, wire):
+class LocalUpdate:
+    """SGD target of the fused local update: the bucket planes (flat, padded) and the hyper-parameters, the same
+    operation as the engine's decode + SGD epilogue (csrc/bfp/bfp_kernels.hip wire_sgd_kernel)."""
+
+    __slots__ = ("master", "lp", "mom", "lr", "grad_scale", "weight_decay", "momentum", "nesterov")
+
+    def __init__(self, master, lp=None, mom=None, *, lr, grad_scale=1.0, weight_decay=0.0, momentum=0.0,
+                 nesterov=False):
+        self.master, self.lp, self.mom = master, lp, mom
+        self.lr, self.grad_scale, self.weight_decay = float(lr), float(grad_scale), float(weight_decay)
+        self.momentum, self.nesterov = float(momentum), bool(nesterov)
+
+    def kwargs(self):
+        return dict(upd_master=self.master, upd_lp=self.lp, upd_mom=self.mom, upd_lr=self.lr,
+                    upd_grad_scale=self.grad_scale, upd_weight_decay=self.weight_decay, upd_momentum=self.momentum,
+                    upd_nesterov=self.nesterov)
+
+
+def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, wire, update=None):
     """bf16 MFMA GEMM launch with its plan: explicit (tile / split_k given), tuned on the device on a shape's first
-    call (ops/gemm_tune.py), or the static planner's."""
+    call (ops/gemm_tune.py), or the static planner's. With a fused ``update`` the tuner's trial launches store the
+    wire instead (an update is not re-runnable); the chosen plan then runs once more with the update."""
     M = A.shape[1] if a_t else A.shape[0]
     K = A.shape[0] if a_t else A.shape[1]
     N = B.shape[0] if b_t else B.shape[1]
@@ -124,13 +148,13 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
         buf, shard, own, codec = wire[:4]
         period = int(wire[4]) if len(wire) > 4 else 0
 
-    def run(plan, waves=0):
+    def run(plan, waves=0, upd=None):
         bm, bn, sk = plan  # launch exactly this tile (re-planning with an explicit split_k differs)
         need = _bf16_ws_floats(M, N, sk, bm, colsum)
         ws = _workspace(C.device, need) if need else None
         if wire is not None:
             Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, bm, bn, colsum, waves, buf, int(shard),
-                    int(own), int(codec), period)
+                    int(own), int(codec), period, **(upd.kwargs() if upd is not None else {}))
         else:
             Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, bm, bn, colsum, waves)
 
@@ -139,16 +163,19 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
     T = gemm_tune.tuner()
     if (tile is not None or split_k is not None or not T.enabled or accumulate
             or torch.cuda.is_current_stream_capturing() or _shares_storage(C, A, B, aux, bias)):
-        run(tuple(static[:3]), tw)
+        run(tuple(static[:3]), tw, update)
         return
-    k = T.key(M, N, K, a_t, b_t, epilogue, colsum is not None, wire is not None, C.device)
+    k = T.key(M, N, K, a_t, b_t, epilogue, colsum is not None, 0 if wire is None else 2 if update is not None else 1,
+              C.device)
     plan = T.lookup(k)
     if plan is None and not T.worth_tuning(M, N, static, C.device):
         plan = T.keep_static(k, static)
     if plan is None:
-        T.tune(k, static, T.candidates(Cx, M, N, K, a_kcontig=not a_t, colsum=colsum is not None), run)
+        plan = T.tune(k, static, T.candidates(Cx, M, N, K, a_kcontig=not a_t, colsum=colsum is not None), run)
+        if update is not None:
+            run(plan, 0, update)
     else:
-        run(plan)
+        run(plan, 0, update)
 
 
 def linear_fwd(x, w, b, out, relu: bool):
@@ -162,9 +189,10 @@ def linear_bwd_data(dz, w, out, relu_input=None):
     return gemm(dz, False, w, True, out, EPI_NONE)
 
 
-def linear_bwd_weight(x, dz, out, accumulate=False, bias_grad=None, wire=None):
+def linear_bwd_weight(x, dz, out, accumulate=False, bias_grad=None, wire=None, update=None):
     """dW = Xᵀ · dZ (f32 out); with ``bias_grad`` also db = colsum(dZ), fused into the same kernel; with
-    ``wire`` dW is written BFP-encoded into the all-reduce wire buffer instead (see :func:`gemm`)."""
+    ``wire`` dW is written BFP-encoded into the all-reduce wire buffer instead (see :func:`gemm`); with ``update``
+    (single-rank engine) the encoded dW updates the weights in place instead."""
     if wire is not None:
-        return gemm(x, True, dz, False, out, EPI_WIRE, colsum=bias_grad, wire=wire)
+        return gemm(x, True, dz, False, out, EPI_WIRE, colsum=bias_grad, wire=wire, update=update)
     return gemm(x, True, dz, False, out, EPI_NONE, accumulate=accumulate, colsum=bias_grad)

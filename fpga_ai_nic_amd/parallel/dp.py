@@ -18,6 +18,7 @@ import time
 import torch
 
 from ..models.mlp import MLP
+from ..ops import gemm as G
 from ..ops import wire
 from ..utils import tracing
 from .allreduce import CompressedAllReduce, Handle, _round_up
@@ -77,13 +78,21 @@ class DataParallelTrainer:
     def __init__(self, model: MLP, engine: CompressedAllReduce | None, *, lr: float = 0.1,
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
                  loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True,
-                 commit_at_end: bool | None = None, panels: int | None = None, panel_submit: str = "split"):
+                 commit_at_end: bool | None = None, panels: int | None = None, panel_submit: str = "split",
+                 fused_update: bool | None = None):
         """``panels`` (default env FAN_PANELS, else off; < 2 disables): the
         last-issued bucket (layer 0: no backward left to hide its exchange behind) is computed as row panels of dW,
         each submitted as a request of its own right after its GEMM (multi-rank C++ engine, mesh, GEMM-encoded
         wire only). ``panel_submit='whole'`` computes
         the same panels but submits the bucket as one request of the same chunked layout (the unsplit schedule,
-        bit-identical results)."""
+        bit-identical results).
+
+        ``fused_update`` (default env FAN_FUSED_UPDATE, else on): with a single-rank engine (world 1, requests
+        inline: the all-reduce of one rank is the identity) and the GEMM-encoded wire, the bwd-weight GEMM's epilogue
+        takes each encoded gradient group through its BFP round trip in registers and applies the SGD update to the
+        layer's weights in place — the engine's decode + SGD pass over the whole bucket (master read + write, bf16
+        copy write, wire read) disappears into the GEMM. Same operations in the same order: bit-identical weights
+        to the unfused schedule. The layer's bwd-data GEMM (which reads the weights) is issued first."""
         self.m = model
         self.engine = engine
         self.world = engine.world if engine is not None else 1
@@ -104,6 +113,10 @@ class DataParallelTrainer:
                               else commit_at_end)
         self.prepack = (prepack and engine is not None and getattr(engine, "prepack", False) and self.cuda
                         and model.dtype == torch.bfloat16)
+        fu = os.environ.get("FAN_FUSED_UPDATE", "1") != "0" if fused_update is None else bool(fused_update)
+        self.fused_update = (fu and self.prepack and bool(getattr(engine, "inline", False))
+                             and getattr(engine, "codec", "") == "bfp_rne")
+        self.fused_updates = 0
         self.panel_submit = panel_submit
         self.panel_plans: dict[int, dict] = {}
         # opt-in (FAN_PANELS=4): measured on the one-GPU pool the split costs more than it hides — each panel adds a
@@ -222,20 +235,29 @@ class DataParallelTrainer:
                 # (the wire epilogue encodes whole 16-column groups: output widths that are multiples of 16)
                 tgt = (self.engine.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout)
                        if self.prepack and l.cout % 16 == 0 else None)
-                m.backward_weight(i, wire=tgt)
-                h = None
-                if self.engine is not None:
-                    kw = {"prepacked": (tgt[0], l.n_pad)} if tgt is not None else {}
-                    h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
-                                                  grad_scale=self.grad_scale, weight_decay=self.wd,
-                                                  momentum=self.momentum, nesterov=self.nesterov, defer=True,
-                                                  name=f"fc{i}", **kw)
-                m.backward_data(i)
-                if h is not None:
-                    self.pending[i] = h if self.commit_at_end else h.commit_after_current()
-                    self.last_handle = self.pending[i]
+                if tgt is not None and self.fused_update:
+                    # single-rank engine: bwd-data first (it reads W_i), then dW's BFP round trip + SGD in the
+                    # bwd-weight epilogue
+                    m.backward_data(i)
+                    m.backward_weight(i, wire=tgt, update=G.LocalUpdate(
+                        l.master, l.lp, l.mom, lr=self.lr, grad_scale=self.grad_scale, weight_decay=self.wd,
+                        momentum=self.momentum, nesterov=self.nesterov))
+                    self.fused_updates += 1
                 else:
-                    self._sgd_local(l)
+                    m.backward_weight(i, wire=tgt)
+                    h = None
+                    if self.engine is not None:
+                        kw = {"prepacked": (tgt[0], l.n_pad)} if tgt is not None else {}
+                        h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
+                                                      grad_scale=self.grad_scale, weight_decay=self.wd,
+                                                      momentum=self.momentum, nesterov=self.nesterov, defer=True,
+                                                      name=f"fc{i}", **kw)
+                    m.backward_data(i)
+                    if h is not None:
+                        self.pending[i] = h if self.commit_at_end else h.commit_after_current()
+                        self.last_handle = self.pending[i]
+                    else:
+                        self._sgd_local(l)
             if prof and i == m.L - 1:
                 self._sync()
                 t1 = time.perf_counter()
