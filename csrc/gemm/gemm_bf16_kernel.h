@@ -916,7 +916,8 @@ __global__ void __launch_bounds__(256, 1)
   // 224x128 tiles: 1792 rows (the reference's per-rank batch, sw/run.sh:16) are 8 row tiles, so a 1792 x 4096 output
   // is 8 x 32 = 256 workgroups, one per CU (256-row tiles give 7 x 32 = 224 and leave 32 CUs idle). The A image is
   // K-contiguous ([rows][64 k], 32 rows per glds piece: 7 pieces); an MN-contiguous A stages 128-column halves.
-  static_assert(BM == 256 || (BM == 224 && BN == 128 && AK && !COLSUM), "224-row tiles: K-contiguous A, BN 128");
+  static_assert(BM == 256 || (BM == 224 && BN == 128 && AK && !COLSUM) || (BM == 128 && BN == 128),
+                "256-row tiles; 224-row tiles (K-contiguous A, BN 128); 128x128 tiles");
   static_assert(OpTile<BM, NT>::BYTES % OpTile<BM, NT>::IB == 0, "whole glds pieces");
   // 256x128 tiles fit 3 operand stages in the LDS (144 KB): K-tile kt + 2 is then fetched during k-step 0 of kt
   // (its stage was consumed in kt - 1) instead of k-step 1, so 1.5 K-tiles of fetch latency are covered (the
@@ -1245,6 +1246,30 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
         }
       }
       launch(gemm_pl_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>);
+      return 0;
+    }
+  }
+  if constexpr (BM == 128 && BN == 128) {
+    // 128x128 tiles on the 4-wave pipelined loop (64x64 per wave, 3 LDS stages): outputs too small for 256-wide tiles
+    // to fill the CUs without split-K — the bwd-weight GEMMs of the 1024-wide layers (4096 x 1024, K = the batch:
+    // 256 tiles, one per CU, no f32 slabs and no reduce pass) — instead of the one-role 8-wave loop
+    const int mode = main_loop_mode();
+    const bool aligned = a.M % BM == 0 && a.N % BN == 0 && a.K % (BK * sk) == 0;
+    if ((mode == 2 || mode == 3) && aligned && (!a.colsum || a.workspace)) {
+      constexpr int lds = 3 * (BM + BN) * BK * 2;
+      auto launch = [&](auto k, bool persist) {
+        FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda,
+                           (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
+                           a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace, a.colsum, wo);
+      };
+      if constexpr (!BKC) {
+        if (a.colsum) {
+          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true, 128, 128>, false);
+          return SPLIT ? sk : a.M / BM;
+        }
+      }
+      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false, 128, 128>, true);
       return 0;
     }
   }

@@ -117,12 +117,6 @@ class DataParallelTrainer:
         self.fused_update = (fu and self.prepack and bool(getattr(engine, "inline", False))
                              and getattr(engine, "codec", "") == "bfp_rne")
         self.fused_updates = 0
-        # fused path: bwd-weight GEMMs of layers >= 1 on a second stream (FAN_BWD_STREAMS=2), so each runs beside the
-        # main stream's next GEMM and its tail (the update's HBM traffic, the split-K reduce) fills CUs the other
-        # GEMM is not using; layer 0's bwd-weight stays on the main stream beside layer 1's
-        self.bwd_streams = int(os.environ.get("FAN_BWD_STREAMS", "1"))
-        self._side = None
-        self._ev = None
         self.panel_submit = panel_submit
         self.panel_plans: dict[int, dict] = {}
         # opt-in (FAN_PANELS=4): measured on the one-GPU pool the split costs more than it hides — each panel adds a
@@ -247,12 +241,9 @@ class DataParallelTrainer:
                     m.backward_data(i)
                     upd = G.LocalUpdate(l.master, l.lp, l.mom, lr=self.lr, grad_scale=self.grad_scale,
                                         weight_decay=self.wd, momentum=self.momentum, nesterov=self.nesterov)
-                    if self.bwd_streams > 1 and i >= 1 and self.cuda:
-                        side = self._fork()
-                        with torch.cuda.stream(side):
-                            m.backward_weight(i, wire=tgt, update=upd)
-                    else:
-                        m.backward_weight(i, wire=tgt, update=upd)
+                    # (the bwd-weight GEMMs of layers >= 1 on a second stream, beside the next GEMM, measured 1.5-2 %
+                    # slower: profiles/r3_fused_update_ab.txt)
+                    m.backward_weight(i, wire=tgt, update=upd)
                     self.fused_updates += 1
                 else:
                     m.backward_weight(i, wire=tgt)
@@ -275,7 +266,6 @@ class DataParallelTrainer:
                 self.times["bwd_first"] += t1 - t0
                 self.times["bwd"] += t1 - t0
                 t0 = t1
-        self._join()
         if self.commit_at_end:  # issue order L-1..0: the epilogues run in the order their all-reduces finish
             for i in reversed(range(m.L)):
                 h = self.pending[i]
@@ -284,24 +274,6 @@ class DataParallelTrainer:
         if prof:
             self._sync()
             self.times["bwd"] += time.perf_counter() - t0
-
-    def _fork(self):
-        """The side stream, ordered after everything issued so far on the current stream."""
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=self.m.device)
-            self._ev = [torch.cuda.Event(), torch.cuda.Event()]
-        self._ev[0].record()
-        self._side.wait_event(self._ev[0])
-        self._side_used = True
-        return self._side
-
-    def _join(self):
-        """The current stream waits for the side stream's GEMMs (the next forward reads the weights they update and
-        overwrites the activations they read)."""
-        if getattr(self, "_side_used", False):
-            self._ev[1].record(self._side)
-            torch.cuda.current_stream().wait_event(self._ev[1])
-            self._side_used = False
 
     def _sync(self):
         if self.cuda:
