@@ -30,7 +30,7 @@ import time
 
 SIZES = [1024, 4096, 4096, 1024]
 REF_MB_PER_RANK = 1792  # sw/run.sh:16: global MB 5376 / 3 ranks
-REF_STEPS = 60  # timed steps of the reference-batch measurement (extra.mb1792) at least
+REF_STEPS = 100  # timed steps of the reference-batch measurement (extra.mb1792) at least
 
 
 def parse_args(argv=None):
@@ -267,16 +267,20 @@ def main(argv=None):
         return elapsed, t_enqueue, float(loss_rows.float().mean().item()), tr, graphed
 
     mb = a.mb_per_gpu
-    elapsed, t_enqueue, loss, _, graphed = run(mb, 1234, True)
-    tr = run(mb, 1234, False, trace=True, warmup=1, tag="traced")[3] if can_trace else None
     ref = None
     if a.ref_mb and a.ref_mb != mb:
-        # a short step: a longer window on the GPU (a host hiccup is then a smaller share of it)
+        # The reference-batch measurement runs first. A short step: a longer window on the GPU (a host hiccup is then
+        # a smaller share of it). Its ~50 ms of sustained load also brings the shader clock to the level a training
+        # run holds, which a short headline window right after start-up would otherwise partly miss (same box:
+        # 5 warmup + 20 steps read 1.080-1.100 ms/step, 40 + 20 read 1.039-1.051, 5 + 200 read 1.029;
+        # profiles/r3_warmup_clock_ramp.txt). The headline still times exactly W warmup + K steps of its own batch.
         ref_steps = max(a.steps, REF_STEPS) if device.type == "cuda" else a.steps
         e2, _, _, _, _ = run(a.ref_mb, 4321, False, tag="ref", steps=ref_steps)
         ref = {"mb_per_gpu": a.ref_mb, "global_batch": a.ref_mb * world, "steps": ref_steps,
                "samples_per_s": round(a.ref_mb * world * ref_steps / e2, 2),
                "ms_per_step": round(e2 / ref_steps * 1e3, 4)}
+    elapsed, t_enqueue, loss, _, graphed = run(mb, 1234, True)
+    tr = run(mb, 1234, False, trace=True, warmup=1, tag="traced")[3] if can_trace else None
     # replicas after every step of the run: bit-identical weights on every rank (the reference reads its NIC
     # registers back to stdout after programming them, sw/mlp_mpi_example_f32.cpp:65-98; here the run proves
     # what it ran on and that the replicas agree)
