@@ -1078,17 +1078,21 @@ __global__ void __launch_bounds__(256, 1)
   }
 }
 
-// Ordered split-K reduction + epilogue (deterministic: slabs summed in split order).
-template <int EPI, typename TC, bool ACCUM>
+// Ordered split-K reduction + epilogue (deterministic: slabs summed in split order). SK > 0: the split count as a
+// compile-time constant, so every slab's load is issued before the first add (SK = 0: runtime split_k, one slab
+// per loop trip).
+template <int EPI, typename TC, bool ACCUM, int SK = 0>
 __global__ void __launch_bounds__(256)
     splitk_reduce_kernel(const float* __restrict__ ws, int split_k, TC* __restrict__ C, int64_t ldc,
                          const bf16_t* __restrict__ bias, const TC* __restrict__ aux, int64_t ldaux, int M, int N) {
   const int64_t total4 = (int64_t)M * N / 4;
+  const int sk = SK > 0 ? SK : split_k;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = i * 4;
     const int row = (int)(e / N), col = (int)(e % N);
     float4 s = reinterpret_cast<const float4*>(ws)[i];
-    for (int k = 1; k < split_k; ++k) {
+#pragma unroll
+    for (int k = 1; k < (SK > 0 ? SK : sk); ++k) {
       const float4 t = reinterpret_cast<const float4*>(ws + (int64_t)k * M * N)[i];
       s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
@@ -1101,10 +1105,11 @@ __global__ void __launch_bounds__(256)
 // encodes the group into the all-reduce wire (owner shard also in f32). With colsum, the threads past the
 // M*N/16 groups reduce the split_k bias partial sums (ws[split_k * M * N + k * N]), write colsum[] and encode the
 // bias segment of the [W | b] bucket.
-template <bool UPD>
+template <bool UPD, int SK = 0>
 __global__ void __launch_bounds__(256)
     splitk_reduce_wire_kernel(const float* __restrict__ ws, int split_k, float* __restrict__ C, int64_t ldc, int M,
                               int N, float* __restrict__ colsum, WireOut wo) {
+  if constexpr (SK > 0) split_k = SK;  // compile-time split count: the slab loads are issued together
   const int gpr = N / 16;
   const int64_t groups = (int64_t)M * gpr;
   const int64_t total = groups + (colsum ? gpr : 0);
@@ -1121,7 +1126,8 @@ __global__ void __launch_bounds__(256)
       const float4 q = *reinterpret_cast<const float4*>(p + u);
       v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
     }
-    for (int k = 1; k < split_k; ++k) {
+#pragma unroll
+    for (int k = 1; k < (SK > 0 ? SK : split_k); ++k) {
 #pragma unroll
       for (int u = 0; u < 16; u += 4) {
         const float4 q = *reinterpret_cast<const float4*>(p + k * stride + u);
@@ -1333,6 +1339,16 @@ void launch_colsum_reduce(const float* part, int parts, const GemmArgs& a, const
   hipLaunchKernelGGL((colsum_reduce_kernel<WIRE, UPD>), cdiv_i(a.N, 64), 256, 0, s, part, parts, a.colsum, a.N, wo);
 }
 
+// The split counts the planner and tuner use as compile-time constants of the slab reduce (others: runtime count).
+template <typename F>
+void with_split_count(int sk, F&& f) {
+  switch (sk) {
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    default: f(std::integral_constant<int, 0>{}); break;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
 void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_period, a.wire_codec,
@@ -1351,12 +1367,16 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     const int parts = launch_main<BM, BN, WM, WN, AK, BKC, kMainEpi, TC, ACCUM, true>(a, sk, wo, s);
     if constexpr (is_wire_epi(EPI)) {
       const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
-      hipLaunchKernelGGL(splitk_reduce_wire_kernel<EPI == kEpiWireUpd>, stream_grid(items), 256, 0, s, (const float*)a.workspace, sk,
-                         (float*)a.C, a.ldc, a.M, a.N, a.colsum, wo);
+      with_split_count(sk, [&](auto skc) {
+        hipLaunchKernelGGL((splitk_reduce_wire_kernel<EPI == kEpiWireUpd, decltype(skc)::value>), stream_grid(items),
+                           256, 0, s, (const float*)a.workspace, sk, (float*)a.C, a.ldc, a.M, a.N, a.colsum, wo);
+      });
     } else {
-      hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM>), stream_grid((size_t)a.M * a.N / 4), 256, 0, s,
-                         (const float*)a.workspace, sk, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
-                         a.ldaux, a.M, a.N);
+      with_split_count(sk, [&](auto skc) {
+        hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM, decltype(skc)::value>),
+                           stream_grid((size_t)a.M * a.N / 4), 256, 0, s, (const float*)a.workspace, sk, (TC*)a.C,
+                           a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N);
+      });
       if (a.colsum)
         launch_colsum_reduce<false>((const float*)a.workspace + (size_t)sk * a.M * a.N, parts, a, wo, s);
     }
