@@ -186,3 +186,25 @@ def test_more_deferred_requests_than_slots(N, algo):
         assert forced == R - 8
         for a, b in zip(deferred, immediate):
             assert np.array_equal(a, b)
+
+
+def test_fused_update_only_on_the_single_rank_gpu_engine(monkeypatch):
+    """The GEMM-fused update is a single-rank (inline engine), GPU, bf16, rne-codec schedule: the CPU / Python-engine
+    trainer keeps the engine's decode + SGD pass (and FAN_FUSED_UPDATE=0 turns the fused path off everywhere)."""
+    import torch
+
+    from fpga_ai_nic_amd.models.mlp import MLP
+    from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine
+    from fpga_ai_nic_amd.parallel.transport import ThreadFabric
+
+    eng = make_engine(ThreadFabric(1).transport(0), "bfp")
+    m = MLP([32, 64, 16], dtype=torch.float32, device="cpu", pad_fn=lambda n: eng.layout(n).n_pad)
+    tr = DataParallelTrainer(m, eng, lr=0.1)
+    assert not tr.fused_update and not tr.prepack
+    x = torch.randn(8, 32)
+    y = torch.randint(0, 16, (8,), dtype=torch.int32)
+    tr.step(x, y)
+    tr.finish()
+    assert tr.fused_updates == 0
+    monkeypatch.setenv("FAN_FUSED_UPDATE", "0")
+    assert not DataParallelTrainer(m, eng, lr=0.1).fused_update
