@@ -32,6 +32,7 @@ import sys
 import time
 
 import torch
+import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fpga_ai_nic_amd.parallel.dp import make_engine  # noqa: E402
@@ -127,6 +128,8 @@ def main():
                    "us": round(t * 1e6, 1), "algo_bw_GBps": round(algo_bw, 1), "bus_bw_GBps": round(bus_bw, 1),
                    "wire_bytes_per_rank": eng.wire_bytes(L), "grad_dtype": a.grad_dtype,
                    "input": "prepacked" if kw else "f32",
+                   # the torch.distributed backend: with FAN_CTRL_BACKEND=gloo the "rccl" variant is a gloo all-reduce
+                   "torch_backend": dist.get_backend() if dist.is_initialized() else None,
                    "direct_rounds": eng.counters().get("direct_rounds", 0) if hasattr(eng, "counters") else 0}
             if comm:
                 tr = sorted(comm, key=lambda x: x["comm_ms"])[len(comm) // 2]  # median round
