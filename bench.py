@@ -13,6 +13,23 @@ every process is one rank on one GPU over RCCL. Without that environment and N >
 exits with its code (the parent never initialises HIP). W untimed warmup steps, then EXACTLY K timed steps
 bracketed by barrier + torch.cuda.synchronize() on both sides; max time over ranks; rank 0 prints ONE JSON line.
 
+World > 1 (GPU): the run chooses its own schedule and checks it before timing anything (``--schedule auto``):
+* every available arm — the C++ engine's mesh over its own RCCL communicator, the direct-P2P mesh and the direct-P2P
+  ring over the link-disjoint rings, each with persistent or tile-grid GEMMs while a request is in flight, and the
+  P2P arms with their pure copies on the copy engines — passes a bit-exact all-reduce gate (one production-path
+  request vs the NumPy simulators, :mod:`fpga_ai_nic_amd.parallel.gate`) and is timed for a few steps;
+  ``extra.schedule_ab`` lists every arm (ms/step, exactness, or the error that excluded it);
+* the headline runs on the fastest exact arm; ``extra.dist.allreduce_exact`` is its gate; the process exits 3 after
+  printing its line when any arm failed the gate;
+* after the headline (bounded by ``--extra-budget`` seconds): ``extra.config4`` (256 MB all-reduce + fused SGD:
+  BFP mesh / ring, the uncompressed f32 all-reduce over the same transport and RCCL f32 + SGD kernel: algo- and
+  bus-BW; BASELINE configs 2/4) and ``extra.uncompressed`` (the same MLP step with an uncompressed all-reduce:
+  the analogue of the reference's smart-NIC vs MPI_Iallreduce comparison, sw/mlp_mpi_example_f32.cpp:615-643 vs
+  :752-787).
+World 1 also reports ``extra.forced_dist_ms_per_step`` (the multi-rank path over a 1-rank group) and
+``extra.unfused_update_ms_per_step`` (decode + SGD as a separate pass instead of inside the bwd-weight GEMM), so a
+1 -> N curve splits into compute, update pass and exposed communication.
+
 Synthetic data (random bf16 inputs, random labels) and random-init weights of the named architecture.
 Reference workload shapes: sw/run.sh:16 (global MB 5376 over 3 ranks = 1792 per rank) — reported as
 ``extra.mb1792`` next to the headline per-GPU batch.
@@ -31,6 +48,7 @@ import time
 SIZES = [1024, 4096, 4096, 1024]
 REF_MB_PER_RANK = 1792  # sw/run.sh:16: global MB 5376 / 3 ranks
 REF_STEPS = 100  # timed steps of the reference-batch measurement (extra.mb1792) at least
+CONFIG4_MB = 256  # BASELINE config 4: 256 MB synthetic gradient
 
 
 def parse_args(argv=None):
@@ -47,6 +65,9 @@ def parse_args(argv=None):
                     help="also time K steps at this per-GPU batch (extra.mb<ref>); 0 disables")
     ap.add_argument("--compress", default="bfp", choices=["bfp", "raw", "raw_bf16", "rccl", "local"])
     ap.add_argument("--rounding", default="rne", choices=["rne", "trunc"])
+    ap.add_argument("--schedule", default="auto", choices=["auto", "fixed"],
+                    help="world > 1: auto = A/B every available transport x algorithm x GEMM form in warmup and run "
+                         "the fastest exact one; fixed = exactly --transport / --algo / --rings")
     ap.add_argument("--algo", default="mesh", choices=["mesh", "ring"])
     ap.add_argument("--rings", type=int, default=1)
     ap.add_argument("--transport", default="native", choices=["torch", "native", "p2p"],
@@ -66,8 +87,14 @@ def parse_args(argv=None):
     ap.add_argument("--epi", default="producer", choices=["comm", "producer"],
                     help="side-stream engine: run each request's decode+SGD epilogue on the comm stream (overlapped "
                          "with the remaining backward) or on the compute stream after the last backward GEMM")
+    ap.add_argument("--gemm-inflight", default="persistent", choices=["persistent", "grid"],
+                    help="schedule fixed: GEMM form while a request is in flight (see DataParallelTrainer)")
+    ap.add_argument("--ab-steps", type=int, default=4, help="timed steps per arm of the schedule A/B")
     ap.add_argument("--no-trace", action="store_true",
                     help="skip the separate traced pass that measures the all-reduce phases (extra.allreduce)")
+    ap.add_argument("--extra-budget", type=float, default=240.0,
+                    help="seconds the extras after the headline may take in total (config 4, uncompressed step, the "
+                         "world-1 split); what does not fit is recorded as skipped; 0 disables them")
     ap.add_argument("--timeout", type=float, default=300.0,
                     help="watchdog budget per phase in seconds (init, warmup, timed steps, ...) and the bound of every "
                          "all-reduce wait: on expiry the engine's debug_status() goes to stderr, the communicator is "
@@ -96,16 +123,11 @@ def self_launch(a, argv) -> int | None:
     return subprocess.call(cmd, env=env)
 
 
-def _time_steps(step, steps, device, D):
-    import torch
+class Setup:
+    """One arm of the run: an engine (or None), the model it trains and its trainer."""
 
-    D.barrier()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    return t0
+    def __init__(self, name, engine, model, trainer, info):
+        self.name, self.engine, self.model, self.trainer, self.info = name, engine, model, trainer, info
 
 
 def main(argv=None):
@@ -119,12 +141,15 @@ def main(argv=None):
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from fpga_ai_nic_amd.models.mlp import MLP
+    from fpga_ai_nic_amd.parallel import gate
     from fpga_ai_nic_amd.parallel.dp import DataParallelTrainer, make_engine
     from fpga_ai_nic_amd.parallel.transport import (NativeTransport, ThreadFabric, TorchDistTransport,
-                                                    make_p2p_comm)
+                                                    try_native_transport, try_p2p_comm)
     from fpga_ai_nic_amd.utils import dist as D
+    from fpga_ai_nic_amd.utils import topology
     from fpga_ai_nic_amd.utils.watchdog import Watchdog
 
+    t_begin = time.perf_counter()
     # watchdog: every phase of the run is bounded; on expiry the engine state goes to stderr and the rank exits 124
     held = {"engine": None, "comm": None, "transport": None}
     env_rank = int(os.environ.get("RANK", "0"))
@@ -162,47 +187,82 @@ def main(argv=None):
     if device.type != "cuda":
         print("[bench] no GPU visible: running the CPU path (functional only)", file=sys.stderr)
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    comm = None
-    impl = a.engine if device.type == "cuda" else "python"
-    if world > 1 or a.force_dist:
-        transport = None
-        if a.transport == "native" and impl == "native":
-            try:  # the C++ engine's own RCCL communicator (unique id exchanged over torch.distributed)
-                transport = NativeTransport(force_collectives=a.force_dist)
-            except Exception as e:  # noqa: BLE001 - keep the run measurable on torch.distributed's communicator
-                print(f"[bench] rank {rank}: native communicator failed ({e}); using torch.distributed", file=sys.stderr)
-                a.transport = "torch"
-            if world > 1:  # every rank on the same communicator
-                ok = torch.tensor([0 if transport is None else 1], device=device)
-                torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN)
-                if int(ok.item()) == 0:
-                    transport, a.transport = None, "torch"
-        if transport is None:
-            transport = TorchDistTransport(force_collectives=a.force_dist)
-        if a.transport == "p2p" and device.type == "cuda" and impl == "native":
-            comm = make_p2p_comm()
-        if comm is None:  # report the transport the gradient plane actually uses
-            a.transport = getattr(transport, "name", a.transport)
-    else:
-        transport = ThreadFabric(1).transport(0)
-    held["transport"], held["comm"] = transport, comm
-    engine = make_engine(transport, a.compress, rounding=a.rounding, algo=a.algo, rings=a.rings,
-                         force_comm=a.force_dist, impl=impl, comm=comm, side_stream=a.side_stream,
-                         timeout_s=a.timeout + 30.0 if a.timeout > 0 else 600.0)  # the watchdog fires first
-    held["engine"] = engine
-    if hasattr(engine, "epilogue_on_producer") and not getattr(engine, "inline", True):
-        engine.epilogue_on_producer = a.epi == "producer"
-    pad_fn = (lambda n: engine.layout(n).n_pad) if engine is not None else None
-    model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
-    if world > 1:
-        for l in model.layers:
-            transport.broadcast_(l.master, 0)
-        model.sync_lp()
-    trainer = DataParallelTrainer(model, engine, lr=a.lr)
-    # device-timed communication phases of the requests (C++ engine, multi-rank path): measured in a separate
-    # traced pass, so the headline steps run with tracing off (its timing events and timed flag waits cost time)
-    can_trace = (not a.no_trace and hasattr(engine, "trace") and not getattr(engine, "inline", True))
-    stall_rank = int(os.environ.get("FAN_BENCH_STALL_RANK", "-1"))
+    cuda = device.type == "cuda"
+    impl = a.engine if cuda else "python"
+    eng_timeout = a.timeout + 30.0 if a.timeout > 0 else 600.0  # the watchdog fires first
+    multi = world > 1 or a.force_dist
+
+    def log(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    # ------------------------------------------------------------------ building blocks
+    ctrl = TorchDistTransport(force_collectives=a.force_dist) if multi else ThreadFabric(1).transport(0)
+    ctx = {"native": None, "native_err": None, "p2p": None, "p2p_err": None}
+
+    def native_transport():
+        if ctx["native"] is None and ctx["native_err"] is None:
+            if not cuda:
+                ctx["native_err"] = "no GPU"
+            else:
+                bus = D.all_gather_object(topology.own_bus_id())
+                if world > 1 and len(set(bus)) < len(bus):  # RCCL refuses two ranks on one device
+                    ctx["native_err"] = f"ranks share a GPU (bus ids {bus}): RCCL refuses duplicate devices"
+                else:
+                    ctx["native"], ctx["native_err"] = try_native_transport(force_collectives=a.force_dist)
+        return ctx["native"]
+
+    def p2p_comm():
+        if ctx["p2p"] is None and ctx["p2p_err"] is None:
+            if not (cuda and world > 1):
+                ctx["p2p_err"] = "needs world > 1 on GPU"
+            else:
+                ctx["p2p"], ctx["p2p_err"] = try_p2p_comm()
+        return ctx["p2p"]
+
+    def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
+              force=False):
+        """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
+        auto (the world-1 / CPU default)."""
+        comm = None
+        t = ctrl
+        eimpl = impl if kind != "rccl" else "python"
+        if transport == "native":
+            t = native_transport()
+            if t is None:
+                raise RuntimeError(f"RCCL communicator unavailable: {ctx['native_err']}")
+        elif transport == "p2p":
+            comm = p2p_comm()
+            if comm is None:
+                raise RuntimeError(f"P2P transport unavailable: {ctx['p2p_err']}")
+            comm.sdma = sdma
+        elif force and cuda and impl == "native":  # world-1 split: the multi-rank path over a 1-rank RCCL group
+            t = NativeTransport(force_collectives=True)
+        eng = make_engine(t, kind, rounding=a.rounding, algo=algo, rings=rings, force_comm=force or a.force_dist,
+                          impl=eimpl, comm=comm, side_stream=a.side_stream and not multi, timeout_s=eng_timeout)
+        if hasattr(eng, "epilogue_on_producer") and not getattr(eng, "inline", True):
+            eng.epilogue_on_producer = a.epi == "producer"
+        pad_fn = (lambda n: eng.layout(n).n_pad) if eng is not None else None
+        model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
+        if world > 1:
+            for l in model.layers:
+                ctrl.broadcast_(l.master, 0)
+            model.sync_lp()
+        tr = DataParallelTrainer(model, eng, lr=a.lr, gemm_inflight=gemm, fused_update=fused)
+        info = {"compress": kind, "algo": algo, "rings": getattr(eng, "rings", 0) if eng is not None else 0,
+                "transport": (getattr(t, "name", transport) if comm is None else "p2p") if multi or force else "none",
+                "gemm_inflight": tr.gemm_inflight, "copy": ("sdma" if sdma else "kernel") if comm is not None else None}
+        return Setup(name, eng, model, tr, info)
+
+    def release(setup):
+        if setup is None:
+            return
+        setup.trainer.finish()
+        setup.engine = setup.model = setup.trainer = None
+        gc.collect()
+        if cuda:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
 
     def batch(mb, seed):
         g = torch.Generator().manual_seed(seed + rank)
@@ -210,31 +270,35 @@ def main(argv=None):
         y = torch.randint(0, SIZES[-1], (mb,), generator=g, dtype=torch.int32).to(device)
         return x, y
 
-    def run(mb, seed, graph_ok, trace=False, warmup=None, tag="timed", steps=None):
-        """W warmup + K timed steps at per-GPU batch mb: (elapsed s max over ranks, host enqueue s, loss,
-        trace summary or None, graphed). The garbage collector is off inside (a collection pause in the launch loop
-        starves the GPU: one 20-step MB-1792 window once read 0.46 instead of 0.38 ms/step)."""
-        steps = a.steps if steps is None else steps
+    stall_rank = int(os.environ.get("FAN_BENCH_STALL_RANK", "-1"))
+
+    def run(setup, mb, seed, warmup, steps, tag, graph_ok=False, trace=False):
+        """W warmup + K timed steps of ``setup`` at per-GPU batch mb: (elapsed s max over ranks, host enqueue s,
+        loss, trace summary or None, graphed). The garbage collector is off inside (a collection pause in the
+        launch loop starves the GPU: one 20-step MB-1792 window once read 0.46 instead of 0.38 ms/step)."""
         gc.collect()
         gc.disable()
+        held["engine"] = setup.engine
+        if setup.info.get("copy") is not None and ctx["p2p"] is not None:  # the arm's copy path (shared comm)
+            ctx["p2p"].sdma = setup.info["copy"] == "sdma"
         try:
-            return _run(mb, seed, graph_ok, trace, warmup, tag, steps)
+            return _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace)
         finally:
             gc.enable()
 
-    def _run(mb, seed, graph_ok, trace, warmup, tag, steps):
+    def _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace):
+        trainer, model, engine = setup.trainer, setup.model, setup.engine
         x, y = batch(mb, seed)
         wd.arm(f"warmup {tag} mb={mb}")
-        if stall_rank == rank:  # test hook: this rank stops taking part (a hung peer for the watchdog test)
+        if stall_rank == rank and tag == "timed":  # test hook: this rank stops taking part (a hung peer)
             time.sleep(float(os.environ.get("FAN_BENCH_STALL_S", "600")))
-        for _ in range(a.warmup if warmup is None else warmup):
+        for _ in range(warmup):
             trainer.step(x, y)
         trainer.finish()
         wd.arm(f"{tag} mb={mb}")
         step = lambda: trainer.step(x, y)  # noqa: E731
         graphed = False
-        if graph_ok and a.graph and device.type == "cuda" and world == 1 and \
-                (engine is None or getattr(engine, "inline", False)):
+        if graph_ok and a.graph and cuda and world == 1 and (engine is None or getattr(engine, "inline", False)):
             # the whole step (fwd, loss, bwd GEMMs, BFP encode, fused SGD) is a fixed kernel sequence on one
             # stream at world 1: capture it once, replay per step (removes the host launch path entirely)
             try:
@@ -250,11 +314,16 @@ def main(argv=None):
                 torch.cuda.synchronize()
         if trace:
             engine.trace(True)
-        t0 = _time_steps(step, steps, device, D)
+        D.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
         loss_rows = model.loss_rows
         t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
         trainer.finish()
-        if device.type == "cuda":
+        if cuda:
             torch.cuda.synchronize()
         D.barrier()
         elapsed = D.max_over_ranks(time.perf_counter() - t0)
@@ -267,6 +336,80 @@ def main(argv=None):
         return elapsed, t_enqueue, float(loss_rows.float().mean().item()), tr, graphed
 
     mb = a.mb_per_gpu
+    gates_failed = []
+    schedule_ab = None
+    gate_rec = None
+    # ------------------------------------------------------------------ the schedule (world > 1: A/B + gate)
+    if world > 1 and a.schedule == "auto" and a.compress == "bfp":
+        arms = []
+        if cuda and impl == "native":
+            R = world - 1  # as many link-disjoint rings as the planner finds (7 on a fully connected 8-GPU node)
+            for gm in ("persistent", "grid"):
+                arms.append(dict(name=f"rccl_mesh_{gm}", kind="bfp", algo="mesh", transport="native", gemm=gm))
+                arms.append(dict(name=f"p2p_mesh_{gm}", kind="bfp", algo="mesh", transport="p2p", gemm=gm))
+                arms.append(dict(name=f"p2p_ring_{gm}", kind="bfp", algo="ring", rings=R, transport="p2p", gemm=gm))
+            arms.append(dict(name="p2p_mesh_sdma", kind="bfp", algo="mesh", transport="p2p", sdma=True))
+            arms.append(dict(name="p2p_ring_sdma", kind="bfp", algo="ring", rings=R, transport="p2p", sdma=True))
+        else:
+            arms.append(dict(name=f"{impl}_{a.algo}", kind="bfp", algo=a.algo, rings=a.rings, transport="torch"))
+        schedule_ab = []
+        arm_gates = {}
+        best = None
+        for spec in arms:
+            wd.arm(f"schedule A/B {spec['name']}")
+            rec = {"arm": spec["name"]}
+            setup = None
+            try:
+                setup = build(spec["name"], spec["kind"], algo=spec.get("algo", "mesh"), rings=spec.get("rings", 1),
+                              transport=spec["transport"], gemm=spec.get("gemm", "persistent"),
+                              sdma=spec.get("sdma", False))
+                rec.update(setup.info)
+                g = gate.allreduce_exactness(setup.engine, timeout_s=min(eng_timeout, 120.0))
+                rec["exact"] = g["exact"]
+                arm_gates[spec["name"]] = g
+                if not g["exact"]:
+                    gates_failed.append({"arm": spec["name"], **g})
+                    rec["gate"] = g
+                    raise RuntimeError(f"all-reduce exactness gate failed: {g}")
+                e, _, _, _, _ = run(setup, mb, 99, 2, a.ab_steps, f"ab {spec['name']}")
+                rec["ms_per_step"] = round(e / a.ab_steps * 1e3, 4)
+            except Exception as ex:  # noqa: BLE001 - a failing arm is recorded and skipped, never fatal
+                rec["error"] = str(ex)[:300]
+                log(f"arm {spec['name']} excluded: {rec['error']}")
+            schedule_ab.append(rec)
+            if "ms_per_step" in rec and (best is None or rec["ms_per_step"] < best[0]["ms_per_step"]):
+                release(best[1] if best else None)
+                best = (rec, setup)
+            else:
+                release(setup)
+        if best is None:
+            log("no arm of the schedule A/B passed: " + json.dumps(schedule_ab))
+            return 3
+        chosen_rec, main_setup = best
+        chosen_rec["chosen"] = True
+        gate_rec = dict(arm_gates[chosen_rec["arm"]], arm=chosen_rec["arm"])
+        log(f"schedule A/B: running {chosen_rec['arm']} ({chosen_rec['ms_per_step']} ms/step in the A/B)")
+    else:
+        transport = "auto"
+        if world > 1 or a.force_dist:
+            transport = {"native": "native" if impl == "native" else "torch", "p2p": "p2p", "torch": "torch"}[
+                a.transport]
+            if transport == "native" and native_transport() is None:
+                log(f"native communicator unavailable ({ctx['native_err']}); using torch.distributed")
+                transport = "torch"
+        main_setup = build("main", a.compress, algo=a.algo, rings=a.rings, transport=transport,
+                           gemm=a.gemm_inflight, force=a.force_dist and impl == "native" and transport == "auto")
+        if multi and main_setup.engine is not None:
+            gate_rec = gate.allreduce_exactness(main_setup.engine)
+            if not gate_rec["exact"]:
+                gates_failed.append({"arm": "main", **gate_rec})
+    engine, model, trainer = main_setup.engine, main_setup.model, main_setup.trainer
+    held["engine"] = engine
+    held["comm"] = ctx["p2p"] if main_setup.info.get("transport") == "p2p" else None
+    held["transport"] = ctx["native"] or ctrl
+    can_trace = (not a.no_trace and hasattr(engine, "trace") and not getattr(engine, "inline", True))
+
+    # ------------------------------------------------------------------ reference batch, headline, traced pass
     ref = None
     if a.ref_mb and a.ref_mb != mb:
         # The reference-batch measurement runs first. A short step: a longer window on the GPU (a host hiccup is then
@@ -274,24 +417,91 @@ def main(argv=None):
         # run holds, which a short headline window right after start-up would otherwise partly miss (same box:
         # 5 warmup + 20 steps read 1.080-1.100 ms/step, 40 + 20 read 1.039-1.051, 5 + 200 read 1.029;
         # profiles/r3_warmup_clock_ramp.txt). The headline still times exactly W warmup + K steps of its own batch.
-        ref_steps = max(a.steps, REF_STEPS) if device.type == "cuda" else a.steps
-        e2, _, _, _, _ = run(a.ref_mb, 4321, False, tag="ref", steps=ref_steps)
+        ref_steps = max(a.steps, REF_STEPS) if cuda else a.steps
+        e2, _, _, _, _ = run(main_setup, a.ref_mb, 4321, a.warmup, ref_steps, "ref")
         ref = {"mb_per_gpu": a.ref_mb, "global_batch": a.ref_mb * world, "steps": ref_steps,
                "samples_per_s": round(a.ref_mb * world * ref_steps / e2, 2),
                "ms_per_step": round(e2 / ref_steps * 1e3, 4)}
-    elapsed, t_enqueue, loss, _, graphed = run(mb, 1234, True)
-    tr = run(mb, 1234, False, trace=True, warmup=1, tag="traced")[3] if can_trace else None
+    elapsed, t_enqueue, loss, _, graphed = run(main_setup, mb, 1234, a.warmup, a.steps, "timed", graph_ok=True)
+    ms = elapsed / a.steps * 1e3
+    tr = run(main_setup, mb, 1234, 1, a.steps, "traced", trace=True)[3] if can_trace else None
+
+    # ------------------------------------------------------------------ extras (bounded)
+    extras = {}
+
+    def budget_left():
+        return a.extra_budget - (time.perf_counter() - t_extra0)
+
+    def extra(name, fn, need_s):
+        """Run one extra if the budget has room (rank 0's clock decides for every rank)."""
+        ok = D.all_gather_object(budget_left() >= need_s)[0]
+        if not ok:
+            extras[name] = {"skipped": f"extra budget ({a.extra_budget:.0f} s) spent"}
+            return
+        wd.arm(f"extra {name}")
+        try:
+            extras[name] = fn()
+        except Exception as ex:  # noqa: BLE001 - an extra never costs the headline its record
+            extras[name] = {"error": str(ex)[:300]}
+            log(f"extra {name} failed: {ex}")
+
+    t_extra0 = time.perf_counter()
+    if a.extra_budget > 0:
+        if world == 1 and not a.force_dist and engine is not None:
+            def split(fused, force):
+                s = build("split", a.compress, transport="auto", fused=fused, force=force)
+                try:
+                    e, _, _, _, _ = run(s, mb, 1234, 3, a.steps, "split")
+                    return round(e / a.steps * 1e3, 4)
+                finally:
+                    release(s)
+
+            def forced():
+                if not (torch.distributed.is_initialized()):
+                    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                    os.environ["MASTER_PORT"] = str(_free_port())
+                    D.init_distributed(force=True)
+                return split(None, True)
+
+            extra("unfused_update_ms_per_step", lambda: split(False, False), 10)
+            extra("forced_dist_ms_per_step", forced, 20)
+        if world > 1:
+            extra("config4", lambda: _config4(a, world, rank, device, ctx, native_transport, p2p_comm, make_engine,
+                                              ctrl, eng_timeout), 30)
+
+            def uncompressed():
+                out = {}
+                arms_u = ((("p2p_raw_f32_mesh", "raw", "p2p"), ("rccl_f32", "rccl", "native")) if cuda and
+                          impl == "native" else (("torch_f32", "rccl", "torch"),))  # CPU: gloo's all-reduce
+                for name, kind, tp in arms_u:
+                    s = None
+                    try:
+                        s = build(name, kind, transport=tp)
+                        e, _, _, _, _ = run(s, mb, 1234, 2, a.steps, f"uncompressed {name}")
+                        out[name] = {"ms_per_step": round(e / a.steps * 1e3, 4), **s.info}
+                    except Exception as ex:  # noqa: BLE001
+                        out[name] = {"skipped": str(ex)[:300]}
+                    finally:
+                        release(s)
+                done = [v["ms_per_step"] for v in out.values() if "ms_per_step" in v]
+                out["compressed_ms_per_step"] = round(ms, 4)
+                out["speedup_vs_best_uncompressed"] = round(min(done) / ms, 4) if done else None
+                return out
+
+            extra("uncompressed", uncompressed, 15)
+    extras_s = time.perf_counter() - t_extra0
+
     # replicas after every step of the run: bit-identical weights on every rank (the reference reads its NIC
     # registers back to stdout after programming them, sw/mlp_mpi_example_f32.cpp:65-98; here the run proves
     # what it ran on and that the replicas agree)
     wd.arm("verify")
-    dist_rec = _dist_report(a, engine, model, world, rank, device, D)
+    dist_rec = _dist_report(main_setup, world, rank, device, D, gate_rec)
     wd.disarm()
 
-    ms = elapsed / a.steps * 1e3
     global_batch = mb * world
     value = global_batch * a.steps / elapsed
     flops = model.flops_per_sample() * global_batch * a.steps / elapsed
+    info = main_setup.info
     if rank == 0:
         rec = {
             "metric": "MLP training samples/sec (1024-4096-4096-1024, BFP all-reduce + fused SGD)",
@@ -312,12 +522,15 @@ def main(argv=None):
                 "seq_len": None,
                 "parallelism": f"dp{world}",
                 "mb_per_gpu": mb,
-                "compress": a.compress,
+                "compress": info["compress"],
                 "rounding": a.rounding,
-                "algo": a.algo,
-                "rings": engine.rings if engine is not None else 0,
-                "transport": a.transport if (world > 1 or a.force_dist) else "none",
+                "algo": info["algo"],
+                "rings": info["rings"],
+                "transport": info["transport"],
                 "engine": impl,
+                "schedule": main_setup.name if schedule_ab is not None else "fixed",
+                "gemm_inflight": info["gemm_inflight"],
+                "p2p_copy": info["copy"],
                 "hip_graph": graphed,
                 "fused_sgd": True,
                 # world 1: dW's BFP round trip + SGD inside the bwd-weight GEMM epilogue (no separate update pass)
@@ -332,7 +545,11 @@ def main(argv=None):
                 "allreduce": _allreduce_report(tr, world),
                 f"mb{a.ref_mb}": ref,
                 "final_loss": round(loss, 5),
+                "schedule_ab": schedule_ab,
                 "dist": dist_rec,
+                **extras,
+                "extras_s": round(extras_s, 2),
+                "run_s": round(time.perf_counter() - t_begin, 2),
                 "gemm_tuning": _tuning_report(),
                 **({"engine_counters": engine.counters()} if hasattr(engine, "counters") else {}),
             },
@@ -344,7 +561,88 @@ def main(argv=None):
     if not dist_rec["replicas_identical"]:
         print(f"[bench] rank {rank}: replicas DIVERGED: {dist_rec['replica_digests']}", file=sys.stderr, flush=True)
         return 2
+    if gates_failed:
+        print(f"[bench] rank {rank}: all-reduce exactness gate FAILED: {json.dumps(gates_failed)}", file=sys.stderr,
+              flush=True)
+        return 3
     return 0
+
+
+def _config4(a, world, rank, device, ctx, native_transport, p2p_comm, make_engine, ctrl, timeout_s):
+    """BASELINE config 4 (and the config-2 uncompressed baseline): a 256 MB f32 gradient, all-reduce + fused SGD
+    per request, over the transports this run has. BFP variants start from the producer's encoding (prepacked, as
+    in training); ``rccl_f32`` is RCCL's ncclAllReduce + a separate SGD kernel (the reference's commented
+    MPI_Iallreduce + host SGD path, sw/mlp_mpi_example_f32.cpp:615-647). Per variant: median per-request time over
+    the slowest rank, algo-BW = logical bytes / time, bus-BW = algo x 2(N-1)/N."""
+    import statistics
+
+    import torch
+
+    from fpga_ai_nic_amd import _ext
+    from fpga_ai_nic_amd.utils import dist as D
+
+    if device.type != "cuda":
+        return {"skipped": "CPU run"}
+    n = CONFIG4_MB * (1 << 20) // 4
+    variants = []
+    p2p = p2p_comm()
+    nat = native_transport()
+    if p2p is not None:
+        variants += [("bfp_mesh_p2p", "bfp", "mesh", 1, None, p2p), ("bfp_ring_p2p", "bfp", "ring", world - 1, None, p2p),
+                     ("raw_f32_mesh_p2p", "raw", "mesh", 1, None, p2p)]
+    if nat is not None:
+        variants += [("bfp_mesh_rccl", "bfp", "mesh", 1, nat, None), ("rccl_f32", "rccl", "mesh", 1, nat, None)]
+    out = {"size_MB_f32": CONFIG4_MB, "n_gpus": world}
+    if p2p is None:
+        out["p2p"] = {"skipped": ctx["p2p_err"]}
+    if nat is None:
+        out["rccl_f32"] = {"skipped": ctx["native_err"]}
+    for name, kind, algo, rings, t, comm in variants:
+        eng = None
+        try:
+            if comm is not None:
+                comm.sdma = False
+            eng = make_engine(t if t is not None else ctrl, kind, rounding=a.rounding, algo=algo, rings=rings,
+                              impl="python" if kind == "rccl" else "native", comm=comm, timeout_s=timeout_s)
+            L = eng.layout(n)
+            g = torch.randn(L.n_pad, device=device) * 1e-3
+            w = torch.randn(L.n_pad, device=device)
+            lp = w.to(torch.bfloat16)
+            kw = {}
+            if kind == "bfp" and getattr(eng, "prepack", False):
+                tgt = eng.prepack_target(g, n)
+                if tgt is not None:
+                    _ext.require().wire_pack_range(g, tgt[0], tgt[1], 0, n, tgt[3])
+                    kw["prepacked"] = (tgt[0], L.n_pad)
+
+            def once():
+                return eng.allreduce_sgd(g, w, lp, n_valid=n, lr=1e-6, grad_scale=1.0 / world, **kw)
+
+            for _ in range(2):
+                once().synchronize(timeout_s)
+            times = []
+            for _ in range(3):
+                D.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                hs = [once() for _ in range(3)]
+                for h in hs:
+                    h.synchronize(timeout_s)
+                torch.cuda.synchronize()
+                times.append(D.max_over_ranks(time.perf_counter() - t0) / 3)
+            t = statistics.median(times)
+            algo_bw = n * 4 / t / 1e9
+            out[name] = {"us": round(t * 1e6, 1), "algo_bw_GBps": round(algo_bw, 2),
+                         "bus_bw_GBps": round(algo_bw * 2 * (world - 1) / world, 2),
+                         "wire_bytes_per_rank": int(eng.wire_bytes(L)), "rings": int(getattr(eng, "rings", 1)),
+                         "input": "prepacked" if kw else "f32"}
+        except Exception as ex:  # noqa: BLE001
+            out[name] = {"error": str(ex)[:300]}
+        finally:
+            del eng
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    return out
 
 
 def _tuning_report():
@@ -369,12 +667,14 @@ def replica_digest(tensors):
     return out
 
 
-def _dist_report(a, engine, model, world, rank, device, D):
+def _dist_report(setup, world, rank, device, D, gate_rec):
     """extra.dist: what the run actually ran on — torch's and the engine communicator's rank counts (RCCL:
     ncclCommCount), the transport, the ring orders and link matrix the planner used, the devices (PCI bus ids) of
-    the ranks — and whether the replicas' weights are bit-identical after the run (all-gathered digests)."""
+    the ranks — whether the production all-reduce path passed the bit-exact gate, and whether the replicas' weights
+    are bit-identical after the run (all-gathered digests)."""
     from fpga_ai_nic_amd.utils import topology
 
+    engine, model = setup.engine, setup.model
     C = getattr(engine, "C", None)
     mine = {
         "digest": replica_digest([l.master for l in model.layers]),
@@ -387,13 +687,15 @@ def _dist_report(a, engine, model, world, rank, device, D):
     return {
         "world": world,
         "torch_backend": D.backend(),
-        "transport": a.transport if world > 1 or a.force_dist else "none",
+        "transport": setup.info["transport"],
         "engine_comm": (C.comm_kind if C is not None else ("python" if engine is not None else "none")),
         "comm_ranks": [e["comm_ranks"] for e in every],
         "algo": getattr(engine, "algo", None),
         "ring_orders": getattr(engine, "orders", None) if getattr(engine, "algo", None) == "ring" else None,
         "links": getattr(engine, "links", None),
         "bus_ids": [e["bus_id"] for e in every],
+        "allreduce_exact": gate_rec["exact"] if gate_rec is not None else None,
+        "allreduce_gate": gate_rec,
         "replicas_identical": ident,
         "replica_digests": digests if not ident else digests[0],
     }
@@ -403,12 +705,13 @@ def _allreduce_report(tr, world):
     """All-reduce algo-BW of the requests of the traced pass (the same K steps again, with per-request device
     timestamps): logical (f32 gradient) bytes / summed device time of their communication phases (request start on
     the comm stream -> end of the all-gather, slowest rank); bus-BW = algo-BW x 2(N-1)/N; wire-BW = bytes this rank
-    actually sent (BFP-packed) / the same time. None when no collective ran (world 1 inline engine: no wire)."""
+    actually sent (BFP-packed) / the same time. Ring schedules add the per-hop split (credit wait, hop kernels,
+    upstream ready wait, longest round). None when no collective ran (world 1 inline engine: no wire)."""
     if not tr or not tr.get("requests") or tr.get("comm_ms", 0) <= 0:
         return None
     s = tr["comm_ms"] / 1e3
     algo = tr["logical_bytes"] / s / 1e9
-    return {
+    rec = {
         "traced_ms_per_step": round(tr["ms_per_step"], 4),
         "requests": tr["requests"],
         "comm_ms_total": round(tr["comm_ms"], 4),
@@ -418,6 +721,14 @@ def _allreduce_report(tr, world):
         "phase_ms": {k: round(tr[k], 4) for k in ("pack_ms", "exchange_ms", "reduce_ms", "gather_ms", "epilogue_ms")},
         "dropped": tr.get("dropped", 0),
     }
+    if tr.get("hop_rounds"):
+        n = tr["hop_rounds"]
+        rec["ring_hops"] = {"rounds": n, "credit_ms": round(tr["hop_credit_ms"], 4),
+                            "kernel_ms": round(tr["hop_kernel_ms"], 4), "ready_ms": round(tr["hop_ready_ms"], 4),
+                            "mean_round_us": round((tr["hop_credit_ms"] + tr["hop_kernel_ms"] + tr["hop_ready_ms"])
+                                                   / n * 1e3, 2),
+                            "max_round_us": round(tr["hop_max_ms"] * 1e3, 2)}
+    return rec
 
 
 if __name__ == "__main__":

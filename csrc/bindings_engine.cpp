@@ -47,6 +47,10 @@ void register_engine(pybind11::module_& m) {
            })
       .def_static("connect_local", &P2PComm::connect_local)
       .def_property_readonly("slot_bytes", &P2PComm::slot_bytes)
+      .def_property_readonly("payload_bytes", &P2PComm::payload_bytes, "slot bytes messages may use (slot - trailer)")
+      .def_property("sdma", &P2PComm::sdma, &P2PComm::set_sdma,
+                    "pure copies (prepacked sends, forwards, arena -> scratch) on the copy engines instead of a CU kernel")
+      .def_property_readonly("cross_device", &P2PComm::cross_device, "some peer's arena is on another GPU")
       .def_property_readonly("sequence", &P2PComm::sequence)
       .def_property_readonly("uncached", &P2PComm::uncached)
       .def_property_readonly("arena_memory", &P2PComm::arena_memory)
@@ -281,6 +285,11 @@ void register_engine(pybind11::module_& m) {
             d["epilogue_ms"] = t.ms[kTpEpiEnd];
             d["comm_ms"] = t.comm_ms;
             d["total_ms"] = t.total_ms;
+            d["hop_rounds"] = t.hop_rounds;
+            d["hop_credit_ms"] = t.hop_credit_ms;
+            d["hop_kernel_ms"] = t.hop_kernel_ms;
+            d["hop_ready_ms"] = t.hop_ready_ms;
+            d["hop_max_ms"] = t.hop_max_ms;
             return d;
           },
           "per-phase device time summed over the traced requests (pack / all-to-all / reduce / all-gather / "

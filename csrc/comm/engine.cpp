@@ -114,6 +114,7 @@ AllReduceEngine::~AllReduceEngine() {
   }
   for (auto& t : trace_pool_)
     for (auto& e : t.ev) hipEventDestroy(e);
+  for (auto& e : hop_pool_) hipEventDestroy(e);
   for (auto& kv : scratch_) hipFree(kv.second.first);
   for (auto& kv : gall_)
     if (kv.second.free) hipEventDestroy(kv.second.free);
@@ -136,7 +137,7 @@ EngineLayout AllReduceEngine::layout(int64_t n, int64_t shard, int64_t chunks) c
     FAN_CHECK(shard > 0 && shard % 256 == 0 && chunks >= 1, "explicit layout: shard % 256 == 0 and chunks >= 1");
     FAN_CHECK(shard * N * chunks >= n, "explicit layout smaller than the bucket");
     if (P2PComm* d = comm_ ? comm_->direct() : nullptr)
-      FAN_CHECK(wire_shard_bytes(cfg_.codec, (size_t)shard) <= d->slot_bytes(), "explicit shard exceeds the p2p slot");
+      FAN_CHECK(wire_shard_bytes(cfg_.codec, (size_t)shard) <= d->payload_bytes(), "explicit shard exceeds the p2p slot");
     L.shard = shard;
     L.chunks = chunks;
     L.n_pad = shard * N * chunks;
@@ -149,7 +150,7 @@ EngineLayout AllReduceEngine::layout(int64_t n, int64_t shard, int64_t chunks) c
     int64_t chunk = cfg_.chunk_elems;
     if (P2PComm* d = comm_ ? comm_->direct() : nullptr) {
       // a P2P message (one wire shard) must fit one arena slot: chunk the bucket so that it does
-      const int64_t max_shard = (int64_t)(d->slot_bytes() / wire_shard_bytes(cfg_.codec, 256)) * 256;
+      const int64_t max_shard = (int64_t)(d->payload_bytes() / wire_shard_bytes(cfg_.codec, 256)) * 256;
       FAN_CHECK(max_shard >= 256, "p2p arena slot smaller than one 256-element wire shard");
       chunk = std::min<int64_t>(chunk, max_shard * N);
     }
@@ -246,7 +247,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
   }
   if (L.chunks > 1)
     return run_mesh_chunked(L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked, cur_defer_);
-  if (P2PComm* d = comm_->direct(); d && N <= kMaxPeers && !verify_ && !fault_.active())
+  if (P2PComm* d = comm_->direct(); d && N <= kMaxPeers)
     return run_mesh_direct(d, L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked, cur_defer_);
   uint8_t* S = scratch("mesh_S" + std::to_string(sb), sb);
   const uint8_t* P = prepacked ? prepacked : g;
@@ -267,7 +268,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     count_peers(sb);
     if (verify_) {
       comm_->all_to_all(tag_region(0), tag_region(1), 16, st);
-      verify_rows(R, sb, N, tag_region(1), 1, 0, st);
+      verify_rows(R, sb, N, tag_region(1), kSiteMeshAllToAll, 0, st);
     }
   }
   mark(kTpExchanged);
@@ -285,7 +286,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     count_peers(sb);
     if (verify_) {
       comm_->all_gather(tag_region(3), tag_region(4), 16, st);
-      verify_rows(G, sb, N, tag_region(4), 2, 0, st);
+      verify_rows(G, sb, N, tag_region(4), kSiteMeshAllGather, 0, st);
     }
   }
   const int64_t n_pad = L.n_pad;
@@ -301,8 +302,9 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
 //   round 2: ready flags; an immediate request decodes + applies SGD reading the gathered shards in place, then
 //            acknowledges; a deferred one (epilogue at commit, after the producer's remaining GEMMs) first moves
 //            them into per-slot scratch, since the slots are reused two rounds later.
-// No staging buffer and no copy kernel on either side of a link (verify mode / fault injection use the copying
-// path). Memory ordering: p2p_comm.h.
+// No staging buffer and no copy kernel on either side of a link. Verify mode tags every message where it landed
+// (the slot trailer, P2PComm::dst_tag) and checks it on the consumer side after the ready flag, before the kernel
+// that reads it (sites "mesh direct send" / "mesh direct gather", row = sender rank). Memory ordering: p2p_comm.h.
 std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineLayout& L, const void* grad, int gdt,
                                                        float* master, bf16_t* lp, float* mom, int64_t n_valid,
                                                        SgdParams p, bool update, float* out_sum,
@@ -310,10 +312,29 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
   const int N = world_, r = rank_, c = cfg_.codec;
   const int64_t s = L.shard;
   const size_t sb = wire_shard_bytes(c, s);
-  FAN_CHECK(sb <= d->slot_bytes(), "p2p: shard larger than the arena slot (raise slot_bytes)");
+  FAN_CHECK(sb <= d->payload_bytes(), "p2p: shard larger than the arena slot (raise slot_bytes)");
   const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
   hipStream_t st = run_stream_;
   const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
+  // verify / fault hooks of one direct round: tag what this rank stored into each peer's slot (trailer tag 0), and
+  // the receiver's check of every peer's message once its flag is up
+  auto tag_sent = [&](const P2PComm::Round& rd, const char* fault_site) {
+    bool first = true;
+    for (int q = 0; q < N; ++q) {
+      if (q == r) continue;
+      if (verify_) tag_direct(d->dst(rd, q), sb, d->dst_tag(rd, q, 0), (uint32_t)rd.seq, st);
+      if (first) fault_.maybe_corrupt(fault_site, d->dst(rd, q), sb, st);  // in flight: after its tag
+      first = false;
+    }
+  };
+  auto check_received = [&](const P2PComm::Round& rd, uint32_t site) {
+    for (int q = 0; q < N; ++q) {
+      if (q == r) continue;
+      uint8_t* m = const_cast<uint8_t*>(d->src(rd, q));
+      fault_.maybe_corrupt("p2p_recv", m, sb, st);  // test hook: the slot changes after its flag was raised
+      if (verify_) verify_direct(m, sb, d->src_tag(rd, q, 0), (uint32_t)rd.seq, site, (uint32_t)q, st);
+    }
+  };
   P2PComm::Round r1 = d->begin(st);
   {
     RoctxRange rr("fan/mesh/direct_send");
@@ -325,13 +346,15 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
       if (prepacked) segs.push_back({prepacked + (size_t)q * sb, to.p[q], sb});
       else if (zero_copy) segs.push_back({g + (size_t)q * s * esize(gdt), to.p[q], sb});
     }
-    if (prepacked || zero_copy) launch_multi_copy(segs, st);
+    if (prepacked || zero_copy) d->move(segs, st);
     else launch_wire_pack_to(c, gdt, g, to, (size_t)s, N, st);
+    tag_sent(r1, "mesh_pack");
   }
   mark(kTpPacked);
   d->publish(r1, st);
   count_peers(sb, d);
   d->wait(r1, st);
+  check_received(r1, kSiteMeshDirectSend);
   mark(kTpExchanged);
   P2PComm::Round r2 = d->begin(st);
   {
@@ -341,11 +364,13 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
     launch_wire_reduce_to(c, gdt, d->src_base(r1), d->src_stride(), N, r, g + (size_t)r * s * esize(gdt), out, N,
                           (size_t)s, st);
     d->release(r1, st);
+    tag_sent(r2, "mesh_reduce");
   }
   mark(kTpReduced);
   d->publish(r2, st);
   count_peers(sb, d);
   d->wait(r2, st);
+  check_received(r2, kSiteMeshDirectGather);
   counters_.direct_rounds += 2;
   const uint8_t* Gv = d->src_base(r2);
   const size_t gstride = d->src_stride();
@@ -354,7 +379,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
     uint8_t* G = epi_scratch("mesh_G" + std::to_string(sb * N), sb * N);
     std::vector<P2PCopy> segs;
     for (int q = 0; q < N; ++q) segs.push_back({Gv + (size_t)q * gstride, G + (size_t)q * sb, sb});
-    launch_multi_copy(segs, st);
+    d->move(segs, st);
     d->release(r2, st);
     return {[=](hipStream_t es) { epilogue(c, es, G, s, N, 0, n_pad, master, lp, mom, n_valid, p, update, out_sum); }};
   }
@@ -432,7 +457,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
     count_peers(sb);
     if (verify_) {
       comm_->all_gather(tag_region(3), tag_region(4), 16, A);
-      verify_rows(gath(ch), sb, N, tag_region(4), 2, (uint32_t)(ch * N), A);
+      verify_rows(gath(ch), sb, N, tag_region(4), kSiteMeshAllGather, (uint32_t)(ch * N), A);
     }
     if (!defer) {  // per-chunk epilogue on the aux stream
       FAN_HIP_CHECK(hipEventRecord(cev_[2][ch % 2], A));
@@ -461,7 +486,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_chunked(const EngineLayout& L, c
       count_peers(sb);
       if (verify_) {
         comm_->all_to_all(tag_region(0), tag_region(1), 16, A);
-        verify_rows(R[ch % 2], sb, N, tag_region(1), 1, (uint32_t)(ch * N), A);
+        verify_rows(R[ch % 2], sb, N, tag_region(1), kSiteMeshAllToAll, (uint32_t)(ch * N), A);
       }
       FAN_HIP_CHECK(hipEventRecord(cev_[0][ch % 2], A));
     }
@@ -501,7 +526,7 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
   if (prepacked)  // encode what the producer did not (bias gradient + padding): slice-sized shards, ring-major
     launch_wire_pack_range(c, gdt, grad, const_cast<uint8_t*>(prepacked), (size_t)S, (size_t)prepacked_elems,
                            (size_t)L.n_pad, st);
-  if (P2PComm* d = comm_ ? comm_->direct() : nullptr; d && N > 1 && !compat && !verify_ && !fault_.active())
+  if (P2PComm* d = comm_ ? comm_->direct() : nullptr; d && N > 1 && !compat)
     return run_ring_direct(d, L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked);
   struct RingState {
     int64_t off;
@@ -543,6 +568,10 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
   uint32_t round_id = 0;
   for (const auto& rnd : rounds) {
     RoctxRange rr("fan/ring/round");
+    if (N > 1) {  // no credit phase on a copying transport: points 0 and 1 coincide
+      hop_mark(0);
+      hop_mark(1);
+    }
     std::vector<P2POp> sends, recvs;
     for (size_t j : rnd) {
       for (auto& rs : rings) {
@@ -592,10 +621,12 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
       for (size_t q = 0; q < nd; ++q) fault_.maybe_corrupt("ring_send", static_cast<uint8_t*>(sends[q].ptr), sb, st);
       if (counters_.peer_bytes.size() != (size_t)world_) counters_.peer_bytes.assign(world_, 0);
       for (const P2POp& op : sends) counters_.peer_bytes[op.peer] += (int64_t)op.bytes;
+      hop_mark(2);
       comm_->sendrecv(sends, recvs, st);
+      hop_mark(3);
       if (verify_)
         for (size_t q = 0; q < nr; ++q)
-          verify_rows(static_cast<const uint8_t*>(recvs[q].ptr), sb, 1, tag_region(1) + q * 4, 3,
+          verify_rows(static_cast<const uint8_t*>(recvs[q].ptr), sb, 1, tag_region(1) + q * 4, kSiteRingRound,
                       round_id * kTagRows + (uint32_t)q, st);
     }
     ++round_id;
@@ -630,9 +661,14 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
 // BFP TX framing and onto the link, hw/all_reduce.sv:1155-1166, hw/bfp_adapter.sv:279-379); SEND_LOCAL encodes
 // (or, for a producer-encoded bucket, copies) the local slice straight into that slot; a FORWARD hop copies the
 // received full slice arena -> downstream arena, and every received full slice is copied once into the gathered
-// wire the epilogue reads. Per round: credit waits for the downstream slots (P2PComm::begin_to), the kernels, ack
-// of the previous round's upstream slots, ready flags downstream, wait for upstream's. The schedule, sums and
-// summation order are those of run_ring's copying rounds (bit-identical; verify / fault / compat modes use that).
+// wire the epilogue reads (pure copies: P2PComm::move, CU kernel or copy engines). Per round: credit waits for the
+// downstream slots (P2PComm::begin_to), the kernels, ack of the previous round's upstream slots, ready flags
+// downstream, wait for upstream's. The schedule, sums and summation order are those of run_ring's copying rounds
+// (bit-identical; the compat owner-f32 mode uses that path). Verify mode tags message k of a round in the slot
+// trailer (tag k) after the round's kernels and checks every received message after the ready wait (site "ring
+// direct hop", row = round). Traced requests record four device timestamps per round (hop_mark): round start,
+// credits granted, kernels done, upstream data ready — the per-hop split of the NIC's stall_eth_in/out counters
+// (hw/all_reduce.sv:892-1085).
 std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineLayout& L, const void* grad, int gdt,
                                                        float* master, bf16_t* lp, float* mom, int64_t n_valid,
                                                        SgdParams p, bool update, float* out_sum,
@@ -641,7 +677,7 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
   const int64_t S = L.slice;
   const size_t sb = wire_shard_bytes(c, S);
   const size_t msg = (sb + 255) / 256 * 256;  // message stride inside an arena slot (<= 2 messages per peer/round)
-  FAN_CHECK(2 * msg <= d->slot_bytes(), "p2p ring: two slices per round must fit an arena slot (lower max_slice_elems)");
+  FAN_CHECK(2 * msg <= d->payload_bytes(), "p2p ring: two slices per round must fit an arena slot (lower max_slice_elems)");
   const int64_t nsl = L.blocks * N;
   const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
   hipStream_t st = run_stream_;
@@ -685,10 +721,18 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
   P2PComm::Round prev_round{0};
   bool have_prev = false;
   if (counters_.peer_bytes.size() != (size_t)world_) counters_.peer_bytes.assign(world_, 0);
+  uint32_t round_id = 0;
   for (const auto& rnd : rounds) {
     RoctxRange rr_("fan/ring/direct_round");
+    hop_mark(0);
     const P2PComm::Round rr = d->begin_to(downs, st);
+    hop_mark(1);
     std::vector<P2PCopy> copies;  // forwards (arena -> downstream arena) and received full slices -> G
+    struct Sent {
+      uint8_t* msg;
+      uint8_t* tag;
+    };
+    std::vector<Sent> sent;  // this round's messages, tagged after all of the round's kernels / copies
     for (size_t i = 0; i < rings.size(); ++i) {
       RS& rs = rings[i];
       size_t kmsg = 0;
@@ -696,6 +740,7 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
         const RingRound& row = rs.plan[j];
         if (row.send_src == kSendNone) continue;
         uint8_t* to = d->dst(rr, rs.down) + kmsg * msg;
+        sent.push_back({to, d->dst_tag(rr, rs.down, (int)kmsg)});
         ++kmsg;
         counters_.peer_bytes[rs.down] += (int64_t)sb;
         d->count_sent(rs.down, sb);
@@ -728,29 +773,40 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
       for (const Rx& x : prev[i])  // every received full slice lands once in the gathered wire
         if (x.full) copies.push_back({x.ptr, rs.G + (size_t)x.slice * sb, sb});
     }
-    if (!copies.empty()) launch_multi_copy(copies, st);
+    if (!copies.empty()) d->move(copies, st);
+    for (const Sent& m : sent) {
+      if (verify_) tag_direct(m.msg, sb, m.tag, (uint32_t)rr.seq, st);
+      fault_.maybe_corrupt("ring_send", m.msg, sb, st);  // in flight: after its tag
+    }
+    hop_mark(2);
     if (have_prev) d->release_from(prev_round, ups, st);  // the previous round's upstream slots are consumed
     d->publish_to(rr, downs, st);
     d->wait_from(rr, ups, st);
+    hop_mark(3);
     for (size_t i = 0; i < rings.size(); ++i) {
       prev[i].clear();
       size_t kmsg = 0;
       for (size_t j : rnd) {
         const RingRound& row = rings[i].plan[j];
         if (row.recv_slice < 0) continue;
-        prev[i].push_back({row.recv_slice, row.recv_full != 0, d->src(rr, rings[i].up) + kmsg * msg});
+        uint8_t* m = const_cast<uint8_t*>(d->src(rr, rings[i].up)) + kmsg * msg;
+        fault_.maybe_corrupt("p2p_recv", m, sb, st);  // test hook: the slot changes after its flag was raised
+        if (verify_)
+          verify_direct(m, sb, d->src_tag(rr, rings[i].up, (int)kmsg), (uint32_t)rr.seq, kSiteRingDirect, round_id, st);
+        prev[i].push_back({row.recv_slice, row.recv_full != 0, m});
         ++kmsg;
       }
     }
     prev_round = rr;
     have_prev = true;
     counters_.direct_rounds++;
+    ++round_id;
   }
   std::vector<P2PCopy> tail;
   for (size_t i = 0; i < rings.size(); ++i)
     for (const Rx& x : prev[i])
       if (x.full) tail.push_back({x.ptr, rings[i].G + (size_t)x.slice * sb, sb});
-  if (!tail.empty()) launch_multi_copy(tail, st);
+  if (!tail.empty()) d->move(tail, st);
   if (have_prev) d->release_from(prev_round, ups, st);
   std::vector<EpiThunk> thunks;
   for (auto& rs : rings) {
@@ -759,6 +815,33 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
     thunks.push_back([=](hipStream_t es) { epilogue(c, es, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum); });
   }
   return thunks;
+}
+
+void AllReduceEngine::tag_direct(const uint8_t* msg, size_t bytes, uint8_t* trailer, uint32_t seq, hipStream_t st) {
+  uint32_t* t = tag_region(0);  // one local row: the tag kernels and this copy are stream-ordered
+  launch_msg_tags(msg, bytes, bytes, 1, seq, t, st);
+  launch_multi_copy({{t, trailer, 16}}, st);
+}
+
+void AllReduceEngine::verify_direct(const uint8_t* msg, size_t bytes, const uint8_t* trailer, uint32_t seq,
+                                    uint32_t site, uint32_t row, hipStream_t st) {
+  launch_msg_verify(msg, bytes, bytes, 1, reinterpret_cast<const uint32_t*>(trailer), seq, tag_region(2), verr_dev_,
+                    site, row, st);
+  counters_.verified_rows++;
+}
+
+void AllReduceEngine::hop_mark(int point) {
+  if (cur_trace_ < 0) return;
+  if (hop_used_ == hop_pool_.size()) {
+    hipEvent_t e;
+    FAN_HIP_CHECK(hipEventCreate(&e));
+    hop_pool_.push_back(e);
+  }
+  RequestTrace& t = trace_pool_[cur_trace_];
+  if (t.hop_count == 0) t.hop_first = hop_used_;
+  FAN_HIP_CHECK(hipEventRecord(hop_pool_[hop_used_++], run_stream_));
+  t.hop_count++;
+  (void)point;
 }
 
 int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
@@ -790,6 +873,7 @@ int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf1
   if (tracing_) {
     if (trace_used_ < trace_pool_.size()) {
       x.trace = cur_trace_ = (int)trace_used_++;
+      trace_pool_[cur_trace_].hop_count = 0;
       trace_pool_[cur_trace_].logical_bytes = n_valid * 4;
       trace_pool_[cur_trace_].wire_bytes = wb;
       mark(kTpStart);
@@ -839,6 +923,7 @@ void AllReduceEngine::set_tracing(bool on, int capacity) {
   if (!on) return;
   // a new trace window: wait for the previous window's requests before their events are re-recorded
   for (size_t i = 0; i < trace_used_; ++i) hipEventSynchronize(trace_pool_[i].ev[kTpEpiEnd]);
+  hop_used_ = 0;
   while ((int)trace_pool_.size() < capacity) {
     RequestTrace t;
     for (auto& e : t.ev) FAN_HIP_CHECK(hipEventCreate(&e));
@@ -869,6 +954,18 @@ TraceSummary AllReduceEngine::trace_summary() {
     r.requests++;
     r.logical_bytes += t.logical_bytes;
     r.wire_bytes += t.wire_bytes;
+    for (size_t h = 0; h + 3 < t.hop_count; h += 4) {
+      const hipEvent_t* e = &hop_pool_[t.hop_first + h];
+      float a = 0.f, b = 0.f, c = 0.f;
+      FAN_HIP_CHECK(hipEventElapsedTime(&a, e[0], e[1]));
+      FAN_HIP_CHECK(hipEventElapsedTime(&b, e[1], e[2]));
+      FAN_HIP_CHECK(hipEventElapsedTime(&c, e[2], e[3]));
+      r.hop_rounds++;
+      r.hop_credit_ms += a;
+      r.hop_kernel_ms += b;
+      r.hop_ready_ms += c;
+      r.hop_max_ms = std::max<double>(r.hop_max_ms, (double)a + b + c);
+    }
   }
   return r;
 }
@@ -981,11 +1078,12 @@ void AllReduceEngine::verify_rows(const uint8_t* rows, size_t row_bytes, int nro
 
 void AllReduceEngine::check_verify() {
   if (!verify_ || verr_host_->flag == 0) return;
-  static const char* sites[] = {"?", "mesh all_to_all", "mesh all_gather", "ring round"};
+  static const char* sites[] = {"?", "mesh all_to_all", "mesh all_gather", "ring round", "mesh direct send",
+                                "mesh direct gather", "ring direct hop"};
   const VerifyError e = *verr_host_;
   std::ostringstream os;
   os << "verify: message " << (e.kind == 1 ? "corrupted" : "out of sequence (dropped or reordered)") << " in "
-     << sites[e.site < 4 ? e.site : 0] << " row " << e.row << " (checksum " << e.got_s1 << " vs tag " << e.exp_s1
+      << sites[e.site < 7 ? e.site : 0] << " row " << e.row << " (checksum " << e.got_s1 << " vs tag " << e.exp_s1
      << ", request " << e.got_seq << " vs expected " << e.exp_seq << ") [rank=" << rank_ << " world=" << world_ << "]";
   throw std::runtime_error(os.str());
 }

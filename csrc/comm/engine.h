@@ -98,6 +98,20 @@ struct TraceSummary {
   double ms[kTpCount] = {0, 0, 0, 0, 0, 0};  // ms[p] = summed time between point p-1 and p (ms[0] unused)
   double comm_ms = 0.0;                       // summed kTpStart -> kTpCommEnd
   double total_ms = 0.0;                      // summed kTpStart -> kTpEpiEnd
+  // ring hops (per round: start -> credits granted -> kernels done -> upstream data ready), summed over the traced
+  // requests' rounds; hop_max_ms: the longest single round
+  uint64_t hop_rounds = 0;
+  double hop_credit_ms = 0.0, hop_kernel_ms = 0.0, hop_ready_ms = 0.0, hop_max_ms = 0.0;
+};
+
+// verify-error sites (VerifyError::site): copying paths 1-3, direct P2P paths 4-6
+enum VerifySite : uint32_t {
+  kSiteMeshAllToAll = 1,
+  kSiteMeshAllGather = 2,
+  kSiteRingRound = 3,
+  kSiteMeshDirectSend = 4,
+  kSiteMeshDirectGather = 5,
+  kSiteRingDirect = 6,
 };
 
 // Deferred epilogue of a request (decode + SGD), launched on the given stream at commit().
@@ -221,7 +235,15 @@ class AllReduceEngine {
   struct RequestTrace {
     hipEvent_t ev[kTpCount] = {};
     int64_t logical_bytes = 0, wire_bytes = 0;
+    size_t hop_first = 0, hop_count = 0;  // ring rounds: 4 events each in hop_pool_
   };
+  std::vector<hipEvent_t> hop_pool_;
+  size_t hop_used_ = 0;
+  void hop_mark(int point);  // ring round timestamp of the traced request being built (point 0..3)
+  // verify mode on the direct P2P paths: tag a message where it landed (trailer of its slot) / check one on arrival
+  void tag_direct(const uint8_t* msg, size_t bytes, uint8_t* trailer, uint32_t seq, hipStream_t st);
+  void verify_direct(const uint8_t* msg, size_t bytes, const uint8_t* trailer, uint32_t seq, uint32_t site,
+                     uint32_t row, hipStream_t st);
   // record trace point tp of the request being built on the stream its phases run on
   void mark(int tp) {
     trace_marked_ |= 1u << tp;

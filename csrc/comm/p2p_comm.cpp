@@ -7,7 +7,10 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
 #include <thread>
+
+#include <unistd.h>
 
 namespace fan {
 
@@ -16,14 +19,27 @@ namespace {
 struct Handles {
   hipIpcMemHandle_t arena;
   hipIpcMemHandle_t flags;
+  char host[64];  // where the arena lives: a peer on another (host, PCI bus) is a cross-device peer
+  char bus[32];
 };
+
+void device_identity(int device, char* host, size_t host_len, char* bus, size_t bus_len) {
+  std::memset(host, 0, host_len);
+  std::memset(bus, 0, bus_len);
+  gethostname(host, host_len - 1);
+  if (hipDeviceGetPCIBusId(bus, (int)bus_len - 1, device) != hipSuccess) {
+    (void)hipGetLastError();
+    std::snprintf(bus, bus_len, "dev%d", device);
+  }
+}
 
 }  // namespace
 
 P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
     : rank_(rank), world_(world), device_(device), slot_((slot_bytes + 255) / 256 * 256) {
   FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
-  FAN_CHECK(slot_ > 0, "slot_bytes must be > 0");
+  FAN_CHECK(slot_ > kTrailerBytes, "slot_bytes must exceed the 256-B verify trailer");
+  if (const char* c = std::getenv("FAN_P2P_COPY")) sdma_ = !std::strcmp(c, "sdma");
   FAN_HIP_CHECK(hipSetDevice(device));
   // Arena and flags UNCACHED (see the memory-ordering argument in p2p_comm.h): peers write them over xGMI, so no
   // line of them may sit in this GPU's (per-XCD, non-coherent) L2 when the reader consumes a new message.
@@ -193,17 +209,21 @@ std::string P2PComm::handles() const {
   Handles h;
   FAN_HIP_CHECK(hipIpcGetMemHandle(&h.arena, arena_));
   FAN_HIP_CHECK(hipIpcGetMemHandle(&h.flags, flags_));
+  device_identity(device_, h.host, sizeof(h.host), h.bus, sizeof(h.bus));
   return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
 }
 
 void P2PComm::connect(const std::vector<std::string>& all) {
   FAN_CHECK((int)all.size() == world_, "connect: need one handle blob per rank");
   FAN_HIP_CHECK(hipSetDevice(device_));
+  char host[64], bus[32];
+  device_identity(device_, host, sizeof(host), bus, sizeof(bus));
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
     FAN_CHECK(all[p].size() == sizeof(Handles), "connect: bad handle blob");
     Handles h;
     std::memcpy(&h, all[p].data(), sizeof(h));
+    if (std::strncmp(h.host, host, sizeof(host)) || std::strncmp(h.bus, bus, sizeof(bus))) cross_device_ = true;
     void* a = nullptr;
     void* f = nullptr;
     FAN_HIP_CHECK(hipIpcOpenMemHandle(&a, h.arena, hipIpcMemLazyEnablePeerAccess));
@@ -212,6 +232,18 @@ void P2PComm::connect(const std::vector<std::string>& all) {
     peer_flags_[p] = reinterpret_cast<uint64_t*>(f);
     opened_[p] = true;
   }
+  // the command-processor release is unverified across devices (p2p_comm.h): peers on other GPUs get the in-kernel
+  // system-scope release unless the user chose a mode
+  if (cross_device_ && !std::getenv("FAN_P2P_RELEASE") && p2p_release_mode() == 3) set_p2p_release_mode(1);
+}
+
+void P2PComm::move(const std::vector<P2PCopy>& segs, hipStream_t s) {
+  if (!sdma_) {
+    launch_multi_copy(segs, s);
+    return;
+  }
+  for (const P2PCopy& c : segs)
+    if (c.bytes) FAN_HIP_CHECK(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDeviceNoCU, s));
 }
 
 void P2PComm::connect_local(const std::vector<P2PComm*>& ranks) {
@@ -246,7 +278,7 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
         any = true;
         dests.push_back(p);
       }
-      FAN_CHECK(off + op.bytes <= slot_, "p2p: message larger than the arena slot (raise slot_bytes)");
+      FAN_CHECK(off + op.bytes <= payload_bytes(), "p2p: message larger than the arena slot (raise slot_bytes)");
       out.push_back({op.ptr, slot_ptr(peer_arena_[p], rank_, q) + off, op.bytes});
       bytes_to_peer_[p] += (int64_t)op.bytes;
       off += (op.bytes + 15) / 16 * 16;
@@ -272,7 +304,7 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
         any = true;
         srcs.push_back(src);
       }
-      FAN_CHECK(off + op.bytes <= slot_, "p2p: message larger than the arena slot (raise slot_bytes)");
+      FAN_CHECK(off + op.bytes <= payload_bytes(), "p2p: message larger than the arena slot (raise slot_bytes)");
       in.push_back({slot_ptr(arena_, src, q) + off, op.ptr, op.bytes});
       off += (op.bytes + 15) / 16 * 16;
     }

@@ -28,6 +28,17 @@
 //      that job; uncached() reports which.)
 //   5. WAR: a sender reuses a parity slot only after the receiver's ack (written after its copy-out kernel
 //      completed) shows the previous message in it was consumed.
+//   Cross-device peers: the command-processor release (mode "cp", the default) was measured only with every rank on
+//   ONE GPU, where system and device scope coincide. Whether posted xGMI stores to another GPU's arena are visible
+//   before a flag written after a hipEventReleaseToSystem marker is UNVERIFIED on this pool (no multi-GPU node), so
+//   connect() switches a process whose peers live on other devices to the in-kernel per-workgroup system-scope
+//   release ("block") unless FAN_P2P_RELEASE names a mode explicitly; verify mode (trailer tags, below) checks the
+//   ordering in band on whichever mode runs.
+// Verify trailer: the last kTrailerBytes of every slot hold up to 16 message tags ({s1, s2, seq, bytes}, verify.h);
+// messages use at most payload_bytes() of a slot.
+// Pure data movement (prepacked sends, FORWARD hops, arena -> scratch) goes through move(): the CU copy kernel, or
+// with FAN_P2P_COPY=sdma the copy engines (hipMemcpyDeviceToDeviceNoCU: no CU, so beside a persistent GEMM that
+// holds every CU the copy still runs).
 // abort() releases every stream parked on this rank's flags (poison value) so a dead peer cannot hang the GPU;
 // the communicator then refuses further calls.
 #pragma once
@@ -51,9 +62,11 @@ class P2PComm : public Comm {
  public:
   P2PComm(int rank, int world, int device, size_t slot_bytes);
   ~P2PComm() override;
+  static constexpr size_t kTrailerBytes = 256;  // per slot: 16 verify tags of 16 B
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   size_t slot_bytes() const { return slot_; }
+  size_t payload_bytes() const { return slot_ - kTrailerBytes; }  // what the messages of one slot may use
 
   // IPC bootstrap: this rank's (arena, flags) handles as bytes; connect() with every rank's bytes (in rank
   // order) opens the peers' mappings. connect_local() wires ranks living in one process (no IPC).
@@ -93,6 +106,17 @@ class P2PComm : public Comm {
   void release_from(const Round& r, const std::vector<int>& from, hipStream_t s);
   // message from rank `src` in round r, in this rank's arena
   const uint8_t* src(const Round& r, int from) const { return slot_ptr(arena_, from, r.seq); }
+  // verify tag k (16 B) of this rank's slot at `peer` / of `from`'s slot here, for round r
+  uint8_t* dst_tag(const Round& r, int peer, int k) const { return dst(r, peer) + payload_bytes() + 16 * (size_t)k; }
+  uint8_t* src_tag(const Round& r, int from, int k) const {
+    return slot_ptr(arena_, from, r.seq) + payload_bytes() + 16 * (size_t)k;
+  }
+  // pure copies (see the header comment): CU kernel or copy engines
+  void move(const std::vector<P2PCopy>& segs, hipStream_t s);
+  bool sdma() const { return sdma_; }
+  void set_sdma(bool on) { sdma_ = on; }
+  // some peer's arena lives on another GPU (or host): set by connect()
+  bool cross_device() const { return cross_device_; }
   void all_to_all(const void* send, void* recv, size_t bytes_per_peer, hipStream_t s) override;
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override;
   std::string async_error() override { return aborted_ ? "p2p transport aborted" : ""; }
@@ -158,6 +182,8 @@ class P2PComm : public Comm {
   bool uncached_ = false;
   std::string arena_mem_;
   hipEvent_t rel_ev_ = nullptr;  // system-scope release before the flag writes (release mode "cp")
+  bool sdma_ = false;
+  bool cross_device_ = false;
   void release_before_flags(hipStream_t s);
 };
 

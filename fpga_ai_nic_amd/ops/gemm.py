@@ -165,8 +165,10 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
             or torch.cuda.is_current_stream_capturing() or _shares_storage(C, A, B, aux, bias)):
         run(tuple(static[:3]), tw, update)
         return
-    k = T.key(M, N, K, a_t, b_t, epilogue, colsum is not None, 0 if wire is None else 2 if update is not None else 1,
-              C.device)
+    # a fused-update call shares the key of the wire call (the tuner's trial launches store the wire either way): the
+    # fused and the unfused schedule of one shape then run the SAME plan, so their dW rounding — and the weights they
+    # train — stay bit-identical (a split-K or tile change alters the summation order)
+    k = T.key(M, N, K, a_t, b_t, epilogue, colsum is not None, 0 if wire is None else 1, C.device)
     plan = T.lookup(k)
     if plan is None and not T.worth_tuning(M, N, static, C.device):
         plan = T.keep_static(k, static)

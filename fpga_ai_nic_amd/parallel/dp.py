@@ -79,7 +79,7 @@ class DataParallelTrainer:
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
                  loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True,
                  commit_at_end: bool | None = None, panels: int | None = None, panel_submit: str = "split",
-                 fused_update: bool | None = None):
+                 fused_update: bool | None = None, gemm_inflight: str | None = None):
         """``panels`` (default env FAN_PANELS, else off; < 2 disables): the
         last-issued bucket (layer 0: no backward left to hide its exchange behind) is computed as row panels of dW,
         each submitted as a request of its own right after its GEMM (multi-rank C++ engine, mesh, GEMM-encoded
@@ -92,7 +92,14 @@ class DataParallelTrainer:
         takes each encoded gradient group through its BFP round trip in registers and applies the SGD update to the
         layer's weights in place — the engine's decode + SGD pass over the whole bucket (master read + write, bf16
         copy write, wire read) disappears into the GEMM. Same operations in the same order: bit-identical weights
-        to the unfused schedule. The layer's bwd-data GEMM (which reads the weights) is issued first."""
+        to the unfused schedule. The layer's bwd-data GEMM (which reads the weights) is issued first.
+
+        ``gemm_inflight`` (default env FAN_GEMM_INFLIGHT, else 'persistent'): the GEMM form while a request of this
+        step is in flight on the side stream (multi-rank engines only). 'persistent': one 4-wave workgroup per CU
+        looping over tiles — it holds every CU until it ends, so the comm stream's kernels start only at GEMM
+        boundaries; 'grid': one workgroup per tile from the first submit to the end of backward, so comm kernels
+        start at tile boundaries (the forced 1-rank path's comm phase took half the device time that way,
+        profiles/r3_persist_vs_tile_grid_forced.txt). bench.py picks between them by timing both at world > 1."""
         self.m = model
         self.engine = engine
         self.world = engine.world if engine is not None else 1
@@ -117,6 +124,12 @@ class DataParallelTrainer:
         self.fused_update = (fu and self.prepack and bool(getattr(engine, "inline", False))
                              and getattr(engine, "codec", "") == "bfp_rne")
         self.fused_updates = 0
+        gi = os.environ.get("FAN_GEMM_INFLIGHT", "persistent") if gemm_inflight is None else gemm_inflight
+        if gi not in ("persistent", "grid"):
+            raise ValueError(f"gemm_inflight must be persistent|grid, got {gi!r}")
+        self.gemm_inflight = gi if (self.cuda and engine is not None and not getattr(engine, "inline", True)) \
+            else "persistent"
+        self._persist_saved = None
         self.panel_submit = panel_submit
         self.panel_plans: dict[int, dict] = {}
         # opt-in (FAN_PANELS=4): measured on the one-GPU pool the split costs more than it hides — each panel adds a
@@ -254,6 +267,7 @@ class DataParallelTrainer:
                                                       grad_scale=self.grad_scale, weight_decay=self.wd,
                                                       momentum=self.momentum, nesterov=self.nesterov, defer=True,
                                                       name=f"fc{i}", **kw)
+                        self._gemm_grid(True)
                     m.backward_data(i)
                     if h is not None:
                         self.pending[i] = h if self.commit_at_end else h.commit_after_current()
@@ -266,6 +280,7 @@ class DataParallelTrainer:
                 self.times["bwd_first"] += t1 - t0
                 self.times["bwd"] += t1 - t0
                 t0 = t1
+        self._gemm_grid(False)
         if self.commit_at_end:  # issue order L-1..0: the epilogues run in the order their all-reduces finish
             for i in reversed(range(m.L)):
                 h = self.pending[i]
@@ -274,6 +289,20 @@ class DataParallelTrainer:
         if prof:
             self._sync()
             self.times["bwd"] += time.perf_counter() - t0
+
+    def _gemm_grid(self, on: bool):
+        """gemm_inflight='grid': GEMMs enqueued while a request is in flight run one workgroup per tile."""
+        if self.gemm_inflight != "grid":
+            return
+        from .. import _ext
+
+        C = _ext.require()
+        if on and self._persist_saved is None:
+            self._persist_saved = C.gemm_persist()
+            C.gemm_set_persist(0)
+        elif not on and self._persist_saved is not None:
+            C.gemm_set_persist(self._persist_saved)
+            self._persist_saved = None
 
     def _sync(self):
         if self.cuda:

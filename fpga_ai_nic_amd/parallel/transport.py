@@ -146,7 +146,10 @@ class NativeTransport(Transport):
             uid = store.get(key)
         self.rank, self.world = rank, world
         self._local = world == 1 and not force_collectives
-        self.comm = C.NativeComm(uid, rank, world, device)
+        from ..utils.dist import stdout_to_stderr
+
+        with stdout_to_stderr():  # RCCL's init banner goes to stderr
+            self.comm = C.NativeComm(uid, rank, world, device)
 
     def all_to_all(self, send, recv):
         if self._local:
@@ -200,6 +203,50 @@ def make_p2p_comm(rank: int | None = None, world: int | None = None, device: int
     comm.connect(blobs)
     dist.barrier()
     return comm
+
+
+def try_p2p_comm(slot_bytes: int = 128 << 20):
+    """:func:`make_p2p_comm` that every rank of the default group either gets or, if ANY rank failed (no IPC, no
+    peer access, allocation refused), all ranks get None together — a collective that cannot leave one rank waiting
+    in a later exchange. Returns (comm or None, error text of the first failing rank or None)."""
+    C = _ext.require()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    comm, err = None, None
+    try:
+        comm = C.P2PComm(rank, world, torch.cuda.current_device(), slot_bytes)
+        blob = comm.handles()
+    except Exception as e:  # noqa: BLE001 - reported, and every rank drops the transport
+        comm, blob, err = None, None, f"rank {rank}: {e}"
+    blobs = [None] * world
+    dist.all_gather_object(blobs, blob)
+    if any(b is None for b in blobs):
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        return None, next((e for e in errs if e), "a rank could not create its arena")
+    try:
+        comm.connect(blobs)
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {e}"
+    errs = [None] * world
+    dist.all_gather_object(errs, err)
+    if any(errs):
+        return None, next(e for e in errs if e)
+    return comm, None
+
+
+def try_native_transport(force_collectives: bool = False):
+    """The engine's own RCCL communicator on every rank, or None on every rank (with the first error text) when
+    any rank could not create it."""
+    t, err = None, None
+    try:
+        t = NativeTransport(force_collectives=force_collectives)
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {dist.get_rank()}: {e}"
+    errs = [None] * dist.get_world_size()
+    dist.all_gather_object(errs, err)
+    if any(errs):
+        return None, next(e for e in errs if e)
+    return t, None
 
 
 class ThreadFabric:

@@ -6,8 +6,10 @@ orders are computed by the planner.
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -36,11 +38,34 @@ def init_distributed(backend: str | None = None, timeout_s: float = 600.0, force
         # FAN_CTRL_BACKEND=gloo: control plane (bootstrap, broadcast, barrier) over gloo even on GPU — for
         # several ranks sharing one GPU with the P2P transport, where RCCL refuses duplicate devices
         be = backend or os.environ.get("FAN_CTRL_BACKEND") or ("nccl" if use_cuda else "gloo")
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if be == "nccl" and local_world > max(1, torch.cuda.device_count()):
+            # more ranks than GPUs on this node: ranks share a device, which RCCL refuses ("invalid usage");
+            # the control plane goes over gloo (the P2P transport still moves the gradients between the ranks)
+            print(f"[dist] {local_world} local ranks on {torch.cuda.device_count()} GPU(s): control plane over gloo",
+                  file=sys.stderr, flush=True)
+            be = "gloo"
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = device
-        dist.init_process_group(**kw)
+        with stdout_to_stderr():  # RCCL prints its version banner on stdout: keep stdout for the results
+            dist.init_process_group(**kw)
     return rank, world, local, device
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Route file descriptor 1 to 2 for the duration (native libraries that print banners on stdout, e.g. RCCL at
+    communicator init), so a benchmark's stdout carries only its result lines."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def barrier():

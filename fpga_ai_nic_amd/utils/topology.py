@@ -145,15 +145,23 @@ def agreed_link_matrix(world: int):
     """The link matrix every rank of the default process group uses: each rank reports the PCI bus id of its own
     device; rank 0 derives the matrix (rocm-smi link types of those GPUs, else peer access from its view) and
     broadcasts it, so all ranks plan the SAME rings even if their local tool calls would disagree (a timed-out
-    or restricted rocm-smi on one rank would otherwise give that rank different rings and mismatched peers)."""
+    or restricted rocm-smi on one rank would otherwise give that rank different rings and mismatched peers).
+    Ranks that span several hosts get None (bus ids are only unique within a host)."""
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() == world):
         return link_matrix(world)
-    bus = [None] * world
-    dist.all_gather_object(bus, own_bus_id())
+    import socket
+
+    ident = [None] * world
+    dist.all_gather_object(ident, (socket.gethostname(), own_bus_id()))
+    bus = [b for _, b in ident]
     obj = [None]
-    if dist.get_rank() == 0:
+    if len({h for h, _ in ident}) > 1:
+        # ranks on several hosts: PCI bus ids repeat across hosts and rank 0's rocm-smi describes only its own node,
+        # so no link matrix is derived (the planner assumes a fully connected world)
+        obj = [{"links": None, "bus_ids": bus}]
+    elif dist.get_rank() == 0:
         peer = None
         if torch.cuda.is_available():  # peer access from rank 0's view, for the devices it can see
             local = {device_bus_id(i): i for i in range(torch.cuda.device_count())}

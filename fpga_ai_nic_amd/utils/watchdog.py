@@ -35,6 +35,7 @@ class Watchdog:
         self.tag = tag
         self.backstop_s = backstop_s
         self.phase: str | None = None
+        self.budget_s = self.timeout_s
         self._deadline = None
         self._cv = threading.Condition()
         self._stop = False
@@ -50,6 +51,7 @@ class Watchdog:
             return
         with self._cv:
             self.phase = phase
+            self.budget_s = t  # what _expire reports (a phase may carry its own budget)
             self._deadline = time.monotonic() + t
             self._cv.notify_all()
         faulthandler.dump_traceback_later(t + self.backstop_s, exit=True)
@@ -79,16 +81,17 @@ class Watchdog:
                 if left > 0:
                     self._cv.wait(left)
                     continue
-                phase = self.phase
+                phase, budget = self.phase, self.budget_s
                 break
             else:
                 return
         self.fired = True
-        self._expire(phase)
+        self._expire(phase, budget)
 
-    def _expire(self, phase):
+    def _expire(self, phase, budget=None):
         err = sys.stderr
-        print(f"[{self.tag}] phase '{phase}' exceeded {self.timeout_s:.0f} s: dumping state and aborting",
+        budget = self.timeout_s if budget is None else budget
+        print(f"[{self.tag}] phase '{phase}' exceeded {budget:.0f} s: dumping state and aborting",
               file=err, flush=True)
         if self.dump is not None:
             try:

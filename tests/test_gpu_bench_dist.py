@@ -3,7 +3,11 @@ torch.distributed.run child), the ranks share the GPU, the gradient plane is the
 receive arenas + stream-ordered flags: the same protocol that runs over xGMI between GPUs) and the control plane is
 gloo (RCCL refuses two ranks on one device). Everything the round-end 8-GPU run reports must already be present and
 self-consistent here: exactly one JSON line, a measured all-reduce (extra.allreduce, from the traced pass), the
-communicator's own rank count, direct P2P rounds, and bit-identical replicas after the run (extra.dist)."""
+communicator's own rank count, direct P2P rounds, and bit-identical replicas after the run (extra.dist) — and the
+self-selection the driver's multi-GPU run relies on: the schedule A/B in warmup (every arm timed or excluded with
+its error: RCCL refuses two ranks on one device, so only the P2P arms run here), the bit-exact all-reduce gate of
+the chosen arm, and the config-4 / uncompressed extras, all within the run's budget. A peer slot corrupted after its
+ready flag makes every arm fail the gate and the run exit non-zero."""
 import json
 import os
 import subprocess
@@ -41,6 +45,31 @@ def test_bench_two_ranks_p2p_one_gpu(tmp_path):
     assert len(d["bus_ids"]) == 2 and d["bus_ids"][0] == d["bus_ids"][1]  # both ranks on the one GPU
     assert ex["engine_counters"]["direct_rounds"] > 0
     assert ex["mb256"]["samples_per_s"] > 0
+    ab = ex["schedule_ab"]
+    timed = [x for x in ab if "ms_per_step" in x]
+    assert len(timed) >= 3 and sum(bool(x.get("chosen")) for x in ab) == 1, ab
+    assert all(x["exact"] for x in timed), ab
+    assert any(x["arm"].startswith("rccl") and "error" in x for x in ab), ab  # excluded, not fatal
+    assert d["allreduce_exact"] is True and d["allreduce_gate"]["prepacked"] is True, d
+    c4 = ex["config4"]
+    assert c4["bfp_mesh_p2p"]["algo_bw_GBps"] > 0 and c4["bfp_ring_p2p"]["algo_bw_GBps"] > 0, c4
+    assert c4["raw_f32_mesh_p2p"]["algo_bw_GBps"] > 0 and "skipped" in c4["rccl_f32"], c4
+    un = ex["uncompressed"]
+    assert un["p2p_raw_f32_mesh"]["ms_per_step"] > 0 and un["speedup_vs_best_uncompressed"] > 0, un
+    assert ex["extras_s"] < 240 and ex["run_s"] < 400, (ex["extras_s"], ex["run_s"])
+
+
+def test_bench_gate_rejects_a_corrupted_peer_slot(tmp_path):
+    """Every engine flips a byte of the first message it receives, after that message's ready flag was raised
+    (fault site p2p_recv): the owner reduces a wrong shard and every rank decodes the same wrong sum (the replicas
+    would still agree). The exactness gate catches it on every arm, so no arm is run and the bench exits non-zero."""
+    os.environ["FAN_FAULT"] = "p2p_recv:0:flip"
+    try:
+        r, recs = _bench(tmp_path, "--extra-budget", "0", timeout=300)
+    finally:
+        os.environ.pop("FAN_FAULT", None)
+    assert r.returncode != 0 and not recs, (r.returncode, r.stdout[-2000:])
+    assert "exactness gate failed" in r.stderr, r.stderr[-4000:]
 
 
 def test_bench_watchdog_fires_on_a_hung_peer(tmp_path):

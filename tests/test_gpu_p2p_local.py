@@ -4,7 +4,10 @@ stream per rank. The two-process test (test_gpu_p2p.py) covers the IPC bootstrap
 neighbour each way; here the direct ring runs over several arc-disjoint rings at once (every rank a different
 downstream peer per ring, hw/all_reduce.sv's single ring generalised: sw/setup_route.sh), and the direct mesh over
 N - 1 peers. Each schedule is bit-exact against the spec simulator, from f32 and from producer-encoded (prepacked)
-input, and counts its direct rounds.
+input, and counts its direct rounds — also in verify mode (every message tagged in its slot's trailer where it landed
+and checked on arrival: ``verified_rows`` > 0) and with the pure copies on the copy engines (FAN_P2P_COPY=sdma). A
+fault rule that corrupts a received slot AFTER its ready flag was raised (``p2p_recv``) must be caught by verify mode
+with the site and row of that message.
 
 The ranks' flag waits are command-processor waits (hipStreamWaitValue64): a stream parked on a peer's flag blocks the
 hardware queue it runs on. HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES queues (4 by default), so N
@@ -29,15 +32,20 @@ from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _run(world, algo, rings, m=40000, max_slice=2048):
+def _run(world, algo, rings, m=40000, max_slice=2048, mode="plain"):
     C = _ext.require()
     comms = [C.P2PComm(r, world, 0, 2 << 20) for r in range(world)]
     C.P2PComm.connect_local(comms)
+    if mode == "sdma":
+        for c in comms:
+            c.sdma = True
     rng = np.random.default_rng(100 + world)
     grads = [rng.standard_normal(m).astype(np.float32) for _ in range(world)]
     res, errs = [None] * world, [None] * world
+    verify = mode in ("verify", "fault")
+    fault = "p2p_recv:0:flip" if mode == "fault" else None
     engines = [NativeAllReduce(None, codec="bfp_rne", algo=algo, rings=rings, max_slice_elems=max_slice,
-                               comm=comms[r]) for r in range(world)]
+                               comm=comms[r], verify=verify, fault=fault) for r in range(world)]
 
     def run(r):
         try:
@@ -58,8 +66,9 @@ def _run(world, algo, rings, m=40000, max_slice=2048):
                     out_p = torch.zeros(L.n_pad, device="cuda")
                     eng.allreduce(g, out_p, n_valid=m, prepacked=(buf, m // 16 * 16)).synchronize(60)
                 s.synchronize()
+                cn = eng.counters()
                 res[r] = (out.cpu().numpy(), None if out_p is None else out_p.cpu().numpy(), L,
-                          eng.counters()["direct_rounds"], [list(o) for o in eng.orders])
+                          cn["direct_rounds"], [list(o) for o in eng.orders], cn["verified_rows"])
         except Exception as e:  # noqa: BLE001
             errs[r] = e
 
@@ -69,6 +78,8 @@ def _run(world, algo, rings, m=40000, max_slice=2048):
     for t in ts:
         t.join(180)
     assert not any(t.is_alive() for t in ts), "virtual rank thread hung"
+    if mode == "fault":
+        return errs, None, None
     assert not any(errs), errs
     L = res[0][2]
     gin = [np.pad(x, (0, L.n_pad - m)) for x in grads]
@@ -79,12 +90,22 @@ def _run(world, algo, rings, m=40000, max_slice=2048):
     return res, ref, L
 
 
-def _check(world, algo, rings):
-    res, ref, L = _run(world, algo, rings)
+def _check(world, algo, rings, mode="plain"):
+    res, ref, L = _run(world, algo, rings, mode=mode)
     m = 40000
+    if mode == "fault":  # every rank corrupted the first message it received, after that message's ready flag
+        site, row = ("mesh direct send", 1) if algo == "mesh" else ("ring direct hop", 0)
+        why = []
+        for r, e in enumerate(res):
+            want_row = (1 if r == 0 else 0) if algo == "mesh" else row
+            if e is None or "corrupted" not in str(e) or f"{site} row {want_row} " not in str(e):
+                why.append(f"rank {r}: expected a '{site} row {want_row}' corruption, got {e!r}")
+        return {"ok": not why, "why": why, "rings": 0}
     out = {"ok": True, "why": [], "rings": len(res[0][4])}
     for r in range(world):
-        o, o_p, _, direct, orders = res[r]
+        o, o_p, _, direct, orders, verified = res[r]
+        if mode == "verify" and verified <= 0:
+            out["why"].append(f"rank {r}: verify mode checked no message")
         if not np.array_equal(o[:m], ref[:m]):
             out["why"].append(f"rank {r}: {algo} x{rings} differs from the simulator")
         if o_p is not None and not np.array_equal(o_p, o):
@@ -97,12 +118,10 @@ def _check(world, algo, rings):
     return out
 
 
-@pytest.mark.parametrize("world,algo,rings", [(3, "ring", 2), (4, "ring", 3), (8, "ring", 7), (3, "mesh", 1),
-                                              (8, "mesh", 1)])
-def test_direct_p2p_schedules_bit_exact(world, algo, rings):
+def _child(world, algo, rings, mode):
     env = dict(os.environ, GPU_MAX_HW_QUEUES="32")
     try:
-        r = subprocess.run([sys.executable, os.path.abspath(__file__), str(world), algo, str(rings)], env=env,
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), str(world), algo, str(rings), mode], env=env,
                            capture_output=True, text=True, timeout=150)
     except subprocess.TimeoutExpired as e:
         pytest.fail(f"world {world} {algo}: child timed out\n{(e.stderr or '')[-3000:]}")
@@ -110,9 +129,30 @@ def test_direct_p2p_schedules_bit_exact(world, algo, rings):
     assert r.returncode == 0 and len(recs) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
     rec = recs[0]
     assert rec["ok"], rec["why"]
+    return rec
+
+
+@pytest.mark.parametrize("world,algo,rings", [(3, "ring", 2), (4, "ring", 3), (8, "ring", 7), (3, "mesh", 1),
+                                              (8, "mesh", 1)])
+def test_direct_p2p_schedules_bit_exact(world, algo, rings):
+    rec = _child(world, algo, rings, "plain")
     if algo == "ring":
         assert rec["rings"] >= min(rings, 2)  # several arc-disjoint rings at once (N = 4 has 2, not 3)
 
 
+@pytest.mark.parametrize("world,algo,rings", [(4, "ring", 3), (4, "mesh", 1)])
+@pytest.mark.parametrize("mode", ["verify", "sdma"])
+def test_direct_p2p_verify_and_sdma_bit_exact(world, algo, rings, mode):
+    """verify mode runs the direct paths (no copying fallback) and checks every message; the copy-engine path moves
+    the same bytes."""
+    _child(world, algo, rings, mode)
+
+
+@pytest.mark.parametrize("algo,rings", [("mesh", 1), ("ring", 2)])
+def test_direct_p2p_verify_catches_a_slot_corrupted_after_its_flag(algo, rings):
+    _child(3, algo, rings, "fault")
+
+
 if __name__ == "__main__":
-    print(json.dumps(_check(int(sys.argv[1]), sys.argv[2], int(sys.argv[3]))), flush=True)
+    mode = sys.argv[4] if len(sys.argv) > 4 else "plain"
+    print(json.dumps(_check(int(sys.argv[1]), sys.argv[2], int(sys.argv[3]), mode)), flush=True)
