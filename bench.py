@@ -221,7 +221,7 @@ def main(argv=None):
         return ctx["p2p"]
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
-              force=False):
+              force=False, panels=None):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default)."""
         comm = None
@@ -248,10 +248,11 @@ def main(argv=None):
             for l in model.layers:
                 ctrl.broadcast_(l.master, 0)
             model.sync_lp()
-        tr = DataParallelTrainer(model, eng, lr=a.lr, gemm_inflight=gemm, fused_update=fused)
+        tr = DataParallelTrainer(model, eng, lr=a.lr, gemm_inflight=gemm, fused_update=fused, panels=panels)
         info = {"compress": kind, "algo": algo, "rings": getattr(eng, "rings", 0) if eng is not None else 0,
                 "transport": (getattr(t, "name", transport) if comm is None else "p2p") if multi or force else "none",
-                "gemm_inflight": tr.gemm_inflight, "copy": ("sdma" if sdma else "kernel") if comm is not None else None}
+                "gemm_inflight": tr.gemm_inflight, "copy": ("sdma" if sdma else "kernel") if comm is not None else None,
+                "panels": tr.panel_plans[0]["chunks"] if tr.panel_plans else 0}
         return Setup(name, eng, model, tr, info)
 
     def release(setup):
@@ -350,6 +351,10 @@ def main(argv=None):
                 arms.append(dict(name=f"p2p_ring_{gm}", kind="bfp", algo="ring", rings=R, transport="p2p", gemm=gm))
             arms.append(dict(name="p2p_mesh_sdma", kind="bfp", algo="mesh", transport="p2p", sdma=True))
             arms.append(dict(name="p2p_ring_sdma", kind="bfp", algo="ring", rings=R, transport="p2p", sdma=True))
+            # layer 0's bucket as 4 row panels, each submitted right after its GEMM (the exchange of the last bucket,
+            # which no backward is left to hide, starts a panel earlier; dp.py panels)
+            arms.append(dict(name="rccl_mesh_panels4", kind="bfp", algo="mesh", transport="native", panels=4))
+            arms.append(dict(name="p2p_mesh_panels4", kind="bfp", algo="mesh", transport="p2p", panels=4))
         else:
             arms.append(dict(name=f"{impl}_{a.algo}", kind="bfp", algo=a.algo, rings=a.rings, transport="torch"))
         schedule_ab = []
@@ -362,7 +367,7 @@ def main(argv=None):
             try:
                 setup = build(spec["name"], spec["kind"], algo=spec.get("algo", "mesh"), rings=spec.get("rings", 1),
                               transport=spec["transport"], gemm=spec.get("gemm", "persistent"),
-                              sdma=spec.get("sdma", False))
+                              sdma=spec.get("sdma", False), panels=spec.get("panels", 0))
                 rec.update(setup.info)
                 g = gate.allreduce_exactness(setup.engine, timeout_s=min(eng_timeout, 120.0))
                 rec["exact"] = g["exact"]

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--engine", default="native", choices=["python", "native"])
+    ap.add_argument("--only", default="", choices=["", "compute", "comm", "overlap"],
+                    help="profiling: run only rounds of this kind (one kernel trace per kind, for tools/overlap_report.py)")
     a = ap.parse_args()
     rank, world, _, dev = D.init_distributed()
     transport = TorchDistTransport() if world > 1 else ThreadFabric(1).transport(0)
@@ -91,10 +93,14 @@ def main():
 
     run(True, True)
     res = {"compute": [], "comm": [], "overlap": []}
+    kinds = {"compute": (True, False), "comm": (False, True), "overlap": (True, True)}
     for _ in range(a.rounds):
-        res["compute"].append(run(True, False))
-        res["comm"].append(run(False, True))
-        res["overlap"].append(run(True, True))
+        for k, (dc, dm) in kinds.items():
+            if not a.only or a.only == k:
+                res[k].append(run(dc, dm))
+    if a.only:
+        for k in res:
+            res[k] = res[k] or [0.0]
     tc, tm, to = (statistics.median(res[k]) * 1e3 for k in ("compute", "comm", "overlap"))
     eff = (tc + tm - to) / min(tc, tm) if min(tc, tm) > 0 else 0.0
     flops = bert.layer_backward_flops(T) * a.layers
