@@ -221,7 +221,7 @@ def main(argv=None):
         return ctx["p2p"]
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
-              force=False, panels=None):
+              force=False, panels=None, ring_sub=1):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default)."""
         comm = None
@@ -239,7 +239,8 @@ def main(argv=None):
         elif force and cuda and impl == "native":  # world-1 split: the multi-rank path over a 1-rank RCCL group
             t = NativeTransport(force_collectives=True)
         eng = make_engine(t, kind, rounding=a.rounding, algo=algo, rings=rings, force_comm=force or a.force_dist,
-                          impl=eimpl, comm=comm, side_stream=a.side_stream and not multi, timeout_s=eng_timeout)
+                          impl=eimpl, comm=comm, side_stream=a.side_stream and not multi, timeout_s=eng_timeout,
+                          **({"ring_sub": ring_sub} if eimpl == "native" else {}))
         if hasattr(eng, "epilogue_on_producer") and not getattr(eng, "inline", True):
             eng.epilogue_on_producer = a.epi == "producer"
         pad_fn = (lambda n: eng.layout(n).n_pad) if eng is not None else None
@@ -252,7 +253,8 @@ def main(argv=None):
         info = {"compress": kind, "algo": algo, "rings": getattr(eng, "rings", 0) if eng is not None else 0,
                 "transport": (getattr(t, "name", transport) if comm is None else "p2p") if multi or force else "none",
                 "gemm_inflight": tr.gemm_inflight, "copy": ("sdma" if sdma else "kernel") if comm is not None else None,
-                "panels": tr.panel_plans[0]["chunks"] if tr.panel_plans else 0}
+                "panels": tr.panel_plans[0]["chunks"] if tr.panel_plans else 0,
+                "ring_sub": int(getattr(eng, "ring_sub", 1)) if algo == "ring" else None}
         return Setup(name, eng, model, tr, info)
 
     def release(setup):
@@ -351,6 +353,8 @@ def main(argv=None):
                 arms.append(dict(name=f"p2p_ring_{gm}", kind="bfp", algo="ring", rings=R, transport="p2p", gemm=gm))
             arms.append(dict(name="p2p_mesh_sdma", kind="bfp", algo="mesh", transport="p2p", sdma=True))
             arms.append(dict(name="p2p_ring_sdma", kind="bfp", algo="ring", rings=R, transport="p2p", sdma=True))
+            # each ring hop streamed in 3 sub-slices (a ready flag each; engine.cpp run_ring_direct)
+            arms.append(dict(name="p2p_ring_stream3", kind="bfp", algo="ring", rings=R, transport="p2p", ring_sub=3))
             # layer 0's bucket as 4 row panels, each submitted right after its GEMM (the exchange of the last bucket,
             # which no backward is left to hide, starts a panel earlier; dp.py panels)
             arms.append(dict(name="rccl_mesh_panels4", kind="bfp", algo="mesh", transport="native", panels=4))
@@ -367,7 +371,8 @@ def main(argv=None):
             try:
                 setup = build(spec["name"], spec["kind"], algo=spec.get("algo", "mesh"), rings=spec.get("rings", 1),
                               transport=spec["transport"], gemm=spec.get("gemm", "persistent"),
-                              sdma=spec.get("sdma", False), panels=spec.get("panels", 0))
+                              sdma=spec.get("sdma", False), panels=spec.get("panels", 0),
+                              ring_sub=spec.get("ring_sub", 1))
                 rec.update(setup.info)
                 g = gate.allreduce_exactness(setup.engine, timeout_s=min(eng_timeout, 120.0))
                 rec["exact"] = g["exact"]

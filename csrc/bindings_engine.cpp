@@ -36,8 +36,9 @@ void register_engine(pybind11::module_& m) {
       .def("lose_round", &LoopbackComm::lose_round)
       .def_property_readonly("collectives", &LoopbackComm::collectives);
   pybind11::class_<P2PComm, Comm>(m, "P2PComm")
-      .def(pybind11::init<int, int, int, size_t>(), pybind11::arg("rank"), pybind11::arg("world"),
-           pybind11::arg("device"), pybind11::arg("slot_bytes") = (size_t)128 << 20)
+      .def(pybind11::init<int, int, int, size_t, int>(), pybind11::arg("rank"), pybind11::arg("world"),
+           pybind11::arg("device"), pybind11::arg("slot_bytes") = (size_t)128 << 20, pybind11::arg("depth") = 2)
+      .def_property_readonly("depth", &P2PComm::depth, "arena slots per sender")
       .def("handles", [](P2PComm& c) { return pybind11::bytes(c.handles()); })
       .def("connect",
            [](P2PComm& c, const std::vector<pybind11::bytes>& all) {
@@ -142,7 +143,7 @@ void register_engine(pybind11::module_& m) {
   py::class_<AllReduceEngine>(m, "AllReduceEngine")
       .def(py::init([](Comm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
                        bool compat, double timeout_s, int priority, bool force_comm, int device, int verify,
-                       int64_t chunk_elems, c10::optional<std::vector<std::vector<int>>> links) {
+                       int64_t chunk_elems, c10::optional<std::vector<std::vector<int>>> links, int ring_sub) {
              EngineConfig c;
              c.codec = codec;
              c.algo = algo;
@@ -154,6 +155,7 @@ void register_engine(pybind11::module_& m) {
              c.force_comm = force_comm;
              c.verify = verify;
              c.chunk_elems = chunk_elems;
+             c.ring_sub = ring_sub;
              if (links) {
                TORCH_CHECK((int)links->size() == world, "links: world x world expected");
                c.links.assign((size_t)world * world, 0);
@@ -167,13 +169,15 @@ void register_engine(pybind11::module_& m) {
            py::keep_alive<1, 2>(), py::arg("comm").none(true), py::arg("rank"), py::arg("world"), py::arg("codec"),
            py::arg("algo"), py::arg("rings"), py::arg("max_slice_elems"), py::arg("compat_owner_fp32"),
            py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"),
-           py::arg("verify") = -1, py::arg("chunk_elems") = 0, py::arg("links") = py::none())
+           py::arg("verify") = -1, py::arg("chunk_elems") = 0, py::arg("links") = py::none(), py::arg("ring_sub") = 0)
+      .def_property_readonly("ring_sub", &AllReduceEngine::ring_sub, "sub-slices per direct-ring hop message")
       .def("layout",
            [](AllReduceEngine& e, int64_t n, int64_t shard, int64_t chunks) {
              const EngineLayout L = e.layout(n, shard, chunks);
              return py::dict(py::arg("n") = L.n, py::arg("n_pad") = L.n_pad, py::arg("algo") = L.algo,
                              py::arg("shard") = L.shard, py::arg("slice") = L.slice, py::arg("blocks") = L.blocks,
-                             py::arg("rings") = L.rings, py::arg("part") = L.part, py::arg("chunks") = L.chunks);
+                             py::arg("rings") = L.rings, py::arg("part") = L.part, py::arg("chunks") = L.chunks,
+                             py::arg("sub") = L.sub);
            },
            py::arg("n"), py::arg("shard") = 0, py::arg("chunks") = 0)
       .def("wire_bytes", [](AllReduceEngine& e, int64_t n) { return e.wire_bytes(e.layout(n)); })
@@ -225,7 +229,8 @@ void register_engine(pybind11::module_& m) {
                TORCH_CHECK(e.prepack_shape(n_valid)[0] > 0, "this engine configuration cannot take prepacked input");
                const int64_t need = L.algo == 0
                                         ? L.chunks * e.world() * (int64_t)wire_shard_bytes(e.codec(), L.shard)
-                                        : (int64_t)L.rings * L.blocks * e.world() * (int64_t)wire_shard_bytes(e.codec(), L.slice);
+                                        : (int64_t)L.rings * L.blocks * e.world() * L.sub *
+                                              (int64_t)wire_shard_bytes(e.codec(), L.slice / L.sub);
                TORCH_CHECK(prepacked->scalar_type() == at::kByte && prepacked->numel() >= need,
                            "prepacked wire buffer too small");
                pre = prepacked->data_ptr<uint8_t>();

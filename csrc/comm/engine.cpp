@@ -38,6 +38,10 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     side_epi = cfg.side_epilogue >= 0 ? cfg.side_epilogue > 0 : (se && se[0] == '1');
     if (side_epi) FAN_HIP_CHECK(hipStreamCreateWithPriority(&epi_stream_, hipStreamNonBlocking, 0));
   }
+  if (cfg_.ring_sub <= 0) {
+    const char* rs = std::getenv("FAN_RING_SUB");
+    cfg_.ring_sub = rs ? std::max(1, std::atoi(rs)) : 1;
+  }
   if (cfg_.chunk_elems <= 0) {
     const char* ce = std::getenv("FAN_CHUNK_ELEMS");
     cfg_.chunk_elems = ce ? std::atoll(ce) : (int64_t(1) << 26);
@@ -161,13 +165,20 @@ EngineLayout AllReduceEngine::layout(int64_t n, int64_t shard, int64_t chunks) c
   }
   const int R = (int)orders_.size();
   const int64_t chunk = cdiv(std::max<int64_t>(n, 1), R);
-  const RingGeometry g = ring_geometry(chunk, N, cfg_.max_slice_elems);
+  L.sub = ring_sub();
+  const RingGeometry g = ring_geometry(chunk, N, cfg_.max_slice_elems, 256 * (int64_t)L.sub);
   L.rings = R;
   L.slice = g.slice_elems;
   L.blocks = g.blocks;
   L.part = g.n_pad;
   L.n_pad = g.n_pad * R;
   return L;
+}
+
+int AllReduceEngine::ring_sub() const {
+  P2PComm* d = comm_ ? comm_->direct() : nullptr;
+  if (cfg_.algo != 1 || d == nullptr || world_ < 2 || cfg_.compat_owner_fp32) return 1;
+  return std::max(1, std::min(cfg_.ring_sub, d->depth() - 1));
 }
 
 int64_t AllReduceEngine::wire_bytes(const EngineLayout& L) const {
@@ -216,9 +227,10 @@ std::array<int64_t, 3> AllReduceEngine::prepack_shape(int64_t n) const {
   if (cfg_.codec != kBfpTrunc && cfg_.codec != kBfpRne) return {0, 0, -1};
   const EngineLayout L = layout(n);
   const bool local = (world_ == 1 && !cfg_.force_comm) || comm_ == nullptr;
-  if (cfg_.algo == 1)  // ring: one shard per slice, ring-major; every local slice is also needed in f32 (each reduce
-                       // hop adds the local contribution), except at world 1 where the encoding is the result
-    return {L.slice, (int64_t)L.rings * L.blocks * world_, world_ == 1 ? -1 : kWireOwnAll};
+  if (cfg_.algo == 1)  // ring: one shard per slice (P sub-shards when the hops stream), ring-major; every local slice
+                       // is also needed in f32 (each reduce hop adds the local contribution), except at world 1 where
+                       // the encoding is the result
+    return {L.slice / L.sub, (int64_t)L.rings * L.blocks * world_ * L.sub, world_ == 1 ? -1 : kWireOwnAll};
   // chunked buckets: the owner shard of chunk c is wire shard c*N + rank (owner = shard index mod N)
   return {L.shard, world_ * L.chunks, local ? -1 : rank_};
 }
@@ -523,8 +535,9 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
   const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
   hipStream_t st = run_stream_;
   const bool compat = cfg_.compat_owner_fp32 && N > 1 && update;
-  if (prepacked)  // encode what the producer did not (bias gradient + padding): slice-sized shards, ring-major
-    launch_wire_pack_range(c, gdt, grad, const_cast<uint8_t*>(prepacked), (size_t)S, (size_t)prepacked_elems,
+  if (prepacked)  // encode what the producer did not (bias gradient + padding): slice-sized shards (sub-shards when
+                  // the direct ring streams its hops), ring-major
+    launch_wire_pack_range(c, gdt, grad, const_cast<uint8_t*>(prepacked), (size_t)(S / L.sub), (size_t)prepacked_elems,
                            (size_t)L.n_pad, st);
   if (P2PComm* d = comm_ ? comm_->direct() : nullptr; d && N > 1 && !compat)
     return run_ring_direct(d, L, grad, gdt, master, lp, mom, n_valid, p, update, out_sum, prepacked);
@@ -568,7 +581,8 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
   uint32_t round_id = 0;
   for (const auto& rnd : rounds) {
     RoctxRange rr("fan/ring/round");
-    if (N > 1) {  // no credit phase on a copying transport: points 0 and 1 coincide
+    if (N > 1) {  // no credit phase on a copying transport: points 0 and 1 coincide; then kernels, exchange
+      if (cur_trace_ >= 0) trace_pool_[cur_trace_].hop_kernel_first = true;
       hop_mark(0);
       hop_mark(1);
     }
@@ -661,24 +675,32 @@ std::vector<EpiThunk> AllReduceEngine::run_ring(const EngineLayout& L, const voi
 // BFP TX framing and onto the link, hw/all_reduce.sv:1155-1166, hw/bfp_adapter.sv:279-379); SEND_LOCAL encodes
 // (or, for a producer-encoded bucket, copies) the local slice straight into that slot; a FORWARD hop copies the
 // received full slice arena -> downstream arena, and every received full slice is copied once into the gathered
-// wire the epilogue reads (pure copies: P2PComm::move, CU kernel or copy engines). Per round: credit waits for the
-// downstream slots (P2PComm::begin_to), the kernels, ack of the previous round's upstream slots, ready flags
-// downstream, wait for upstream's. The schedule, sums and summation order are those of run_ring's copying rounds
-// (bit-identical; the compat owner-f32 mode uses that path). Verify mode tags message k of a round in the slot
-// trailer (tag k) after the round's kernels and checks every received message after the ready wait (site "ring
-// direct hop", row = round). Traced requests record four device timestamps per round (hop_mark): round start,
-// credits granted, kernels done, upstream data ready — the per-hop split of the NIC's stall_eth_in/out counters
-// (hw/all_reduce.sv:892-1085).
+// wire the epilogue reads (pure copies: P2PComm::move, CU kernel or copy engines). The schedule, sums and summation
+// order are those of run_ring's copying rounds (bit-identical; the compat owner-f32 mode uses that path).
+//
+// Streaming (L.sub = P > 1): every round's messages go out as P sub-slices (wire sub-shards of S/P elements), each
+// its own P2P sub-round with its own ready flag. Sub-slice s of round t only needs sub-slice s of the upstream's
+// round t-1, which landed P sub-rounds earlier, so the downstream starts reducing it while this rank still encodes
+// the rest — the NIC forwards each reduced beat through send_fifo the same way instead of storing a whole slice
+// (hw/all_reduce.sv:1155-1166, 1033-1061). A message is consumed P sub-rounds after it lands, so the arena keeps
+// P + 1 or more slots per sender (P2PComm depth). P = 1 is the lock-step ring. Per sub-round j: credit wait for the
+// downstream slots (begin_to), wait for the upstream messages of sub-round j - P (wait_from), the kernels / copies,
+// ack of those upstream messages, ready flags downstream.
+// Verify mode tags message k of a sub-round in its slot trailer (tag k) after the kernels and checks every message
+// before the kernels that read it (site "ring direct hop", row = the sub-round it was sent in). Traced requests
+// record four device timestamps per sub-round (hop_mark): start, credits granted, upstream data ready, kernels done.
 std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineLayout& L, const void* grad, int gdt,
                                                        float* master, bf16_t* lp, float* mom, int64_t n_valid,
                                                        SgdParams p, bool update, float* out_sum,
                                                        const uint8_t* prepacked) {
   const int N = world_, c = cfg_.codec;
-  const int64_t S = L.slice;
-  const size_t sb = wire_shard_bytes(c, S);
+  const int P = L.sub;
+  const int64_t S = L.slice, Sp = S / P;
+  const size_t sb = wire_shard_bytes(c, Sp);  // one message: one sub-shard
   const size_t msg = (sb + 255) / 256 * 256;  // message stride inside an arena slot (<= 2 messages per peer/round)
+  FAN_CHECK(S % (256 * (int64_t)P) == 0 && P <= d->depth() - 1, "p2p ring: bad sub-slice geometry");
   FAN_CHECK(2 * msg <= d->payload_bytes(), "p2p ring: two slices per round must fit an arena slot (lower max_slice_elems)");
-  const int64_t nsl = L.blocks * N;
+  const int64_t nsl = L.blocks * N, nsh = nsl * P;  // slices / wire (sub-)shards per ring part
   const uint8_t* g = reinterpret_cast<const uint8_t*>(grad);
   hipStream_t st = run_stream_;
   struct RS {
@@ -691,10 +713,11 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
     int64_t slice;
     bool full;
     const uint8_t* ptr;
+    const uint8_t* tag;
   };
   std::vector<RS> rings;
   std::vector<int> downs, ups;
-  const std::string k = std::to_string(sb) + "_" + std::to_string(nsl);
+  const std::string k = std::to_string(sb) + "_" + std::to_string(nsh);
   for (size_t i = 0; i < orders_.size(); ++i) {
     const auto& o = orders_[i];
     int pos = 0;
@@ -705,7 +728,7 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
     rs.down = o[(pos - 1 + N) % N];
     rs.up = o[(pos + 1) % N];
     rs.plan = ring_plan(N, pos, L.blocks);
-    rs.G = epi_scratch("ring_G" + std::to_string(i) + "_" + k, sb * nsl);
+    rs.G = epi_scratch("ring_G" + std::to_string(i) + "_" + k, sb * nsh);
     downs.push_back(rs.down);
     ups.push_back(rs.up);
     rings.push_back(rs);
@@ -716,103 +739,121 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
     if (!rounds.empty() && j > 0 && rings[0].plan[j].send_src == kSendLocal) rounds.back().push_back(j);
     else rounds.push_back({j});
   }
-  auto local = [&](const RS& rs, int64_t x) { return g + (size_t)(rs.off + x * S) * esize(gdt); };
-  std::vector<std::vector<Rx>> prev(rings.size());
-  P2PComm::Round prev_round{0};
-  bool have_prev = false;
+  // local f32 / bf16 elements of sub-slice s of slice x
+  auto local = [&](const RS& rs, int64_t x, int s) { return g + (size_t)(rs.off + x * S + (int64_t)s * Sp) * esize(gdt); };
+  auto gsub = [&](const RS& rs, int64_t x, int s) { return rs.G + (size_t)(x * P + s) * sb; };  // G sub-shard
+  std::vector<P2PComm::Round> sub_round(rounds.size() * P);  // P2P round of every sub-round (its sequence number)
+  // the upstream messages of sub-round jj: ready wait, fault hook, verify
+  auto arrive = [&](size_t jj, std::vector<std::vector<Rx>>& per_ring) {
+    d->wait_from(sub_round[jj], ups, st);
+    for (size_t i = 0; i < rings.size(); ++i)
+      for (Rx& x : per_ring[i]) {
+        fault_.maybe_corrupt("p2p_recv", const_cast<uint8_t*>(x.ptr), sb, st);  // test hook: changed after its flag
+        if (verify_) verify_direct(x.ptr, sb, x.tag, (uint32_t)sub_round[jj].seq, kSiteRingDirect, (uint32_t)jj, st);
+      }
+  };
   if (counters_.peer_bytes.size() != (size_t)world_) counters_.peer_bytes.assign(world_, 0);
-  uint32_t round_id = 0;
-  for (const auto& rnd : rounds) {
-    RoctxRange rr_("fan/ring/direct_round");
-    hop_mark(0);
-    const P2PComm::Round rr = d->begin_to(downs, st);
-    hop_mark(1);
-    std::vector<P2PCopy> copies;  // forwards (arena -> downstream arena) and received full slices -> G
-    struct Sent {
-      uint8_t* msg;
-      uint8_t* tag;
-    };
-    std::vector<Sent> sent;  // this round's messages, tagged after all of the round's kernels / copies
-    for (size_t i = 0; i < rings.size(); ++i) {
-      RS& rs = rings[i];
-      size_t kmsg = 0;
-      for (size_t j : rnd) {
-        const RingRound& row = rs.plan[j];
-        if (row.send_src == kSendNone) continue;
-        uint8_t* to = d->dst(rr, rs.down) + kmsg * msg;
-        sent.push_back({to, d->dst_tag(rr, rs.down, (int)kmsg)});
-        ++kmsg;
-        counters_.peer_bytes[rs.down] += (int64_t)sb;
-        d->count_sent(rs.down, sb);
-        if (row.send_src == kSendLocal) {
-          if (prepacked) {
-            copies.push_back({prepacked + ((size_t)i * nsl + row.send_slice) * sb, to, sb});
-          } else {
+  if (cur_trace_ >= 0) trace_pool_[cur_trace_].hop_kernel_first = false;  // points: credit, ready, kernels
+  // got[s][ring]: the messages sub-round (t - 1, s) delivered, consumed by (t, s)
+  std::vector<std::vector<std::vector<Rx>>> got(P, std::vector<std::vector<Rx>>(rings.size()));
+  for (size_t t = 0; t < rounds.size(); ++t) {
+    const auto& rnd = rounds[t];
+    for (int s = 0; s < P; ++s) {
+      RoctxRange rr_("fan/ring/direct_round");
+      const size_t j = t * P + s;
+      hop_mark(0);
+      const P2PComm::Round rr = d->begin_to(downs, st);
+      sub_round[j] = rr;
+      hop_mark(1);
+      std::vector<std::vector<Rx>>& prev = got[s];  // what sub-round (t - 1, s) delivered
+      if (t > 0) arrive(j - P, prev);
+      hop_mark(2);
+      std::vector<P2PCopy> copies;  // forwards (arena -> downstream arena) and received full sub-slices -> G
+      struct Sent {
+        uint8_t* msg;
+        uint8_t* tag;
+      };
+      std::vector<Sent> sent;  // this sub-round's messages, tagged after all of its kernels / copies
+      for (size_t i = 0; i < rings.size(); ++i) {
+        RS& rs = rings[i];
+        size_t kmsg = 0;
+        for (size_t jr : rnd) {
+          const RingRound& row = rs.plan[jr];
+          if (row.send_src == kSendNone) continue;
+          uint8_t* to = d->dst(rr, rs.down) + kmsg * msg;
+          sent.push_back({to, d->dst_tag(rr, rs.down, (int)kmsg)});
+          ++kmsg;
+          counters_.peer_bytes[rs.down] += (int64_t)sb;
+          d->count_sent(rs.down, sb);
+          if (row.send_src == kSendLocal) {
+            if (prepacked) {
+              copies.push_back({prepacked + ((size_t)i * nsh + (size_t)row.send_slice * P + s) * sb, to, sb});
+            } else {
+              WirePtrs w{};
+              w.p[0] = to;
+              launch_wire_pack_to(c, gdt, local(rs, row.send_slice, s), w, (size_t)Sp, 1, st);
+            }
+          } else if (row.send_src == kSendReduce) {
+            const Rx* part = nullptr;
+            for (const Rx& x : prev[i])
+              if (!x.full) part = &x;
+            FAN_CHECK(part != nullptr, "p2p ring: no upstream partial for a reduce hop");
             WirePtrs w{};
             w.p[0] = to;
-            launch_wire_pack_to(c, gdt, local(rs, row.send_slice), w, (size_t)S, 1, st);
+            int nd = 1;
+            if (row.owned >= 0) w.p[nd++] = gsub(rs, row.send_slice, s);  // this rank's fully reduced sub-slice
+            launch_wire_reduce_to(c, gdt, part->ptr, 0, 2, 1, local(rs, row.send_slice, s), w, nd, (size_t)Sp, st);
+          } else {  // kSendForward: the full sub-slice received last round goes on downstream
+            const Rx* full = nullptr;
+            for (const Rx& x : prev[i])
+              if (x.full && x.slice == row.send_slice) full = &x;
+            FAN_CHECK(full != nullptr, "p2p ring: forwarded slice not received");
+            copies.push_back({full->ptr, to, sb});
           }
-        } else if (row.send_src == kSendReduce) {
-          const Rx* part = nullptr;
-          for (const Rx& x : prev[i])
-            if (!x.full) part = &x;
-          FAN_CHECK(part != nullptr, "p2p ring: no upstream partial for a reduce hop");
-          WirePtrs w{};
-          w.p[0] = to;
-          int nd = 1;
-          if (row.owned >= 0) w.p[nd++] = rs.G + (size_t)row.send_slice * sb;  // this rank's fully reduced slice
-          launch_wire_reduce_to(c, gdt, part->ptr, 0, 2, 1, local(rs, row.send_slice), w, nd, (size_t)S, st);
-        } else {  // kSendForward: the full slice received last round goes on downstream
-          const Rx* full = nullptr;
-          for (const Rx& x : prev[i])
-            if (x.full && x.slice == row.send_slice) full = &x;
-          FAN_CHECK(full != nullptr, "p2p ring: forwarded slice not received");
-          copies.push_back({full->ptr, to, sb});
+        }
+        for (const Rx& x : prev[i])  // every received full sub-slice lands once in the gathered wire
+          if (x.full) copies.push_back({x.ptr, gsub(rs, x.slice, s), sb});
+      }
+      if (!copies.empty()) d->move(copies, st);
+      for (const Sent& m : sent) {
+        if (verify_) tag_direct(m.msg, sb, m.tag, (uint32_t)rr.seq, st);
+        fault_.maybe_corrupt("ring_send", m.msg, sb, st);  // in flight: after its tag
+      }
+      hop_mark(3);
+      if (t > 0) d->release_from(sub_round[j - P], ups, st);  // the messages of (t - 1, s) are consumed
+      d->publish_to(rr, downs, st);
+      // what this sub-round will deliver from upstream (read in (t + 1, s) or by the drain below)
+      for (size_t i = 0; i < rings.size(); ++i) {
+        prev[i].clear();
+        size_t kmsg = 0;
+        for (size_t jr : rnd) {
+          const RingRound& row = rings[i].plan[jr];
+          if (row.recv_slice < 0) continue;
+          prev[i].push_back({row.recv_slice, row.recv_full != 0, d->src(rr, rings[i].up) + kmsg * msg,
+                             d->src_tag(rr, rings[i].up, (int)kmsg)});
+          ++kmsg;
         }
       }
-      for (const Rx& x : prev[i])  // every received full slice lands once in the gathered wire
-        if (x.full) copies.push_back({x.ptr, rs.G + (size_t)x.slice * sb, sb});
+      counters_.direct_rounds++;
     }
-    if (!copies.empty()) d->move(copies, st);
-    for (const Sent& m : sent) {
-      if (verify_) tag_direct(m.msg, sb, m.tag, (uint32_t)rr.seq, st);
-      fault_.maybe_corrupt("ring_send", m.msg, sb, st);  // in flight: after its tag
-    }
-    hop_mark(2);
-    if (have_prev) d->release_from(prev_round, ups, st);  // the previous round's upstream slots are consumed
-    d->publish_to(rr, downs, st);
-    d->wait_from(rr, ups, st);
-    hop_mark(3);
-    for (size_t i = 0; i < rings.size(); ++i) {
-      prev[i].clear();
-      size_t kmsg = 0;
-      for (size_t j : rnd) {
-        const RingRound& row = rings[i].plan[j];
-        if (row.recv_slice < 0) continue;
-        uint8_t* m = const_cast<uint8_t*>(d->src(rr, rings[i].up)) + kmsg * msg;
-        fault_.maybe_corrupt("p2p_recv", m, sb, st);  // test hook: the slot changes after its flag was raised
-        if (verify_)
-          verify_direct(m, sb, d->src_tag(rr, rings[i].up, (int)kmsg), (uint32_t)rr.seq, kSiteRingDirect, round_id, st);
-        prev[i].push_back({row.recv_slice, row.recv_full != 0, m});
-        ++kmsg;
-      }
-    }
-    prev_round = rr;
-    have_prev = true;
-    counters_.direct_rounds++;
-    ++round_id;
   }
-  std::vector<P2PCopy> tail;
-  for (size_t i = 0; i < rings.size(); ++i)
-    for (const Rx& x : prev[i])
-      if (x.full) tail.push_back({x.ptr, rings[i].G + (size_t)x.slice * sb, sb});
-  if (!tail.empty()) d->move(tail, st);
-  if (have_prev) d->release_from(prev_round, ups, st);
+  // drain: the last round's P sub-rounds of messages (full slices of the all-gather's end) -> G, then ack
+  const size_t T = rounds.size();
+  for (int s = 0; s < P; ++s) {
+    const size_t jj = (T - 1) * P + s;
+    arrive(jj, got[s]);
+    std::vector<P2PCopy> tail;
+    for (size_t i = 0; i < rings.size(); ++i)
+      for (const Rx& x : got[s][i])
+        if (x.full) tail.push_back({x.ptr, gsub(rings[i], x.slice, s), sb});
+    if (!tail.empty()) d->move(tail, st);
+    d->release_from(sub_round[jj], ups, st);
+  }
   std::vector<EpiThunk> thunks;
   for (auto& rs : rings) {
     const int64_t off = rs.off, part = L.part;
     uint8_t* G = rs.G;
-    thunks.push_back([=](hipStream_t es) { epilogue(c, es, G, S, (int)nsl, off, part, master, lp, mom, n_valid, p, update, out_sum); });
+    thunks.push_back([=](hipStream_t es) { epilogue(c, es, G, Sp, (int)nsh, off, part, master, lp, mom, n_valid, p, update, out_sum); });
   }
   return thunks;
 }
@@ -962,8 +1003,8 @@ TraceSummary AllReduceEngine::trace_summary() {
       FAN_HIP_CHECK(hipEventElapsedTime(&c, e[2], e[3]));
       r.hop_rounds++;
       r.hop_credit_ms += a;
-      r.hop_kernel_ms += b;
-      r.hop_ready_ms += c;
+      r.hop_kernel_ms += t.hop_kernel_first ? b : c;
+      r.hop_ready_ms += t.hop_kernel_first ? c : b;
       r.hop_max_ms = std::max<double>(r.hop_max_ms, (double)a + b + c);
     }
   }

@@ -47,6 +47,11 @@ struct EngineConfig {
   // world 1 (inline, no communication phase): run each committed epilogue (decode + SGD) on an engine stream
   // beside the producer's next kernels instead of in the producer's stream order; -1: from FAN_SIDE_EPI
   int side_epilogue = -1;
+  // direct-P2P ring: each hop's message streams in this many sub-slices, each with its own ready flag, so the
+  // downstream rank reduces sub-slice s of round t as soon as it lands (the NIC's beat-level send_fifo pipeline,
+  // hw/all_reduce.sv:1155-1166) instead of after the whole slice; capped by the P2P arena depth - 1. 0: from
+  // FAN_RING_SUB (default 1: lock-step hops).
+  int ring_sub = 0;
 };
 
 struct EngineLayout {
@@ -58,6 +63,7 @@ struct EngineLayout {
   int64_t blocks = 0;       // ring
   int rings = 1;
   int64_t part = 0;         // ring: padded elements per ring part
+  int sub = 1;              // ring: sub-slices (wire sub-shards of slice / sub elements) per hop message
 };
 
 // Per-engine performance counters: the reference NIC's perf/debug registers re-expressed (hw/all_reduce.sv:92-98,
@@ -156,6 +162,7 @@ class AllReduceEngine {
   int rank() const { return rank_; }
   bool is_inline() const { return table_->config().inline_mode; }
   int codec() const { return cfg_.codec; }
+  int ring_sub() const;  // sub-slices per ring hop this engine runs (1 unless direct P2P ring streaming)
 
   // Enqueue the communication phase of a request. grad: padded flat buffer (f32 or bf16) ready on `producer`.
   // If `defer`, the weight update is enqueued later by commit(); otherwise immediately. Returns the slot.
@@ -236,6 +243,7 @@ class AllReduceEngine {
     hipEvent_t ev[kTpCount] = {};
     int64_t logical_bytes = 0, wire_bytes = 0;
     size_t hop_first = 0, hop_count = 0;  // ring rounds: 4 events each in hop_pool_
+    bool hop_kernel_first = false;         // point order: credit, kernels, ready (copying) or credit, ready, kernels
   };
   std::vector<hipEvent_t> hop_pool_;
   size_t hop_used_ = 0;

@@ -35,8 +35,9 @@ void device_identity(int device, char* host, size_t host_len, char* bus, size_t 
 
 }  // namespace
 
-P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
-    : rank_(rank), world_(world), device_(device), slot_((slot_bytes + 255) / 256 * 256) {
+P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes, int depth)
+    : rank_(rank), world_(world), device_(device), slot_((slot_bytes + 255) / 256 * 256), depth_(depth) {
+  FAN_CHECK(depth >= 2 && depth <= 16, "p2p: 2 <= depth <= 16 arena slots per sender");
   FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
   FAN_CHECK(slot_ > kTrailerBytes, "slot_bytes must exceed the 256-B verify trailer");
   if (const char* c = std::getenv("FAN_P2P_COPY")) sdma_ = !std::strcmp(c, "sdma");
@@ -50,13 +51,13 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
   const std::string mem = me ? me : "uncached";
   unsigned aflag = mem == "fine" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
   uncached_ = mem != "coarse" && mem != "fine" &&
-              hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * 2 * slot_, aflag) == hipSuccess;
+              hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * depth_ * slot_, aflag) == hipSuccess;
   if (!uncached_) {
     (void)hipGetLastError();
     if (mem == "fine") {
-      FAN_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * 2 * slot_, aflag));
+      FAN_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&arena_), (size_t)world * depth_ * slot_, aflag));
     } else {
-      FAN_HIP_CHECK(hipMalloc(&arena_, (size_t)world * 2 * slot_));
+      FAN_HIP_CHECK(hipMalloc(&arena_, (size_t)world * depth_ * slot_));
     }
   }
   arena_mem_ = uncached_ ? "uncached" : mem == "fine" ? "fine" : "coarse";
@@ -76,8 +77,7 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes)
   opened_.assign(world, false);
   peer_arena_[rank] = arena_;
   peer_flags_[rank] = flags_;
-  last_sent_[0].assign(world, 0);
-  last_sent_[1].assign(world, 0);
+  last_sent_.assign(depth_, std::vector<uint64_t>(world, 0));
   bytes_to_peer_.assign(world, 0);
   FAN_HIP_CHECK(hipEventCreateWithFlags(&rel_ev_, hipEventDisableTiming | hipEventReleaseToSystem));
 }
@@ -259,7 +259,7 @@ void P2PComm::connect_local(const std::vector<P2PComm*>& ranks) {
 void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>& recvs, hipStream_t s) {
   FAN_CHECK(!aborted_, "p2p transport aborted");
   const uint64_t q = ++seq_;
-  const int par = (int)(q & 1);
+  const int par = (int)(q % depth_);
   // sends: per destination, in issue order, packed back to back into this rank's slot of the peer's arena.
   // WAR first (the receiver drained what we last put into this parity slot), then ONE copy launch for all
   // destinations (every link busy at once), then one ready flag per destination.
@@ -316,7 +316,7 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
 P2PComm::Round P2PComm::begin(hipStream_t s) {
   FAN_CHECK(!aborted_, "p2p transport aborted");
   Round r{++seq_};
-  const int par = (int)(r.seq & 1);
+  const int par = (int)(r.seq % depth_);
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
     FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
@@ -327,7 +327,7 @@ P2PComm::Round P2PComm::begin(hipStream_t s) {
 }
 
 void P2PComm::publish(const Round& r, hipStream_t s) {
-  const int par = (int)(r.seq & 1);
+  const int par = (int)(r.seq % depth_);
   release_before_flags(s);
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
@@ -349,7 +349,7 @@ void P2PComm::release(const Round& r, hipStream_t s) {
 P2PComm::Round P2PComm::begin_to(const std::vector<int>& to, hipStream_t s) {
   FAN_CHECK(!aborted_, "p2p transport aborted");
   Round r{++seq_};
-  const int par = (int)(r.seq & 1);
+  const int par = (int)(r.seq % depth_);
   for (int p : to) {
     FAN_CHECK(p != rank_ && p >= 0 && p < world_ && peer_arena_[p] != nullptr, "p2p: bad or unconnected peer");
     const uint64_t prev = last_sent_[par][p];
@@ -359,7 +359,7 @@ P2PComm::Round P2PComm::begin_to(const std::vector<int>& to, hipStream_t s) {
 }
 
 void P2PComm::publish_to(const Round& r, const std::vector<int>& to, hipStream_t s) {
-  const int par = (int)(r.seq & 1);
+  const int par = (int)(r.seq % depth_);
   release_before_flags(s);
   for (int p : to) {
     FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, r.seq, 0));

@@ -7,8 +7,10 @@
 // command-processor wait, so no CU spins and nothing can deadlock on occupancy — copies the payload out
 // and acknowledges into the sender's flag block, which frees that arena slot for reuse.
 //
-// Arena: world x 2 slots of slot_bytes (double-buffered by sequence parity per sender), so a sender only
-// stalls when it is two messages ahead of a receiver. Flags: ready[world] + ack[world] (uint64 each).
+// Arena: world x depth slots of slot_bytes (a ring of `depth` slots per sender, indexed by sequence mod depth; depth 2
+// = double-buffered by parity), so a sender only stalls when it is `depth` messages ahead of a receiver — a ring hop
+// streamed in P sub-slices consumes each message P sub-rounds after it lands and needs depth >= P + 1.
+// Flags: ready[world] + ack[world] (uint64 each, monotone sequence numbers).
 // Reference analogue: the NIC's Ethernet link + credit flow control (hw/all_reduce.sv:468-483) and the
 // done-flag writes (hw/all_reduce.sv:1368-1375); here sequence numbers play the role of both.
 //
@@ -60,12 +62,13 @@ void launch_multi_copy(const std::vector<P2PCopy>& segs, hipStream_t stream);
 
 class P2PComm : public Comm {
  public:
-  P2PComm(int rank, int world, int device, size_t slot_bytes);
+  P2PComm(int rank, int world, int device, size_t slot_bytes, int depth = 2);
   ~P2PComm() override;
   static constexpr size_t kTrailerBytes = 256;  // per slot: 16 verify tags of 16 B
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   size_t slot_bytes() const { return slot_; }
+  int depth() const { return depth_; }
   size_t payload_bytes() const { return slot_ - kTrailerBytes; }  // what the messages of one slot may use
 
   // IPC bootstrap: this rank's (arena, flags) handles as bytes; connect() with every rank's bytes (in rank
@@ -95,8 +98,8 @@ class P2PComm : public Comm {
   uint8_t* dst(const Round& r, int peer) const { return slot_ptr(peer_arena_[peer], rank_, r.seq); }
   void publish(const Round& r, hipStream_t s);
   void wait(const Round& r, hipStream_t s);
-  const uint8_t* src_base(const Round& r) const { return arena_ + (r.seq & 1) * slot_; }
-  size_t src_stride() const { return 2 * slot_; }
+  const uint8_t* src_base(const Round& r) const { return arena_ + (r.seq % depth_) * slot_; }
+  size_t src_stride() const { return (size_t)depth_ * slot_; }
   void release(const Round& r, hipStream_t s);
   // The same round protocol restricted to a peer subset (ring rounds: send to the downstream neighbours, receive
   // from the upstream ones). Every rank must start the same number of rounds (begin / begin_to) in the same order.
@@ -131,7 +134,7 @@ class P2PComm : public Comm {
   bool uncached() const { return uncached_; }
   const std::string& arena_memory() const { return arena_mem_; }
   uint8_t* arena() const { return arena_; }
-  size_t arena_bytes() const { return (size_t)world_ * 2 * slot_; }
+  size_t arena_bytes() const { return (size_t)world_ * depth_ * slot_; }
 
   // Device-side stall counters (the NIC's stall_* / credit registers, hw/all_reduce.sv:892-1085, 468-483): every
   // flag wait the command processor parks a stream on, split into ready waits (data from a peer) and credit waits
@@ -155,15 +158,18 @@ class P2PComm : public Comm {
 
  private:
   void copy(const std::vector<P2PCopy>& segs, hipStream_t s);
-  uint8_t* slot_ptr(uint8_t* arena, int src, uint64_t seq) const { return arena + ((size_t)src * 2 + (seq & 1)) * slot_; }
+  uint8_t* slot_ptr(uint8_t* arena, int src, uint64_t seq) const {
+    return arena + ((size_t)src * depth_ + seq % depth_) * slot_;
+  }
   int rank_, world_, device_;
   size_t slot_;
+  int depth_;
   uint8_t* arena_ = nullptr;   // local receive arena
   uint64_t* flags_ = nullptr;  // local flags: [0, world) ready-from-src, [world, 2 world) ack-from-dst
   std::vector<uint8_t*> peer_arena_;
   std::vector<uint64_t*> peer_flags_;
   std::vector<bool> opened_;   // peer mapping opened through IPC (to be closed)
-  std::vector<uint64_t> last_sent_[2];  // per parity: sequence of the last message sent to each peer
+  std::vector<std::vector<uint64_t>> last_sent_;  // per slot index (seq % depth): last sequence sent to each peer
   uint64_t seq_ = 0;
   bool aborted_ = false;
   // stall accounting

@@ -9,15 +9,16 @@ namespace fan {
 
 static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-RingGeometry ring_geometry(int64_t n, int world, int64_t max_slice_elems) {
+RingGeometry ring_geometry(int64_t n, int world, int64_t max_slice_elems, int64_t granule) {
   if (world < 1) throw std::invalid_argument("world must be >= 1");
-  if (max_slice_elems < 256) max_slice_elems = 256;
-  max_slice_elems = max_slice_elems / 256 * 256;
+  if (granule < 256 || granule % 256) throw std::invalid_argument("granule must be a multiple of 256");
+  if (max_slice_elems < granule) max_slice_elems = granule;
+  max_slice_elems = max_slice_elems / granule * granule;
   RingGeometry g;
   g.n = n;
   const int64_t nn = std::max<int64_t>(n, 1);
   g.blocks = cdiv(nn, (int64_t)world * max_slice_elems);
-  g.slice_elems = cdiv(cdiv(nn, (int64_t)world * g.blocks), 256) * 256;
+  g.slice_elems = cdiv(cdiv(nn, (int64_t)world * g.blocks), granule) * granule;
   g.n_pad = g.blocks * world * g.slice_elems;
   return g;
 }

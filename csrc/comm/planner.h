@@ -31,12 +31,13 @@ struct RingRound {
 
 struct RingGeometry {
   int64_t n;            // valid elements
-  int64_t slice_elems;  // S (multiple of 256)
+  int64_t slice_elems;  // S (multiple of the granule, 256 by default)
   int64_t blocks;       // B
   int64_t n_pad;        // B * N * S
 };
 
-RingGeometry ring_geometry(int64_t n, int world, int64_t max_slice_elems);
+// granule: the slice is a multiple of it (256: one wire shard; 256 * P: P sub-shards for a streamed ring hop)
+RingGeometry ring_geometry(int64_t n, int world, int64_t max_slice_elems, int64_t granule = 256);
 std::vector<RingRound> ring_plan(int world, int position, int64_t blocks);
 
 // Arc-disjoint directed Hamiltonian cycles of the link digraph on `world` vertices (up to world-1 rings; fewer

@@ -124,6 +124,7 @@ class BucketLayout:
     rings: int = 1
     part: int = 0           # ring: padded elements per ring part
     chunks: int = 1         # mesh (C++ engine): chunks of `world` shards streamed through the collectives
+    sub: int = 1            # ring (C++ engine, direct P2P): sub-slices per hop message (streamed hops)
 
     @property
     def key(self):

@@ -54,7 +54,7 @@ class RcclAllReduce(CompressedAllReduce):
 def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str = "rne", algo: str = "mesh",
                 rings: int = 1, max_slice_elems: int = 1 << 22, compat_owner_fp32: bool = False,
                 timeout_s: float = 600.0, force_comm: bool = False, impl: str = "python", comm=None,
-                side_stream: bool = False):
+                side_stream: bool = False, ring_sub: int = 0):
     """kind: 'bfp' (compressed engine), 'raw' (engine, uncompressed fp32 wire), 'rccl' (baseline),
     'local' (no communication: world 1). impl: 'python' (request path issued from Python over any
     transport) or 'native' (C++ engine over its own RCCL communicator, or over ``comm``, e.g. the direct P2P
@@ -69,7 +69,7 @@ def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str
 
         return NativeAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
                                compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm,
-                               comm=comm, side_stream=side_stream)
+                               comm=comm, side_stream=side_stream, ring_sub=ring_sub)
     return CompressedAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
                                compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm)
 

@@ -104,7 +104,7 @@ class NativeAllReduce:
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
                  timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None,
                  side_stream: bool = False, verify: bool | None = None, fault: str | None = None,
-                 chunk_elems: int = 0, links="auto"):
+                 chunk_elems: int = 0, links="auto", ring_sub: int = 0):
         """``comm``: an explicit ``_C.Comm`` (e.g. ``_C.LoopbackFabric(N).comm(r)`` for virtual ranks on one
         GPU); otherwise the engine's own RCCL communicator is created from ``transport``. ``side_stream``
         (world 1): run requests on the engine's comm stream instead of inline (overlap measurements).
@@ -114,7 +114,10 @@ class NativeAllReduce:
         stream through the collectives in chunks — all-to-all / owner reduce / all-gather / epilogue pipelined over
         two streams with scratch bounded by two chunks (0: env FAN_CHUNK_ELEMS, default 64 Mi elements).
         ``links`` (ring): direct-link matrix the rings must follow (``"auto"``: this node's xGMI links from
-        :func:`~fpga_ai_nic_amd.utils.topology.link_matrix`; None: fully connected)."""
+        :func:`~fpga_ai_nic_amd.utils.topology.link_matrix`; None: fully connected). ``ring_sub`` (direct-P2P ring):
+        each hop's message streams in this many sub-slices with a ready flag each, so the downstream rank starts on
+        sub-slice s while this one still encodes the rest (0: env FAN_RING_SUB, default 1 = lock-step hops; capped at
+        the P2P arena depth - 1)."""
         if algo not in _ALGOS:
             raise ValueError(f"unknown algo {algo!r}")
         C = _ext.require()
@@ -145,7 +148,8 @@ class NativeAllReduce:
         self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
                                    compat_owner_fp32, timeout_s, stream_priority, force_comm or side_stream,
                                    self.device.index, -1 if verify is None else int(bool(verify)), int(chunk_elems),
-                                   links)
+                                   links, int(ring_sub))
+        self.ring_sub = int(self.C.ring_sub)
         if fault is not None:
             self.C.set_fault(fault)
         self.verify = bool(self.C.verify)
@@ -194,7 +198,7 @@ class NativeAllReduce:
         d = self.C.layout(int(n), int(shard), int(chunks))
         return BucketLayout(n=d["n"], n_pad=d["n_pad"], algo=self.algo, world=self.world, shard=d["shard"],
                             slice_elems=d["slice"], blocks=d["blocks"], rings=d["rings"], part=d["part"],
-                            chunks=d["chunks"])
+                            chunks=d["chunks"], sub=d["sub"])
 
     def wire_bytes(self, L: BucketLayout) -> int:
         return int(self.C.wire_bytes(L.n))

@@ -205,15 +205,16 @@ def make_p2p_comm(rank: int | None = None, world: int | None = None, device: int
     return comm
 
 
-def try_p2p_comm(slot_bytes: int = 128 << 20):
+def try_p2p_comm(slot_bytes: int = 128 << 20, depth: int = 4):
     """:func:`make_p2p_comm` that every rank of the default group either gets or, if ANY rank failed (no IPC, no
     peer access, allocation refused), all ranks get None together — a collective that cannot leave one rank waiting
-    in a later exchange. Returns (comm or None, error text of the first failing rank or None)."""
+    in a later exchange. ``depth``: arena slots per sender (a ring hop streamed in P sub-slices needs P + 1).
+    Returns (comm or None, error text of the first failing rank or None)."""
     C = _ext.require()
     rank, world = dist.get_rank(), dist.get_world_size()
     comm, err = None, None
     try:
-        comm = C.P2PComm(rank, world, torch.cuda.current_device(), slot_bytes)
+        comm = C.P2PComm(rank, world, torch.cuda.current_device(), slot_bytes, depth)
         blob = comm.handles()
     except Exception as e:  # noqa: BLE001 - reported, and every rank drops the transport
         comm, blob, err = None, None, f"rank {rank}: {e}"

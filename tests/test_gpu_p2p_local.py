@@ -34,7 +34,8 @@ pytestmark = pytest.mark.gpu
 
 def _run(world, algo, rings, m=40000, max_slice=2048, mode="plain"):
     C = _ext.require()
-    comms = [C.P2PComm(r, world, 0, 2 << 20) for r in range(world)]
+    stream = mode.startswith("stream")
+    comms = [C.P2PComm(r, world, 0, 2 << 20, 4 if stream else 2) for r in range(world)]
     C.P2PComm.connect_local(comms)
     if mode == "sdma":
         for c in comms:
@@ -42,10 +43,13 @@ def _run(world, algo, rings, m=40000, max_slice=2048, mode="plain"):
     rng = np.random.default_rng(100 + world)
     grads = [rng.standard_normal(m).astype(np.float32) for _ in range(world)]
     res, errs = [None] * world, [None] * world
-    verify = mode in ("verify", "fault")
+    verify = mode in ("verify", "fault", "stream_verify")
     fault = "p2p_recv:0:flip" if mode == "fault" else None
     engines = [NativeAllReduce(None, codec="bfp_rne", algo=algo, rings=rings, max_slice_elems=max_slice,
-                               comm=comms[r], verify=verify, fault=fault) for r in range(world)]
+                               comm=comms[r], verify=verify, fault=fault, ring_sub=3 if stream else 1)
+               for r in range(world)]
+    if stream:
+        assert all(e.ring_sub == 3 for e in engines) and engines[0].layout(m).sub == 3
 
     def run(r):
         try:
@@ -104,7 +108,7 @@ def _check(world, algo, rings, mode="plain"):
     out = {"ok": True, "why": [], "rings": len(res[0][4])}
     for r in range(world):
         o, o_p, _, direct, orders, verified = res[r]
-        if mode == "verify" and verified <= 0:
+        if mode in ("verify", "stream_verify") and verified <= 0:
             out["why"].append(f"rank {r}: verify mode checked no message")
         if not np.array_equal(o[:m], ref[:m]):
             out["why"].append(f"rank {r}: {algo} x{rings} differs from the simulator")
@@ -146,6 +150,13 @@ def test_direct_p2p_verify_and_sdma_bit_exact(world, algo, rings, mode):
     """verify mode runs the direct paths (no copying fallback) and checks every message; the copy-engine path moves
     the same bytes."""
     _child(world, algo, rings, mode)
+
+
+@pytest.mark.parametrize("world,rings,mode", [(3, 2, "stream"), (8, 7, "stream"), (4, 3, "stream_verify")])
+def test_direct_ring_streamed_hops_bit_exact(world, rings, mode):
+    """Each hop's message in 3 sub-slices with a ready flag each (4-slot arenas): the sums, summation order and
+    results are the lock-step ring's, bit for bit, from f32 and from prepacked input (sub-shard wire layout)."""
+    _child(world, "ring", rings, mode)
 
 
 @pytest.mark.parametrize("algo,rings", [("mesh", 1), ("ring", 2)])

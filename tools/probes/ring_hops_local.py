@@ -23,12 +23,12 @@ from fpga_ai_nic_amd import _ext  # noqa: E402
 from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce  # noqa: E402
 
 
-def run(world, algo, rings, n, iters, max_slice, prepacked):
+def run(world, algo, rings, sub, n, iters, max_slice, prepacked):
     C = _ext.require()
-    comms = [C.P2PComm(r, world, 0, 128 << 20) for r in range(world)]
+    comms = [C.P2PComm(r, world, 0, 64 << 20, max(2, sub + 1)) for r in range(world)]
     C.P2PComm.connect_local(comms)
     engines = [NativeAllReduce(None, codec="bfp_rne", algo=algo, rings=rings, max_slice_elems=max_slice,
-                               comm=comms[r]) for r in range(world)]
+                               comm=comms[r], ring_sub=sub) for r in range(world)]
     out, errs = [None] * world, [None] * world
     bar = threading.Barrier(world)
 
@@ -75,7 +75,8 @@ def run(world, algo, rings, n, iters, max_slice, prepacked):
         raise RuntimeError(str(errs))
     wall = max(o[0] for o in out)
     tr = out[0][1]
-    rec = {"probe": "ring_hops_local", "world": world, "algo": algo, "rings": out[0][2], "size_MB_f32": n * 4 / 2**20,
+    rec = {"probe": "ring_hops_local", "world": world, "algo": algo, "rings": out[0][2], "sub": sub,
+           "size_MB_f32": n * 4 / 2**20,
            "input": "prepacked" if prepacked else "f32", "iters": iters, "us_per_request": round(wall / iters * 1e6, 1),
            "comm_us_per_request": round(tr["comm_ms"] * 1e3 / max(1, tr["requests"]), 1)}
     if tr.get("hop_rounds"):
@@ -97,13 +98,14 @@ def main():
     ap.add_argument("--size-mb", type=float, default=64)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--max-slice", type=int, default=1 << 22)
-    ap.add_argument("--arms", default="ring:1,ring:7,mesh:1")
+    ap.add_argument("--arms", default="ring:1,ring:7,ring:7:3,mesh:1", help="algo:rings[:sub-slices per hop]")
     ap.add_argument("--prepacked", action="store_true")
     a = ap.parse_args()
     n = int(a.size_mb * (1 << 20)) // 4 // 16 * 16
     for arm in a.arms.split(","):
-        algo, rings = arm.split(":")
-        print(json.dumps(run(a.world, algo, int(rings), n, a.iters, a.max_slice, a.prepacked)), flush=True)
+        f = arm.split(":")
+        algo, rings, sub = f[0], int(f[1]), int(f[2]) if len(f) > 2 else 1
+        print(json.dumps(run(a.world, algo, rings, sub, n, a.iters, a.max_slice, a.prepacked)), flush=True)
 
 
 if __name__ == "__main__":
