@@ -2,8 +2,14 @@
 """Summarise rocprofv3 --pmc counter_collection CSVs per kernel (mean over dispatches).
 
 Usage: python tools/pmc_summary.py gpurun_out/pmc1/p_counter_collection.csv [more.csv ...] [--filter gemm]
-Derived: effective clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel time; meaningless below ~0.3 ms), MFMA busy share,
+Derived: effective clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel time; reads high below ~0.3 ms), MFMA busy share,
 L2 hit rate, FETCH/WRITE bandwidth (GB/s over the dispatch; counters from separate passes are averaged per kernel).
+
+MFMA utilisation without the saturating SQ_VALU_MFMA_BUSY_CYCLES (it wraps at 2^28 on a 200 µs GEMM summed over
+1024 SIMDs): SQ_INSTS_MFMA (MFMA instructions issued, summed over SEs) x 16 cycles per v_mfma_f32_16x16x32_bf16 on
+one SIMD / (kernel cycles x 1024 SIMDs), kernel cycles = GRBM_GUI_ACTIVE / 8; achieved TFLOP/s from
+SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 / kernel time, and its share of the 2.5 PF dense bf16 peak. ``--table`` prints one
+line per kernel shape instead (sorted by total time).
 """
 import argparse
 import collections
@@ -14,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv", nargs="+")
     ap.add_argument("--filter", default="")
+    ap.add_argument("--table", action="store_true", help="one line per kernel shape: MFMA utilisation table")
+    ap.add_argument("--mfma-cycles", type=float, default=16.0, help="SIMD cycles per MFMA instruction (16x16x32 bf16)")
     a = ap.parse_args()
     agg = collections.OrderedDict()
     for f in a.csv:
@@ -28,6 +36,22 @@ def main():
             d[c][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])  # per pass: dispatch ids restart
             d["_meta"] = (r["VGPR_Count"], r["Accum_VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"])
             d.setdefault("_t", {})[(f, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    if a.table:
+        rows = []
+        for (name, grid), d in agg.items():
+            m = {c: sum(v.values()) / len(v) for c, v in d.items() if not c.startswith("_")}
+            t_ns = sum(d["_t"].values()) / len(d["_t"])
+            n = len(d["_t"])
+            cyc = m.get("GRBM_GUI_ACTIVE", 0.0) / 8
+            busy = m["SQ_INSTS_MFMA"] * a.mfma_cycles / (cyc * 1024) if cyc and "SQ_INSTS_MFMA" in m else None
+            fl = m.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512
+            rows.append((t_ns * n, name, grid, n, t_ns, cyc / t_ns if cyc else None, busy, fl / t_ns / 1e3 if fl else None))
+        rows.sort(key=lambda r: -r[0])
+        print(f"{'kernel':60s} {'grid':>8s} {'n':>4s} {'us':>8s} {'GHz':>6s} {'mfma_busy%':>10s} {'TFLOP/s':>8s} {'%2.5PF':>7s}")
+        for tot, name, grid, n, t_ns, ghz, busy, tf in rows:
+            print(f"{name[:60]:60s} {grid:>8s} {n:4d} {t_ns / 1e3:8.1f} {ghz or 0:6.2f} "
+                  f"{(busy or 0) * 100:10.1f} {tf or 0:8.1f} {(tf or 0) / 25:7.1f}")
+        return
     for (name, grid), d in agg.items():
         m = {c: sum(v.values()) / len(v) for c, v in d.items() if not c.startswith("_")}
         t_ns = sum(d["_t"].values()) / len(d["_t"])
