@@ -91,13 +91,15 @@ def main():
         torch.cuda.synchronize()
         return D.max_over_ranks(time.perf_counter() - t0)
 
-    run(True, True)
-    res = {"compute": [], "comm": [], "overlap": []}
     kinds = {"compute": (True, False), "comm": (False, True), "overlap": (True, True)}
+    run(*kinds[a.only or "overlap"])  # warmup (GEMM plan tuning, engine scratch): in --only mode of that kind only
+    res = {"compute": [], "comm": [], "overlap": []}
     for _ in range(a.rounds):
         for k, (dc, dm) in kinds.items():
             if not a.only or a.only == k:
                 res[k].append(run(dc, dm))
+                if a.only:  # a clear idle gap between rounds, so a trace can be cut into them
+                    time.sleep(0.01)
     if a.only:
         for k in res:
             res[k] = res[k] or [0.0]
@@ -110,8 +112,9 @@ def main():
             "engine": a.engine,
             "algo": a.algo, "params": bert.num_params(a.layers), "t_compute_ms": round(tc, 3),
             "t_comm_ms": round(tm, 3), "t_overlap_ms": round(to, 3), "overlap_efficiency": round(eff, 3),
-            "bwd_gemm_tflops": round(flops / (tc / 1e3) / 1e12, 1),
-            "comm_algo_bw_GBps": round(bert.num_params(a.layers) * 4 / (tm / 1e3) / 1e9, 1)}), flush=True)
+            "bwd_gemm_tflops": round(flops / (tc / 1e3) / 1e12, 1) if tc > 0 else None,
+            "comm_algo_bw_GBps": round(bert.num_params(a.layers) * 4 / (tm / 1e3) / 1e9, 1) if tm > 0 else None,
+            "only": a.only or None}), flush=True)
     D.cleanup()
 
 

@@ -12,4 +12,5 @@ for k in compute comm overlap; do
 done
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc1 -o p --output-format csv -- python3 bench.py --steps 5 --warmup 2 --ref-mb 0 --extra-budget 0 > $O/pmc1.log 2>&1; echo pmc_rc=$?
 f=$(find $O/pmc1 -name '*counter_collection.csv' | head -1); [ -n "$f" ] && python tools/pmc_summary.py "$f" --table > $O/mfma_table.txt 2>&1; head -30 $O/mfma_table.txt
+python tools/overlap_attrib.py $(find $O/prof_compute -name '*kernel_trace.csv' | head -1) $(find $O/prof_comm -name '*kernel_trace.csv' | head -1) $(find $O/prof_overlap -name '*kernel_trace.csv' | head -1) > $O/overlap_attrib.txt 2>&1; head -40 $O/overlap_attrib.txt
 echo done

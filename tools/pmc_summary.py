@@ -14,6 +14,7 @@ line per kernel shape instead (sorted by total time).
 import argparse
 import collections
 import csv
+import statistics
 
 
 def main():
@@ -37,19 +38,35 @@ def main():
             d["_meta"] = (r["VGPR_Count"], r["Accum_VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"])
             d.setdefault("_t", {})[(f, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     if a.table:
+        # per dispatch, then grouped by (kernel, grid, MFMA FLOPs): a persistent GEMM launches the same grid for every
+        # shape, so the FLOP count (SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512) is what tells its shapes apart
+        per = collections.defaultdict(dict)
+        for f in a.csv:
+            for r in csv.DictReader(open(f)):
+                if a.filter and a.filter not in r["Kernel_Name"]:
+                    continue
+                k = (f, r["Dispatch_Id"])
+                d = per[k]
+                d["name"], d["grid"] = r["Kernel_Name"], r["Grid_Size"]
+                d["t"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        groups = collections.defaultdict(list)
+        for d in per.values():
+            fl = d.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512
+            groups[(d["name"], d["grid"], float(f"{fl:.3g}"))].append(d)
         rows = []
-        for (name, grid), d in agg.items():
-            m = {c: sum(v.values()) / len(v) for c, v in d.items() if not c.startswith("_")}
-            t_ns = sum(d["_t"].values()) / len(d["_t"])
-            n = len(d["_t"])
-            cyc = m.get("GRBM_GUI_ACTIVE", 0.0) / 8
-            busy = m["SQ_INSTS_MFMA"] * a.mfma_cycles / (cyc * 1024) if cyc and "SQ_INSTS_MFMA" in m else None
-            fl = m.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512
-            rows.append((t_ns * n, name, grid, n, t_ns, cyc / t_ns if cyc else None, busy, fl / t_ns / 1e3 if fl else None))
+        for (name, grid, fl), ds in groups.items():
+            t_ns = statistics.mean(d["t"] for d in ds)
+            cyc = statistics.mean(d.get("GRBM_GUI_ACTIVE", 0.0) for d in ds) / 8
+            mf = statistics.mean(d.get("SQ_INSTS_MFMA", 0.0) for d in ds)
+            busy = mf * a.mfma_cycles / (cyc * 1024) if cyc and mf else None
+            rows.append((t_ns * len(ds), name, grid, len(ds), t_ns, cyc / t_ns if cyc else None, busy,
+                         fl / t_ns / 1e3 if fl else None, fl))
         rows.sort(key=lambda r: -r[0])
-        print(f"{'kernel':60s} {'grid':>8s} {'n':>4s} {'us':>8s} {'GHz':>6s} {'mfma_busy%':>10s} {'TFLOP/s':>8s} {'%2.5PF':>7s}")
-        for tot, name, grid, n, t_ns, ghz, busy, tf in rows:
-            print(f"{name[:60]:60s} {grid:>8s} {n:4d} {t_ns / 1e3:8.1f} {ghz or 0:6.2f} "
+        print(f"{'kernel':58s} {'GFLOP':>7s} {'n':>4s} {'us':>8s} {'GHz':>5s} {'mfma_busy%':>10s} {'TFLOP/s':>8s} "
+              f"{'%2.5PF':>7s}")
+        for tot, name, grid, n, t_ns, ghz, busy, tf, fl in rows:
+            print(f"{name[:58]:58s} {fl / 1e9:7.1f} {n:4d} {t_ns / 1e3:8.1f} {ghz or 0:5.2f} "
                   f"{(busy or 0) * 100:10.1f} {tf or 0:8.1f} {(tf or 0) / 25:7.1f}")
         return
     for (name, grid), d in agg.items():
