@@ -221,7 +221,7 @@ def main(argv=None):
         return ctx["p2p"]
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
-              force=False, panels=None, ring_sub=1):
+              force=False, panels=None, ring_sub=1, epi=None):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default)."""
         comm = None
@@ -242,7 +242,7 @@ def main(argv=None):
                           impl=eimpl, comm=comm, side_stream=a.side_stream and not multi, timeout_s=eng_timeout,
                           **({"ring_sub": ring_sub} if eimpl == "native" else {}))
         if hasattr(eng, "epilogue_on_producer") and not getattr(eng, "inline", True):
-            eng.epilogue_on_producer = a.epi == "producer"
+            eng.epilogue_on_producer = (epi or a.epi) == "producer"
         pad_fn = (lambda n: eng.layout(n).n_pad) if eng is not None else None
         model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
         if world > 1:
@@ -254,7 +254,9 @@ def main(argv=None):
                 "transport": (getattr(t, "name", transport) if comm is None else "p2p") if multi or force else "none",
                 "gemm_inflight": tr.gemm_inflight, "copy": ("sdma" if sdma else "kernel") if comm is not None else None,
                 "panels": tr.panel_plans[0]["chunks"] if tr.panel_plans else 0,
-                "ring_sub": int(getattr(eng, "ring_sub", 1)) if algo == "ring" else None}
+                "ring_sub": int(getattr(eng, "ring_sub", 1)) if algo == "ring" else None,
+                "epilogue_stream": ("compute" if getattr(eng, "epilogue_on_producer", False) else "comm")
+                if eng is not None and not getattr(eng, "inline", True) else "inline"}
         return Setup(name, eng, model, tr, info)
 
     def release(setup):
@@ -359,6 +361,10 @@ def main(argv=None):
             # which no backward is left to hide, starts a panel earlier; dp.py panels)
             arms.append(dict(name="rccl_mesh_panels4", kind="bfp", algo="mesh", transport="native", panels=4))
             arms.append(dict(name="p2p_mesh_panels4", kind="bfp", algo="mesh", transport="p2p", panels=4))
+            # each request's decode + SGD epilogue on the comm stream as soon as its all-gather lands (overlapping the
+            # rest of the backward) instead of on the compute stream after the last backward GEMM
+            arms.append(dict(name="rccl_mesh_epicomm", kind="bfp", algo="mesh", transport="native", epi="comm"))
+            arms.append(dict(name="p2p_mesh_epicomm", kind="bfp", algo="mesh", transport="p2p", epi="comm"))
         else:
             arms.append(dict(name=f"{impl}_{a.algo}", kind="bfp", algo=a.algo, rings=a.rings, transport="torch"))
         schedule_ab = []
@@ -372,7 +378,7 @@ def main(argv=None):
                 setup = build(spec["name"], spec["kind"], algo=spec.get("algo", "mesh"), rings=spec.get("rings", 1),
                               transport=spec["transport"], gemm=spec.get("gemm", "persistent"),
                               sdma=spec.get("sdma", False), panels=spec.get("panels", 0),
-                              ring_sub=spec.get("ring_sub", 1))
+                              ring_sub=spec.get("ring_sub", 1), epi=spec.get("epi"))
                 rec.update(setup.info)
                 g = gate.allreduce_exactness(setup.engine, timeout_s=min(eng_timeout, 120.0))
                 rec["exact"] = g["exact"]

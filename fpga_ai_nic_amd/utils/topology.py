@@ -141,6 +141,9 @@ def link_matrix(world: int, devices=None):
     return link_matrix_for([device_bus_id(d) for d in devices], peer=peer)
 
 
+_AGREED: dict = {}
+
+
 def agreed_link_matrix(world: int):
     """The link matrix every rank of the default process group uses: each rank reports the PCI bus id of its own
     device; rank 0 derives the matrix (rocm-smi link types of those GPUs, else peer access from its view) and
@@ -151,6 +154,9 @@ def agreed_link_matrix(world: int):
 
     if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() == world):
         return link_matrix(world)
+    key = (world, id(dist.distributed_c10d._get_default_group()))
+    if key in _AGREED:  # one rocm-smi query + agreement per process group (every ring engine asks)
+        return _AGREED[key]
     import socket
 
     ident = [None] * world
@@ -170,6 +176,7 @@ def agreed_link_matrix(world: int):
                 peer = [[pm[local[a]][local[b]] for b in bus] for a in bus]
         obj = [{"links": link_matrix_for(bus, peer=peer), "bus_ids": bus}]
     dist.broadcast_object_list(obj, src=0)
+    _AGREED[key] = obj[0]["links"]
     return obj[0]["links"]
 
 
