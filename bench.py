@@ -380,8 +380,11 @@ def main(argv=None):
                               sdma=spec.get("sdma", False), panels=spec.get("panels", 0),
                               ring_sub=spec.get("ring_sub", 1), epi=spec.get("epi"))
                 rec.update(setup.info)
+                t_arm = time.perf_counter()
+                log(f"arm {spec['name']}: built, running the exactness gate")
                 g = gate.allreduce_exactness(setup.engine, timeout_s=min(eng_timeout, 120.0))
                 rec["exact"] = g["exact"]
+                log(f"arm {spec['name']}: gate exact={g['exact']} ({time.perf_counter() - t_arm:.1f} s)")
                 arm_gates[spec["name"]] = g
                 if not g["exact"]:
                     gates_failed.append({"arm": spec["name"], **g})
@@ -389,6 +392,7 @@ def main(argv=None):
                     raise RuntimeError(f"all-reduce exactness gate failed: {g}")
                 e, _, _, _, _ = run(setup, mb, 99, 2, a.ab_steps, f"ab {spec['name']}")
                 rec["ms_per_step"] = round(e / a.ab_steps * 1e3, 4)
+                log(f"arm {spec['name']}: {rec['ms_per_step']} ms/step ({time.perf_counter() - t_arm:.1f} s)")
             except Exception as ex:  # noqa: BLE001 - a failing arm is recorded and skipped, never fatal
                 rec["error"] = str(ex)[:300]
                 log(f"arm {spec['name']} excluded: {rec['error']}")
@@ -440,6 +444,7 @@ def main(argv=None):
                "ms_per_step": round(e2 / ref_steps * 1e3, 4)}
     elapsed, t_enqueue, loss, _, graphed = run(main_setup, mb, 1234, a.warmup, a.steps, "timed", graph_ok=True)
     ms = elapsed / a.steps * 1e3
+    log(f"headline: {ms:.4f} ms/step over {a.steps} steps")
     tr = run(main_setup, mb, 1234, 1, a.steps, "traced", trace=True)[3] if can_trace else None
 
     # ------------------------------------------------------------------ extras (bounded)
@@ -455,6 +460,7 @@ def main(argv=None):
             extras[name] = {"skipped": f"extra budget ({a.extra_budget:.0f} s) spent"}
             return
         wd.arm(f"extra {name}")
+        log(f"extra {name}")
         try:
             extras[name] = fn()
         except Exception as ex:  # noqa: BLE001 - an extra never costs the headline its record
@@ -652,6 +658,22 @@ def _config4(a, world, rank, device, ctx, native_transport, p2p_comm, make_engin
                          "bus_bw_GBps": round(algo_bw * 2 * (world - 1) / world, 2),
                          "wire_bytes_per_rank": int(eng.wire_bytes(L)), "rings": int(getattr(eng, "rings", 1)),
                          "input": "prepacked" if kw else "f32"}
+            if hasattr(eng, "trace"):  # one traced request: phase split (mesh) / per-hop split (ring), this rank
+                eng.trace(True)
+                once().synchronize(timeout_s)
+                tr = eng.trace_summary()
+                eng.trace(False)
+                out[name]["comm_us"] = round(tr["comm_ms"] * 1e3, 1)
+                if tr.get("hop_rounds"):
+                    k = tr["hop_rounds"]
+                    out[name]["ring_hops"] = {
+                        "rounds": k, "credit_us": round(tr["hop_credit_ms"] * 1e3 / k, 2),
+                        "ready_us": round(tr["hop_ready_ms"] * 1e3 / k, 2),
+                        "kernel_us": round(tr["hop_kernel_ms"] * 1e3 / k, 2),
+                        "max_round_us": round(tr["hop_max_ms"] * 1e3, 2)}
+                else:
+                    out[name]["phase_us"] = {p[:-3]: round(tr[p] * 1e3, 1) for p in
+                                             ("pack_ms", "exchange_ms", "reduce_ms", "gather_ms", "epilogue_ms")}
         except Exception as ex:  # noqa: BLE001
             out[name] = {"error": str(ex)[:300]}
         finally:
