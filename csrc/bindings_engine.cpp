@@ -37,13 +37,15 @@ void register_engine(pybind11::module_& m) {
       .def_property_readonly("collectives", &LoopbackComm::collectives);
   pybind11::class_<P2PComm, Comm>(m, "P2PComm")
       .def(pybind11::init<int, int, int, size_t, int>(), pybind11::arg("rank"), pybind11::arg("world"),
-           pybind11::arg("device"), pybind11::arg("slot_bytes") = (size_t)128 << 20, pybind11::arg("depth") = 2)
+           pybind11::arg("device"), pybind11::arg("slot_bytes") = (size_t)128 << 20, pybind11::arg("depth") = 2,
+           pybind11::call_guard<pybind11::gil_scoped_release>())
       .def_property_readonly("depth", &P2PComm::depth, "arena slots per sender")
       .def("handles", [](P2PComm& c) { return pybind11::bytes(c.handles()); })
       .def("connect",
            [](P2PComm& c, const std::vector<pybind11::bytes>& all) {
              std::vector<std::string> v;
              for (auto& b : all) v.push_back(std::string(b));
+             pybind11::gil_scoped_release nogil;  // a stuck IPC import must not block the run's watchdog thread
              c.connect(v);
            })
       .def_static("connect_local", &P2PComm::connect_local)

@@ -166,7 +166,16 @@ EngineLayout AllReduceEngine::layout(int64_t n, int64_t shard, int64_t chunks) c
   const int R = (int)orders_.size();
   const int64_t chunk = cdiv(std::max<int64_t>(n, 1), R);
   L.sub = ring_sub();
-  const RingGeometry g = ring_geometry(chunk, N, cfg_.max_slice_elems, 256 * (int64_t)L.sub);
+  int64_t max_slice = cfg_.max_slice_elems;
+  if (P2PComm* d = comm_ ? comm_->direct() : nullptr) {
+    // two (sub-)slice messages per peer and round must fit one arena slot (run_ring_direct): halve the slice cap
+    // until they do (the arena slot is clamped by the IPC size cap, p2p_comm.h)
+    const int64_t gran = 256 * (int64_t)L.sub;
+    auto fits = [&](int64_t s) { return 2 * round_up((int64_t)wire_shard_bytes(cfg_.codec, s / L.sub), 256) <=
+                                        (int64_t)d->payload_bytes(); };
+    while (max_slice > gran && !fits(max_slice)) max_slice = std::max<int64_t>(gran, max_slice / 2 / gran * gran);
+  }
+  const RingGeometry g = ring_geometry(chunk, N, max_slice, 256 * (int64_t)L.sub);
   L.rings = R;
   L.slice = g.slice_elems;
   L.blocks = g.blocks;

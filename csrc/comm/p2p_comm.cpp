@@ -39,6 +39,18 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes, int depth)
     : rank_(rank), world_(world), device_(device), slot_((slot_bytes + 255) / 256 * 256), depth_(depth) {
   FAN_CHECK(depth >= 2 && depth <= 16, "p2p: 2 <= depth <= 16 arena slots per sender");
   FAN_CHECK(world >= 1 && rank >= 0 && rank < world, "bad rank/world");
+  // One IPC-exported allocation stays <= kMaxArenaBytes: on this image a peer's hipIpcOpenMemHandle of a 2 GiB
+  // allocation never returned (4 processes, uncached and coarse alike; 1 GiB arenas open in 0.1-0.3 ms —
+  // tools/probes/p2p_connect_probe.py), and 8 ranks x depth 4 x 128 MB slots would be 4 GiB. The slot shrinks
+  // instead; the engine chunks its messages to payload_bytes() (engine.cpp layout), so only the chunk count grows.
+  size_t cap = kMaxArenaBytes;
+  if (const char* c = std::getenv("FAN_P2P_ARENA_MAX_MB")) cap = (size_t)std::atoll(c) << 20;
+  const size_t max_slot = cap / ((size_t)world * depth) / 256 * 256;
+  if (slot_ > max_slot) {
+    if (std::getenv("FAN_P2P_DEBUG"))
+      std::fprintf(stderr, "[p2p rank %d] slot %zu -> %zu B (arena cap %zu MB)\n", rank, slot_, max_slot, cap >> 20);
+    slot_ = max_slot;
+  }
   FAN_CHECK(slot_ > kTrailerBytes, "slot_bytes must exceed the 256-B verify trailer");
   if (const char* c = std::getenv("FAN_P2P_COPY")) sdma_ = !std::strcmp(c, "sdma");
   FAN_HIP_CHECK(hipSetDevice(device));
@@ -61,6 +73,9 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes, int depth)
     }
   }
   arena_mem_ = uncached_ ? "uncached" : mem == "fine" ? "fine" : "coarse";
+  if (std::getenv("FAN_P2P_DEBUG"))
+    std::fprintf(stderr, "[p2p rank %d] arena %zu MB (%s) allocated\n", rank, ((size_t)world * depth_ * slot_) >> 20,
+                 arena_mem_.c_str());
   // flags are polled by the command processor (hipStreamWaitValue64) and written by peers' command
   // processors (hipStreamWriteValue64); device memory supports both and HIP IPC export (probed on
   // MI355X: tools/probes/stream_wait_probe.cpp)
@@ -209,6 +224,7 @@ std::string P2PComm::handles() const {
   Handles h;
   FAN_HIP_CHECK(hipIpcGetMemHandle(&h.arena, arena_));
   FAN_HIP_CHECK(hipIpcGetMemHandle(&h.flags, flags_));
+  if (std::getenv("FAN_P2P_DEBUG")) std::fprintf(stderr, "[p2p rank %d] IPC handles exported\n", rank_);
   device_identity(device_, h.host, sizeof(h.host), h.bus, sizeof(h.bus));
   return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
 }
@@ -226,8 +242,12 @@ void P2PComm::connect(const std::vector<std::string>& all) {
     if (std::strncmp(h.host, host, sizeof(host)) || std::strncmp(h.bus, bus, sizeof(bus))) cross_device_ = true;
     void* a = nullptr;
     void* f = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     FAN_HIP_CHECK(hipIpcOpenMemHandle(&a, h.arena, hipIpcMemLazyEnablePeerAccess));
     FAN_HIP_CHECK(hipIpcOpenMemHandle(&f, h.flags, hipIpcMemLazyEnablePeerAccess));
+    if (std::getenv("FAN_P2P_DEBUG"))
+      std::fprintf(stderr, "[p2p rank %d] opened peer %d's arena + flags (%s %s) in %.1f ms\n", rank_, p, h.host,
+                   h.bus, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     peer_arena_[p] = reinterpret_cast<uint8_t*>(a);
     peer_flags_[p] = reinterpret_cast<uint64_t*>(f);
     opened_[p] = true;

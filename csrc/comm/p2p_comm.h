@@ -7,9 +7,10 @@
 // command-processor wait, so no CU spins and nothing can deadlock on occupancy — copies the payload out
 // and acknowledges into the sender's flag block, which frees that arena slot for reuse.
 //
-// Arena: world x depth slots of slot_bytes (a ring of `depth` slots per sender, indexed by sequence mod depth; depth 2
-// = double-buffered by parity), so a sender only stalls when it is `depth` messages ahead of a receiver — a ring hop
-// streamed in P sub-slices consumes each message P sub-rounds after it lands and needs depth >= P + 1.
+// Arena: world x depth slots of slot_bytes, at most kMaxArenaBytes in all (a ring of `depth` slots per sender,
+// indexed by sequence mod depth; depth 2 = double-buffered by parity), so a sender only stalls when it is `depth`
+// messages ahead of a receiver — a ring hop streamed in P sub-slices consumes each message P sub-rounds after it
+// lands and needs depth >= P + 1.
 // Flags: ready[world] + ack[world] (uint64 each, monotone sequence numbers).
 // Reference analogue: the NIC's Ethernet link + credit flow control (hw/all_reduce.sv:468-483) and the
 // done-flag writes (hw/all_reduce.sv:1368-1375); here sequence numbers play the role of both.
@@ -65,6 +66,9 @@ class P2PComm : public Comm {
   P2PComm(int rank, int world, int device, size_t slot_bytes, int depth = 2);
   ~P2PComm() override;
   static constexpr size_t kTrailerBytes = 256;  // per slot: 16 verify tags of 16 B
+  // the arena (world x depth slots) is one IPC-exported allocation of at most this size: slot_bytes() is clamped to
+  // fit (FAN_P2P_ARENA_MAX_MB overrides; see the constructor for the 2 GiB import hang that sets it)
+  static constexpr size_t kMaxArenaBytes = (size_t)1 << 30;
   int rank() const override { return rank_; }
   int world() const override { return world_; }
   size_t slot_bytes() const { return slot_; }

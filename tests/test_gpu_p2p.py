@@ -230,3 +230,64 @@ def test_abort_releases_a_parked_stream():
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "parked=True" in r.stdout and "UNBLOCKED" in r.stdout and "raises after abort" in r.stdout, out[-3000:]
+
+
+def _arena_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fpga_ai_nic_amd.parallel import gate
+        from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce
+        from fpga_ai_nic_amd.parallel.transport import try_p2p_comm
+
+        torch.cuda.set_device(0)
+        comm, err = try_p2p_comm()  # the bench's arena: 128 MB slots asked for, depth 4
+        assert comm is not None, err
+        ok = {"arena_capped": comm.slot_bytes * world * comm.depth <= 1 << 30 and comm.depth == 4}
+        n = 4096
+        send = torch.cat([torch.full((n,), float(rank * 100 + p), device="cuda") for p in range(world)])
+        recv = torch.empty_like(send)
+        comm.all_to_all(send.view(torch.uint8), recv.view(torch.uint8))
+        torch.cuda.synchronize()
+        ok["all_to_all"] = bool(torch.equal(recv.cpu(), torch.cat([torch.full((n,), float(p * 100 + rank))
+                                                                    for p in range(world)])))
+        for algo, rings in (("mesh", 1), ("ring", world - 1)):
+            eng = NativeAllReduce(None, codec="bfp_rne", algo=algo, rings=rings, comm=comm)
+            # a bucket whose wire shards exceed the capped slot: the layout chunks it (mesh) / shrinks the slice
+            big = 4 * comm.slot_bytes * world
+            L = eng.layout(big)
+            ok[f"{algo}_fits_slot"] = (L.shard if algo == "mesh" else 2 * L.slice_elems) * 1.07 <= comm.payload_bytes
+            g = gate.allreduce_exactness(eng, n=1 << 20, timeout_s=60)
+            ok[f"{algo}_gate"] = bool(g["exact"])
+        q.put((rank, ok, comm.sequence))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, {"error": repr(e)}, -1))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_p2p_four_processes_default_arena():
+    """Four processes on the GPU with the bench's P2P arena request (128 MB slots x depth 4 x 4 senders = 2 GiB, a
+    size whose IPC import never returned on this image): the arena is clamped to 1 GiB, every rank connects, and the
+    mesh and the 3-ring pass the exactness gate (BFP sums bit-exact vs the spec simulators)."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.start_processes(_arena_worker, args=(world, _free_port(), q), nprocs=world, join=False,
+                            start_method="spawn")
+    res = {}
+    try:
+        for _ in range(world):
+            rank, ok, seq = q.get(timeout=180)
+            res[rank] = (ok, seq)
+    except _queue.Empty:
+        for p in pc.processes:
+            p.kill()
+        pytest.fail("p2p arena workers did not report within 180 s")
+    while not pc.join(60):
+        pass
+    for rank, (ok, seq) in res.items():
+        assert "error" not in ok, ok
+        assert all(ok.values()), (rank, ok)
+    assert len({s for _, s in res.values()}) == 1, "ranks issued different numbers of rounds"
