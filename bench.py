@@ -102,6 +102,12 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def _release_mode() -> int:
+    from fpga_ai_nic_amd import _ext
+
+    return _ext.require().p2p_release_mode()
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -553,6 +559,11 @@ def main(argv=None):
                 "schedule": main_setup.name if schedule_ab is not None else "fixed",
                 "gemm_inflight": info["gemm_inflight"],
                 "p2p_copy": info["copy"],
+                # release of the peer-storing kernels' stores before each ready flag: "cp" (command processor,
+                # one-GPU default) or "block" (in-kernel, chosen by P2PComm.connect when a peer is on another GPU)
+                "p2p_release": ({0: "none", 1: "block", 2: "thread", 3: "cp"}[_release_mode()]
+                                if info["copy"] is not None else None),
+                "p2p_cross_device": bool(ctx["p2p"].cross_device) if ctx["p2p"] is not None else None,
                 "hip_graph": graphed,
                 "fused_sgd": True,
                 # world 1: dW's BFP round trip + SGD inside the bwd-weight GEMM epilogue (no separate update pass)

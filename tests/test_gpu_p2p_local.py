@@ -43,7 +43,7 @@ def _run(world, algo, rings, m=40000, max_slice=2048, mode="plain"):
     rng = np.random.default_rng(100 + world)
     grads = [rng.standard_normal(m).astype(np.float32) for _ in range(world)]
     res, errs = [None] * world, [None] * world
-    verify = mode in ("verify", "fault", "stream_verify")
+    verify = mode in ("verify", "fault", "stream_verify", "block_verify")
     fault = "p2p_recv:0:flip" if mode == "fault" else None
     engines = [NativeAllReduce(None, codec="bfp_rne", algo=algo, rings=rings, max_slice_elems=max_slice,
                                comm=comms[r], verify=verify, fault=fault, ring_sub=3 if stream else 1)
@@ -105,10 +105,10 @@ def _check(world, algo, rings, mode="plain"):
             if e is None or "corrupted" not in str(e) or f"{site} row {want_row} " not in str(e):
                 why.append(f"rank {r}: expected a '{site} row {want_row}' corruption, got {e!r}")
         return {"ok": not why, "why": why, "rings": 0}
-    out = {"ok": True, "why": [], "rings": len(res[0][4])}
+    out = {"ok": True, "why": [], "rings": len(res[0][4]), "release_mode": _ext.require().p2p_release_mode()}
     for r in range(world):
         o, o_p, _, direct, orders, verified = res[r]
-        if mode in ("verify", "stream_verify") and verified <= 0:
+        if mode in ("verify", "stream_verify", "block_verify") and verified <= 0:
             out["why"].append(f"rank {r}: verify mode checked no message")
         if not np.array_equal(o[:m], ref[:m]):
             out["why"].append(f"rank {r}: {algo} x{rings} differs from the simulator")
@@ -124,6 +124,8 @@ def _check(world, algo, rings, mode="plain"):
 
 def _child(world, algo, rings, mode):
     env = dict(os.environ, GPU_MAX_HW_QUEUES="32")
+    if mode.startswith(("block", "thread")):  # the in-kernel release forms (cross-device peers default to "block")
+        env["FAN_P2P_RELEASE"] = mode.split("_")[0]
     try:
         r = subprocess.run([sys.executable, os.path.abspath(__file__), str(world), algo, str(rings), mode], env=env,
                            capture_output=True, text=True, timeout=150)
@@ -157,6 +159,16 @@ def test_direct_ring_streamed_hops_bit_exact(world, rings, mode):
     """Each hop's message in 3 sub-slices with a ready flag each (4-slot arenas): the sums, summation order and
     results are the lock-step ring's, bit for bit, from f32 and from prepacked input (sub-shard wire layout)."""
     _child(world, "ring", rings, mode)
+
+
+@pytest.mark.parametrize("world,algo,rings", [(4, "ring", 3), (4, "mesh", 1)])
+@pytest.mark.parametrize("mode", ["block", "thread", "block_verify"])
+def test_direct_p2p_in_kernel_release_bit_exact(world, algo, rings, mode):
+    """The in-kernel release forms of the peer-storing kernels (p2p_release: "block" = per-workgroup drain + one
+    system-scope release, the mode a process with peers on OTHER GPUs runs unless FAN_P2P_RELEASE says otherwise;
+    "thread" = a system fence per wave): same sums, bit for bit, also with verify mode checking every message."""
+    rec = _child(world, algo, rings, mode)
+    assert rec["release_mode"] == (1 if mode.startswith("block") else 2), rec
 
 
 @pytest.mark.parametrize("algo,rings", [("mesh", 1), ("ring", 2)])
