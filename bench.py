@@ -517,6 +517,8 @@ def main(argv=None):
                 return out
 
             extra("uncompressed", uncompressed, 15)
+            extra("config5", lambda: _config5(a, world, device, main_setup.info, ctx, native_transport, p2p_comm,
+                                              make_engine, ctrl, eng_timeout), 30)
     extras_s = time.perf_counter() - t_extra0
 
     # replicas after every step of the run: bit-identical weights on every rank (the reference reads its NIC
@@ -599,6 +601,29 @@ def main(argv=None):
               flush=True)
         return 3
     return 0
+
+
+def _config5(a, world, device, info, ctx, native_transport, p2p_comm, make_engine, ctrl, timeout_s):
+    """BASELINE config 5 at world > 1: BERT-base backward GEMMs overlapped with each layer bucket's BFP all-reduce +
+    fused SGD over the headline's transport and algorithm (bench/bert_overlap.py measure(): compute only, comm only,
+    both; 3 rounds, max over ranks). At world 1 the "comm" is CU work with no link time to hide,
+    so the record carries it only where links are."""
+    if device.type != "cuda":
+        return {"skipped": "CPU run"}
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
+    import bert_overlap
+
+    comm, t = None, ctrl
+    if info.get("transport") == "p2p":
+        comm = p2p_comm()
+        comm.sdma = info.get("copy") == "sdma"
+    else:
+        t = native_transport() or ctrl
+    eng = make_engine(t, "bfp", rounding=a.rounding, algo=info.get("algo", "mesh"), rings=max(1, info.get("rings", 1)),
+                      impl="native", comm=comm, timeout_s=timeout_s)
+    r = bert_overlap.measure(eng, device, world, tokens=4096, layers=12, rounds=3)
+    r.update(transport="p2p" if comm is not None else getattr(t, "name", "torch"), algo=info.get("algo", "mesh"))
+    return r
 
 
 def _config4(a, world, rank, device, ctx, native_transport, p2p_comm, make_engine, ctrl, timeout_s):

@@ -6,8 +6,8 @@ self-consistent here: exactly one JSON line, a measured all-reduce (extra.allred
 communicator's own rank count, direct P2P rounds, and bit-identical replicas after the run (extra.dist) — and the
 self-selection the driver's multi-GPU run relies on: the schedule A/B in warmup (every arm timed or excluded with
 its error: RCCL refuses two ranks on one device, so only the P2P arms run here), the bit-exact all-reduce gate of
-the chosen arm, and the config-4 / uncompressed extras, all within the run's budget. A peer slot corrupted after its
-ready flag makes every arm fail the gate and the run exit non-zero."""
+the chosen arm, and the config-4 / uncompressed / config-5 extras, all within the run's budget. A peer slot
+corrupted after its ready flag makes every arm fail the gate and the run exit non-zero."""
 import json
 import os
 import subprocess
@@ -56,6 +56,8 @@ def test_bench_two_ranks_p2p_one_gpu(tmp_path):
     assert c4["raw_f32_mesh_p2p"]["algo_bw_GBps"] > 0 and "skipped" in c4["rccl_f32"], c4
     un = ex["uncompressed"]
     assert un["p2p_raw_f32_mesh"]["ms_per_step"] > 0 and un["speedup_vs_best_uncompressed"] > 0, un
+    c5 = ex["config5"]  # BERT-base backward + per-layer all-reduce over the headline's transport
+    assert c5["t_compute_ms"] > 0 and c5["t_comm_ms"] > 0 and c5["t_overlap_ms"] > 0 and c5["transport"] == "p2p", c5
     assert ex["extras_s"] < 240 and ex["run_s"] < 400, (ex["extras_s"], ex["run_s"])
 
 
