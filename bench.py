@@ -95,11 +95,23 @@ def parse_args(argv=None):
     ap.add_argument("--extra-budget", type=float, default=240.0,
                     help="seconds the extras after the headline may take in total (config 4, uncompressed step, the "
                          "world-1 split); what does not fit is recorded as skipped; 0 disables them")
+    ap.add_argument("--arm-timeout", type=float, default=90.0,
+                    help="world > 1 schedule A/B: bound of each arm's exactness gate and of its steps' waits; an arm "
+                         "whose transport hangs fails at this bound, the transport is aborted on every rank and its "
+                         "remaining arms are excluded")
     ap.add_argument("--timeout", type=float, default=300.0,
                     help="watchdog budget per phase in seconds (init, warmup, timed steps, ...) and the bound of every "
                          "all-reduce wait: on expiry the engine's debug_status() goes to stderr, the communicator is "
                          "aborted and the rank exits with code 124 (0 disables)")
     return ap.parse_args(argv)
+
+
+def _transport_error(t) -> str:
+    """The communicator's sticky error ("p2p transport aborted", "aborted", an RCCL async error) or ""."""
+    try:
+        return t.async_error() or ""
+    except Exception as e:  # noqa: BLE001
+        return str(e) or "error"
 
 
 def _release_mode() -> int:
@@ -268,7 +280,10 @@ def main(argv=None):
     def release(setup):
         if setup is None:
             return
-        setup.trainer.finish()
+        try:
+            setup.trainer.finish()
+        except Exception as ex:  # noqa: BLE001 - an arm that failed in flight: its transport was aborted
+            log(f"release of {setup.name}: {str(ex)[:200]}")
         setup.engine = setup.model = setup.trainer = None
         gc.collect()
         if cuda:
@@ -283,7 +298,7 @@ def main(argv=None):
 
     stall_rank = int(os.environ.get("FAN_BENCH_STALL_RANK", "-1"))
 
-    def run(setup, mb, seed, warmup, steps, tag, graph_ok=False, trace=False):
+    def run(setup, mb, seed, warmup, steps, tag, graph_ok=False, trace=False, wait_s=None):
         """W warmup + K timed steps of ``setup`` at per-GPU batch mb: (elapsed s max over ranks, host enqueue s,
         loss, trace summary or None, graphed). The garbage collector is off inside (a collection pause in the
         launch loop starves the GPU: one 20-step MB-1792 window once read 0.46 instead of 0.38 ms/step)."""
@@ -293,11 +308,11 @@ def main(argv=None):
         if setup.info.get("copy") is not None and ctx["p2p"] is not None:  # the arm's copy path (shared comm)
             ctx["p2p"].sdma = setup.info["copy"] == "sdma"
         try:
-            return _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace)
+            return _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace, wait_s)
         finally:
             gc.enable()
 
-    def _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace):
+    def _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace, wait_s=None):
         trainer, model, engine = setup.trainer, setup.model, setup.engine
         x, y = batch(mb, seed)
         wd.arm(f"warmup {tag} mb={mb}")
@@ -305,7 +320,7 @@ def main(argv=None):
             time.sleep(float(os.environ.get("FAN_BENCH_STALL_S", "600")))
         for _ in range(warmup):
             trainer.step(x, y)
-        trainer.finish()
+        trainer.finish(wait_s)  # wait_s: an A/B arm's bound (a hung transport raises instead of parking the rank)
         wd.arm(f"{tag} mb={mb}")
         step = lambda: trainer.step(x, y)  # noqa: E731
         graphed = False
@@ -333,7 +348,7 @@ def main(argv=None):
             step()
         loss_rows = model.loss_rows
         t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
-        trainer.finish()
+        trainer.finish(wait_s)
         if cuda:
             torch.cuda.synchronize()
         D.barrier()
@@ -376,6 +391,7 @@ def main(argv=None):
         schedule_ab = []
         arm_gates = {}
         best = None
+        arm_wait = min(eng_timeout, a.arm_timeout)  # gate and A/B waits: below the watchdog's per-phase budget
         for spec in arms:
             wd.arm(f"schedule A/B {spec['name']}")
             rec = {"arm": spec["name"]}
@@ -388,7 +404,7 @@ def main(argv=None):
                 rec.update(setup.info)
                 t_arm = time.perf_counter()
                 log(f"arm {spec['name']}: built, running the exactness gate")
-                g = gate.allreduce_exactness(setup.engine, timeout_s=min(eng_timeout, 120.0))
+                g = gate.allreduce_exactness(setup.engine, timeout_s=arm_wait)
                 rec["exact"] = g["exact"]
                 log(f"arm {spec['name']}: gate exact={g['exact']} ({time.perf_counter() - t_arm:.1f} s)")
                 arm_gates[spec["name"]] = g
@@ -396,13 +412,37 @@ def main(argv=None):
                     gates_failed.append({"arm": spec["name"], **g})
                     rec["gate"] = g
                     raise RuntimeError(f"all-reduce exactness gate failed: {g}")
-                e, _, _, _, _ = run(setup, mb, 99, 2, a.ab_steps, f"ab {spec['name']}")
+                e, _, _, _, _ = run(setup, mb, 99, 2, a.ab_steps, f"ab {spec['name']}", wait_s=arm_wait)
                 rec["ms_per_step"] = round(e / a.ab_steps * 1e3, 4)
                 log(f"arm {spec['name']}: {rec['ms_per_step']} ms/step ({time.perf_counter() - t_arm:.1f} s)")
             except Exception as ex:  # noqa: BLE001 - a failing arm is recorded and skipped, never fatal
                 rec["error"] = str(ex)[:300]
                 log(f"arm {spec['name']} excluded: {rec['error']}")
             schedule_ab.append(rec)
+            # A transport whose request timed out was aborted by the engine (poisoned P2P flags / ncclCommAbort release
+            # the parked streams). Every rank learns which transports ANY rank lost and drops them together, so the
+            # later arms and extras stay symmetric: a hung link costs its arms, not the run (the watchdog would
+            # otherwise end every rank at --timeout with no record).
+            lost = [k for k in ("p2p", "native") if ctx[k] is not None and _transport_error(ctx[k])]
+            lost_any = sorted({k for ks in D.all_gather_object(lost) for k in ks})
+            for k in lost_any:
+                if ctx[k] is not None and not _transport_error(ctx[k]):
+                    try:
+                        ctx[k].abort()
+                    except Exception:  # noqa: BLE001
+                        pass
+                ctx[k] = None
+                ctx[k + "_err"] = f"aborted after arm {spec['name']} failed: {rec.get('error', '?')[:160]}"
+                rec.setdefault("transport_lost", []).append(k)
+                log(f"transport {k} aborted and excluded after arm {spec['name']}")
+            if lost_any and "ms_per_step" in rec:  # its numbers came from a transport that is gone
+                rec["error"] = ctx[lost_any[0] + "_err"]
+                del rec["ms_per_step"]
+            if best is not None and best[0].get("transport") in lost_any:  # the fastest so far ran on a lost transport
+                best[0]["error"] = ctx[best[0]["transport"] + "_err"]
+                best[0].pop("ms_per_step", None)
+                release(best[1])
+                best = None
             if "ms_per_step" in rec and (best is None or rec["ms_per_step"] < best[0]["ms_per_step"]):
                 release(best[1] if best else None)
                 best = (rec, setup)

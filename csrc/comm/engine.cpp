@@ -372,7 +372,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
     tag_sent(r1, "mesh_pack");
   }
   mark(kTpPacked);
-  d->publish(r1, st);
+  if (!fault_.maybe_drop("p2p_publish")) d->publish(r1, st);  // test hook: the round is never announced
   count_peers(sb, d);
   d->wait(r1, st);
   check_received(r1, kSiteMeshDirectSend);
@@ -388,7 +388,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
     tag_sent(r2, "mesh_reduce");
   }
   mark(kTpReduced);
-  d->publish(r2, st);
+  if (!fault_.maybe_drop("p2p_publish")) d->publish(r2, st);
   count_peers(sb, d);
   d->wait(r2, st);
   check_received(r2, kSiteMeshDirectGather);
@@ -830,7 +830,7 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
       }
       hop_mark(3);
       if (t > 0) d->release_from(sub_round[j - P], ups, st);  // the messages of (t - 1, s) are consumed
-      d->publish_to(rr, downs, st);
+      if (!fault_.maybe_drop("p2p_publish")) d->publish_to(rr, downs, st);
       // what this sub-round will deliver from upstream (read in (t + 1, s) or by the drain below)
       for (size_t i = 0; i < rings.size(); ++i) {
         prev[i].clear();

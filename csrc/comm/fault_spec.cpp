@@ -40,7 +40,7 @@ std::vector<FaultRule> parse_fault_spec(const std::string& spec) {
         bad(item, "delay_ms needs a number of milliseconds in [0, 3.6e6]");
       r.kind = "delay_ms";
       r.delay_ms = ms;
-    } else if (r.kind != "flip" && r.kind != "nan") {
+    } else if (r.kind != "flip" && r.kind != "nan" && r.kind != "drop") {
       bad(item, "unknown fault kind '" + r.kind + "'");
     }
     out.push_back(r);

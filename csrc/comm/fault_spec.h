@@ -11,7 +11,7 @@ namespace fan {
 struct FaultRule {
   std::string site;
   int64_t index;     // which call of `site` (0-based) the rule fires on
-  std::string kind;  // "flip", "nan" or "delay_ms"
+  std::string kind;  // "flip", "nan", "delay_ms" or "drop" (a site that sends: the message is never announced)
   double delay_ms = 0.0;
 };
 

@@ -12,7 +12,8 @@
 // Fault injection (FAN_FAULT="site:index:kind[,...]", test-only; the same grammar as the Python engine's
 // fpga_ai_nic_amd/utils/faults.py): sites mesh_pack (the packed shards before the all-to-all), mesh_reduce (the
 // owner's reduced shard before the all-gather), ring_send (one ring message); kinds flip (xor the first byte),
-// nan (last byte = 0xFF: an exponent of 255), delay_ms=<ms> (the issuing thread stalls the stream's progress).
+// nan (last byte = 0xFF: an exponent of 255), delay_ms=<ms> (the issuing thread stalls the stream's progress);
+// site p2p_publish (the ready flags of one direct P2P round) with kind drop: the round is never announced.
 #pragma once
 #include <cstdint>
 #include <map>
@@ -51,6 +52,9 @@ class FaultInjector {
   bool active() const { return !rules_.empty(); }
   // apply the rules matching the next call of `site` to buf[0, bytes) on stream s
   void maybe_corrupt(const std::string& site, uint8_t* buf, size_t bytes, hipStream_t s);
+  // true when a "drop" rule matches the next call of `site` (the caller then skips the send it guards: a lost
+  // message, so the peers' waits never complete — what a dead link looks like; test-only)
+  bool maybe_drop(const std::string& site);
 
  private:
   std::vector<FaultRule> rules_;

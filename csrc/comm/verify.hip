@@ -134,4 +134,12 @@ void FaultInjector::maybe_corrupt(const std::string& site, uint8_t* buf, size_t 
   }
 }
 
+bool FaultInjector::maybe_drop(const std::string& site) {
+  if (rules_.empty()) return false;
+  const int64_t k = counts_[site]++;
+  for (const FaultRule& r : rules_)
+    if (r.site == site && r.index == k && r.kind == "drop") return true;
+  return false;
+}
+
 }  // namespace fan

@@ -5,7 +5,9 @@ The reference has no failure handling at all (its ``wait()`` spins forever, sw/m
 
 Configure with ``FAN_FAULT="<site>:<call-index>:<kind>"`` (comma separated list), e.g.
 ``ring_send:3:flip`` (xor the first byte of the 4th ring message), ``mesh_pack:0:nan`` (plant an Inf exponent
-in the packed gradient), ``ring_send:0:delay_ms=200``.
+in the packed gradient), ``ring_send:0:delay_ms=200``. The native engine also knows ``p2p_publish:<k>:drop``: the
+k-th direct P2P round's ready flags are never written (a lost message: the peers' waits never complete), which the
+bench uses to show that a hung transport is aborted and excluded instead of ending the run.
 """
 from __future__ import annotations
 

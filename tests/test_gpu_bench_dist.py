@@ -12,6 +12,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -88,3 +89,24 @@ def test_bench_watchdog_fires_on_a_hung_peer(tmp_path):
     assert r.returncode != 0 and not recs
     assert "exceeded 20 s" in r.stderr and "debug_status" in r.stderr, r.stderr[-4000:]
     assert '"comm_kind": "p2p"' in r.stderr, r.stderr[-4000:]
+
+
+def test_bench_survives_a_hung_transport(tmp_path):
+    """Every engine's first direct P2P round is never announced (FAN_FAULT p2p_publish:0:drop: the ready flags are
+    not written, what a dead link looks like to the peers). The first P2P arm's exactness gate then times out at
+    --arm-timeout on both ranks, the engine aborts the transport (poisoned flags release the parked streams), the
+    ranks agree to drop P2P and exclude its remaining arms — a hung link costs its arms, not the whole record. Here
+    no other transport exists (RCCL refuses two ranks on one GPU), so the run ends non-zero, quickly and without the
+    watchdog."""
+    os.environ["FAN_FAULT"] = "p2p_publish:0:drop"
+    t0 = time.monotonic()
+    try:
+        r, recs = _bench(tmp_path, "--extra-budget", "0", "--arm-timeout", "15", timeout=300)
+    finally:
+        os.environ.pop("FAN_FAULT", None)
+    took = time.monotonic() - t0
+    assert r.returncode not in (0, 124) and not recs, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    assert "transport p2p aborted and excluded after arm p2p_mesh_persistent" in r.stderr, r.stderr[-4000:]
+    assert "exceeded" not in r.stderr, r.stderr[-4000:]  # the watchdog never fired
+    assert "P2P transport unavailable: aborted after arm p2p_mesh_persistent" in r.stderr, r.stderr[-4000:]
+    assert took < 150, took
