@@ -82,6 +82,9 @@ std::atomic<int>& gemm_main_loop_flag();
 // grid cap of the persistent 4-wave pipelined kernel (FAN_GEMM_PERSIST, default 256 = one workgroup per CU; 0: one
 // workgroup per tile); settable for in-process A/B and for tests that force several tiles per workgroup
 std::atomic<int>& gemm_persist_flag();
+// 256x256 persistent 4-wave loop on the ring of four 32-k half-stages (gemm_pl4h_kernel) instead of two 64-k stages
+// (FAN_GEMM_HALF, gemm_set_half_stage)
+std::atomic<int>& gemm_half_stage_flag();
 // diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
 void gemm_set_stamp_buffer(void* p);
 void* gemm_stamp_buffer();

@@ -1088,7 +1088,9 @@ __global__ void __launch_bounds__(256, 1)
     static_for<MI * NJ>([&](auto qc) __attribute__((always_inline)) {
       constexpr int q = decltype(qc)::value;
       if constexpr (READ && q % RSP == 0 && q / RSP < R) read_next(rd_st, rd_ks, cur ^ 1, q / RSP);
+#ifndef FAN_GEMM_NODMA  // diagnostic builds only: the main loop without its operand DMA (wrong results, timing)
       if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_kt, q / DSP);
+#endif
       mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
     });
   };
@@ -1163,6 +1165,225 @@ __global__ void __launch_bounds__(256, 1)
     for (int v = blockIdx.x; v < tiles * split_k; v += gridDim.x) {
       tile_body(v);
       __syncthreads();  // every wave's staging reads done before the next tile's DMA overwrites the LDS
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// The same 256x256 4-wave AGPR loop on a ring of FOUR half-stages (32 k each, 32 KiB: the LDS of the two 64-k
+// stages above) with one barrier per k-step instead of per K-tile. Why: the LDS-DMA issue is the loop's limiter
+// (a diagnostic build without the in-loop DMA, -DFAN_GEMM_NODMA, runs the big GEMMs 12-13 % faster:
+// profiles/r4_gemm_nodma_ab.jsonl), and in gemm_pl4_kernel all 16 pieces of a K-tile go into k-step 1, the step
+// that also carries the next step's 16 fragment reads, while k-step 0 carries none (a stage can only be refilled
+// after the mid-tile barrier). Here every k-step carries 8 pieces + 16 reads + 64 MFMAs:
+//   k-step h: MFMAs on the fragments of half-stage h (registers, set h & 1); under them the fragments of h + 1 are
+//   read (stage (h + 1) % 4, set (h + 1) & 1) and the DMA of half-stage h + 3 goes into stage (h + 3) % 4 = the
+//   stage of h - 1, whose reads every wave retired before the barrier that ended k-step h - 2; then lgkmcnt(0) +
+//   vmcnt(8) (this wave's pieces of h + 2 landed; those of h + 3 may stay in flight) and ONE barrier.
+// A half-stage's DMA has two k-steps to land, as before. Images: K-contiguous operands as [rows][32 k] (64-B rows,
+// 16-B chunk c of row r at slot c ^ ((r >> 1) & 3): conflict-free ds_read_b128), MN-contiguous ones as
+// [32 k][128 columns] per 128-column half (the ds_read_b64_tr_b16 image of gemm_pl4_kernel, 32 k-rows). The
+// MFMAs run in the same k order, so results are bit-identical to gemm_pl4_kernel.
+template <bool KCONTIG, int OUTER, int NT>
+__device__ __forceinline__ uint32_t piece_off_h(int64_t ld, int o0, int wave, int lane, int i) {
+  constexpr int IB = NT * 16;
+  const int t = wave * 64 + lane;
+  if (KCONTIG) {
+    const int row = i * (IB / 64) + (t >> 2);  // rows of 64 B
+    const int c = (t & 3) ^ ((row >> 1) & 3);
+    return (uint32_t)(((int64_t)(o0 + row) * ld + c * 8) * 2);
+  } else {
+    constexpr int PER_HALF = (32 * 256) / IB;
+    const int half = i / PER_HALF;
+    const int krow = (i % PER_HALF) * (IB / 256) + (t >> 4);  // k-rows of 256 B
+    const int cs = t & 15;
+    const int blk = (cs >> 1) ^ mn_swz(krow);
+    return (uint32_t)(((int64_t)krow * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8) * 2);
+  }
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ s16x8 read_frag_h(const char* lds, int o, int lane) {
+  if (KCONTIG) {
+    const int row = o + (lane & 15);
+    const int chunk = lane >> 4;
+    return *reinterpret_cast<const s16x8*>(lds + row * 64 + ((chunk ^ ((row >> 1) & 3)) << 4));
+  } else {
+    const char* h = lds + (o >> 7) * (32 * 256);
+    const int oo = o & 127;
+    const int q = (lane & 15) >> 2, p = lane & 3;
+    const int kb = 8 * (lane >> 4) + q;
+    const int blk = oo >> 4;
+    const int off0 = kb * 256 + ((blk ^ mn_swz(kb)) << 5) + 8 * p;
+    const int off1 = (kb + 4) * 256 + ((blk ^ mn_swz(kb + 4)) << 5) + 8 * p;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(h + off0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(h + off1));
+    s16x8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false>
+__global__ void __launch_bounds__(256, 1)
+    gemm_pl4h_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
+                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
+                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
+                     float* __restrict__ colsum, WireOut wo) {
+  constexpr int BM = 256, BN = 256, NT = 256, HK = 32, IB = NT * 16;
+  constexpr int A_BYTES = BM * HK * 2, STAGE = A_BYTES + BN * HK * 2;  // 16 + 16 KiB
+  constexpr int GA = A_BYTES / IB, G = GA + BN * HK * 2 / IB;         // 4 + 4 pieces per wave and half-stage
+  constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NJ = WTN / 16;
+  constexpr int Q = MI * NJ, R = MI + NJ;
+  constexpr int RSP = (Q * 3 / 4) / R, DSP = Q / G;  // 3 and 8
+  static_assert(RSP >= 1 && DSP >= 1 && G * DSP <= Q, "schedule");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / 2, wn = wave % 2;
+  const uint32_t lds0 = lds_addr_of(smem);
+  auto tile_body = [&](int v) __attribute__((always_inline)) {
+  const int wg = xcd_remap(v, tiles * split_k);
+  const int tile = wg % tiles, ksplit = wg / tiles;
+  const int GM = tiles_m >= 4 ? 4 : tiles_m;
+  const int grp = tile / (GM * tiles_n);
+  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
+  const int in_grp = tile % (GM * tiles_n);
+  const int m0 = (grp * GM + in_grp % gm) * BM;
+  const int n0 = (in_grp / gm) * BN;
+  const int k_per = K / split_k;
+  const int kbeg = ksplit * k_per;
+  const int nh = k_per / HK;
+
+  const int im = SPLIT ? 0 : m0 / BM;
+  const int cs0 = SPLIT ? (m0 == 0 ? 0 : nh) : im * nh / tiles_m;
+  const int cs1 = SPLIT ? nh : (im + 1) * nh / tiles_m;
+  const bool do_colsum = COLSUM && wm == 0;
+  float cs[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 fa[2][MI], fb[2][NJ];
+
+  uint32_t off[G];
+#pragma unroll
+  for (int p = 0; p < GA; ++p) off[p] = piece_off_h<AK, BM, NT>(lda, m0, wave, lane, p);
+#pragma unroll
+  for (int p = GA; p < G; ++p) off[p] = piece_off_h<BKC, BN, NT>(ldb, n0, wave, lane, p - GA);
+  const int64_t a_step = AK ? (int64_t)HK * 2 : (int64_t)HK * lda * 2;
+  const int64_t b_step = BKC ? (int64_t)HK * 2 : (int64_t)HK * ldb * 2;
+  const char* a_k0 = reinterpret_cast<const char*>(A) + (AK ? (int64_t)kbeg * 2 : (int64_t)kbeg * lda * 2);
+  const char* b_k0 = reinterpret_cast<const char*>(B) + (BKC ? (int64_t)kbeg * 2 : (int64_t)kbeg * ldb * 2);
+
+  auto piece = [&](int h, int p) __attribute__((always_inline)) {
+    const uint32_t st = lds0 + (h & 3) * STAGE + wave * 1024;
+    if (p < GA) glds16_s(a_k0 + h * a_step, off[p], st + p * IB);
+    else glds16_s(b_k0 + h * b_step, off[p], st + A_BYTES + (p - GA) * IB);
+  };
+  auto read_next = [&](const char* st, int set, int r) __attribute__((always_inline)) {
+    if (r < MI) fa[set][r] = read_frag_h<AK>(st, wm * WTM + r * 16, lane);
+    else fb[set][r - MI] = read_frag_h<BKC>(st + A_BYTES, wn * WTN + (r - MI) * 16, lane);
+  };
+  auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int dma_h,
+                   bool csk) __attribute__((always_inline)) {
+    constexpr int cur = decltype(cur_c)::value;
+    constexpr bool READ = decltype(read_c)::value, DMA = decltype(dma_c)::value;
+    if (COLSUM && csk)
+      static_for<NJ>([&](auto jc) __attribute__((always_inline)) { cs[jc.value] += frag_sum(fb[cur][jc.value]); });
+    static_for<MI * NJ>([&](auto qc) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+      if constexpr (READ && q % RSP == 0 && q / RSP < R) read_next(rd_st, cur ^ 1, q / RSP);
+#ifndef FAN_GEMM_NODMA
+      if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_h, q / DSP);
+#endif
+      mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
+    });
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+
+  // prologue: half-stages 0, 1, 2 in flight; retire 0 AND 1 (step 0 reads the fragments of 1; only 2 may stay in
+  // flight), barrier, read the fragments of 0
+#pragma unroll
+  for (int p = 0; p < G; ++p) piece(0, p);
+  if (nh > 1) {
+#pragma unroll
+    for (int p = 0; p < G; ++p) piece(1, p);
+  }
+  if (nh > 2) {
+#pragma unroll
+    for (int p = 0; p < G; ++p) piece(2, p);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int r = 0; r < R; ++r) read_next(smem, 0, r);
+
+  // one k-step; MORE: a step h + 1 exists (read it, then wait + barrier); MORE3: half-stage h + 3 exists (DMA it)
+  auto kstep = [&](int h, auto cur_c, auto more_c, auto more3_c) __attribute__((always_inline)) {
+    constexpr bool MORE = decltype(more_c)::value, MORE3 = decltype(more3_c)::value;
+    const bool csk = do_colsum && h >= cs0 && h < cs1;
+    block(cur_c, more_c, more3_c, smem + ((h + 1) & 3) * STAGE, h + 3, csk);
+    if constexpr (MORE) {
+      // this wave's reads of h + 1 retired and its pieces of h + 2 landed (h + 3's may stay in flight)
+      if constexpr (MORE3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  };
+  int h = 0;
+  for (; h + 4 < nh; h += 2) {  // pairs of steps keep the register set a compile-time constant
+    kstep(h, I0{}, T_{}, T_{});
+    kstep(h + 1, I1{}, T_{}, T_{});
+  }
+  // tail: at most 4 steps left (h even); the step flags as above, from the steps that remain
+  if (h < nh) {
+    if (h + 3 < nh) kstep(h, I0{}, T_{}, T_{});
+    else if (h + 1 < nh) kstep(h, I0{}, T_{}, F_{});
+    else kstep(h, I0{}, F_{}, F_{});
+  }
+  if (h + 1 < nh) {  // (h + 1) + 3 < nh cannot hold here
+    if (h + 2 < nh) kstep(h + 1, I1{}, T_{}, F_{});
+    else kstep(h + 1, I1{}, F_{}, F_{});
+  }
+  if (h + 2 < nh) {
+    if (h + 3 < nh) kstep(h + 2, I0{}, T_{}, F_{});
+    else kstep(h + 2, I0{}, F_{}, F_{});
+  }
+  if (h + 3 < nh) kstep(h + 3, I1{}, F_{}, F_{});
+
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
+  if (COLSUM && do_colsum && (!SPLIT || m0 == 0))
+    colsum_finish<NJ, WTN, kEpiNone, true>(
+        cs, lane, n0 + wn * WTN, ws + (SPLIT ? (int64_t)split_k * M * N + (int64_t)ksplit * N : (int64_t)im * N), wo,
+        N);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
+                                                 aux, ldaux, M, N, ksplit, ws, wo);
+  };
+  if constexpr (COLSUM) {
+    tile_body(blockIdx.x);
+  } else {
+    for (int v = blockIdx.x; v < tiles * split_k; v += gridDim.x) {
+      tile_body(v);
+      __syncthreads();
     }
   }
 }
@@ -1317,13 +1538,16 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
                            (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
                            (float*)a.workspace, a.colsum, wo);
       };
+      const bool half = gemm_half_stage_flag().load(std::memory_order_relaxed) != 0;
       if constexpr (!BKC) {
         if (a.colsum) {
-          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);
+          if (half) launch(gemm_pl4h_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);
+          else launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);
           return SPLIT ? sk : a.M / BM;
         }
       }
-      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>, true);
+      if (half) launch(gemm_pl4h_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>, true);
+      else launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>, true);
       return 0;
     }
     if ((mode == 2 || mode == 5) && aligned && (!a.colsum || a.workspace)) {

@@ -40,6 +40,14 @@ std::atomic<int>& gemm_main_loop_flag() {
   return flag;
 }
 
+std::atomic<int>& gemm_half_stage_flag() {
+  static std::atomic<int> flag{[] {
+    const char* e = getenv("FAN_GEMM_HALF");
+    return e ? atoi(e) : 0;
+  }()};
+  return flag;
+}
+
 std::atomic<int>& gemm_persist_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_PERSIST");
