@@ -430,12 +430,12 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
   // ReLU-mask epilogue: the activation reads are latency-bound (64 MB over a 190 us GEMM is no bandwidth), so the
   // loads of 16-row block i + kPf are issued before block i is staged and stored; each lane keeps kPf + 1 blocks
   // of 4-element activation chunks in registers (bwd-data 8192x4096: 19 us of exposed load latency otherwise).
-  // bf16 outputs: 8 columns (16 B) per lane and store (epi8_bf16) when every pointer the lanes touch is 16-B aligned
-  // (a uniform run-time branch; else the 8-B path below)
+  // bf16 outputs: 8 columns (16 B) per lane and store (epi8_bf16). C, bias and the activation must be 16-B aligned
+  // with ldc, ldaux % 8 == 0 (launch_gemm_bf16 checks; ops/gemm.py stages misaligned operands through aligned
+  // copies). One path only: keeping the 8-B path beside it as a run-time fallback spilled 20-33 VGPRs in the
+  // persistent kernels.
   if constexpr (sizeof(TC) == 2 && !SPLIT && !is_wire_epi(EPI)) {
-    const bool wide = (((uintptr_t)C | (uintptr_t)bias | (uintptr_t)aux) & 15) == 0 && (ldc & 7) == 0 &&
-                      (EPI != kEpiReluMask || (ldaux & 7) == 0);
-    if (wide) {
+    {
       constexpr int C8 = WTN / 8;   // 16-B chunks per staged row
       constexpr int RP8 = 64 / C8;  // rows per pass
       constexpr int NP8 = 16 / RP8;
@@ -1179,7 +1179,12 @@ __global__ void __launch_bounds__(256, 1)
 //   k-step h: MFMAs on the fragments of half-stage h (registers, set h & 1); under them the fragments of h + 1 are
 //   read (stage (h + 1) % 4, set (h + 1) & 1) and the DMA of half-stage h + 3 goes into stage (h + 3) % 4 = the
 //   stage of h - 1, whose reads every wave retired before the barrier that ended k-step h - 2; then lgkmcnt(0) +
-//   vmcnt(8) (this wave's pieces of h + 2 landed; those of h + 3 may stay in flight) and ONE barrier.
+//   vmcnt(8) (this wave's pieces of h + 2 landed; those of h + 3 may stay in flight) and ONE barrier (asm
+//   s_barrier with a memory clobber: the builtin does not stop the compiler from hoisting LDS reads above it).
+// Every step runs the same body (reads and fetch clamped past the end): one loop, 178 VGPRs, no spills.
+// MEASURED SLOWER (profiles/r4_gemm_half_stage_ab.jsonl: +4.8 % on the 8192x4096x4096 forward, +8.3 % on the
+// flagship step): the extra barrier per K-tile and the half-size DMA bursts cost more than the issue clustering they
+// remove. Kept opt-in (FAN_GEMM_HALF=1) and bit-identical (tests/test_gpu_gemm_half_stage.py).
 // A half-stage's DMA has two k-steps to land, as before. Images: K-contiguous operands as [rows][32 k] (64-B rows,
 // 16-B chunk c of row r at slot c ^ ((r >> 1) & 3): conflict-free ds_read_b128), MN-contiguous ones as
 // [32 k][128 columns] per 128-column half (the ds_read_b64_tr_b16 image of gemm_pl4_kernel, 32 k-rows). The
@@ -1283,16 +1288,17 @@ __global__ void __launch_bounds__(256, 1)
   const char* a_k0 = reinterpret_cast<const char*>(A) + (AK ? (int64_t)kbeg * 2 : (int64_t)kbeg * lda * 2);
   const char* b_k0 = reinterpret_cast<const char*>(B) + (BKC ? (int64_t)kbeg * 2 : (int64_t)kbeg * ldb * 2);
 
-  auto piece = [&](int h, int p) __attribute__((always_inline)) {
-    const uint32_t st = lds0 + (h & 3) * STAGE + wave * 1024;
-    if (p < GA) glds16_s(a_k0 + h * a_step, off[p], st + p * IB);
-    else glds16_s(b_k0 + h * b_step, off[p], st + A_BYTES + (p - GA) * IB);
+  // glds piece p of half-stage `src` (clamped by the caller to the last one) into LDS stage `stg` & 3
+  auto piece = [&](int stg, int src, int p) __attribute__((always_inline)) {
+    const uint32_t st = lds0 + (stg & 3) * STAGE + wave * 1024;
+    if (p < GA) glds16_s(a_k0 + src * a_step, off[p], st + p * IB);
+    else glds16_s(b_k0 + src * b_step, off[p], st + A_BYTES + (p - GA) * IB);
   };
   auto read_next = [&](const char* st, int set, int r) __attribute__((always_inline)) {
     if (r < MI) fa[set][r] = read_frag_h<AK>(st, wm * WTM + r * 16, lane);
     else fb[set][r - MI] = read_frag_h<BKC>(st + A_BYTES, wn * WTN + (r - MI) * 16, lane);
   };
-  auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int dma_h,
+  auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int dma_stg, int dma_src,
                    bool csk) __attribute__((always_inline)) {
     constexpr int cur = decltype(cur_c)::value;
     constexpr bool READ = decltype(read_c)::value, DMA = decltype(dma_c)::value;
@@ -1302,7 +1308,7 @@ __global__ void __launch_bounds__(256, 1)
       constexpr int q = decltype(qc)::value;
       if constexpr (READ && q % RSP == 0 && q / RSP < R) read_next(rd_st, cur ^ 1, q / RSP);
 #ifndef FAN_GEMM_NODMA
-      if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_h, q / DSP);
+      if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_stg, dma_src, q / DSP);
 #endif
       mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
     });
@@ -1312,57 +1318,32 @@ __global__ void __launch_bounds__(256, 1)
   using T_ = std::true_type;
   using F_ = std::false_type;
 
-  // prologue: half-stages 0, 1, 2 in flight; retire 0 AND 1 (step 0 reads the fragments of 1; only 2 may stay in
-  // flight), barrier, read the fragments of 0
+  // prologue: half-stages 0, 1, 2 in flight (past the end: the last one again); retire 0 AND 1 (step 0 reads the
+  // fragments of 1; only 2 may stay in flight), barrier, read the fragments of 0
 #pragma unroll
-  for (int p = 0; p < G; ++p) piece(0, p);
-  if (nh > 1) {
+  for (int p = 0; p < G; ++p) piece(0, 0, p);
 #pragma unroll
-    for (int p = 0; p < G; ++p) piece(1, p);
-  }
-  if (nh > 2) {
+  for (int p = 0; p < G; ++p) piece(1, min(1, nh - 1), p);
 #pragma unroll
-    for (int p = 0; p < G; ++p) piece(2, p);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
+  for (int p = 0; p < G; ++p) piece(2, min(2, nh - 1), p);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  asm volatile("s_barrier" ::: "memory");
 #pragma unroll
   for (int r = 0; r < R; ++r) read_next(smem, 0, r);
 
-  // one k-step; MORE: a step h + 1 exists (read it, then wait + barrier); MORE3: half-stage h + 3 exists (DMA it)
-  auto kstep = [&](int h, auto cur_c, auto more_c, auto more3_c) __attribute__((always_inline)) {
-    constexpr bool MORE = decltype(more_c)::value, MORE3 = decltype(more3_c)::value;
+  // one k-step h (set h & 1): the fragments of h + 1 are read and half-stage h + 3 is fetched on EVERY step; past
+  // the end both are clamped to valid memory (the last half-stage fetched again into a consumed stage, fragments
+  // nobody uses), which keeps one loop body (a tail with compile-time flags doubles the live ranges: spills)
+  auto kstep = [&](int h, auto cur_c) __attribute__((always_inline)) {
     const bool csk = do_colsum && h >= cs0 && h < cs1;
-    block(cur_c, more_c, more3_c, smem + ((h + 1) & 3) * STAGE, h + 3, csk);
-    if constexpr (MORE) {
-      // this wave's reads of h + 1 retired and its pieces of h + 2 landed (h + 3's may stay in flight)
-      if constexpr (MORE3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
+    block(cur_c, T_{}, T_{}, smem + ((h + 1) & 3) * STAGE, h + 3, min(h + 3, nh - 1), csk);
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
+    asm volatile("s_barrier" ::: "memory");
   };
-  int h = 0;
-  for (; h + 4 < nh; h += 2) {  // pairs of steps keep the register set a compile-time constant
-    kstep(h, I0{}, T_{}, T_{});
-    kstep(h + 1, I1{}, T_{}, T_{});
+  for (int h = 0; h < nh; h += 2) {  // nh is even (K % 64 == 0): pairs keep the register set a constant
+    kstep(h, I0{});
+    kstep(h + 1, I1{});
   }
-  // tail: at most 4 steps left (h even); the step flags as above, from the steps that remain
-  if (h < nh) {
-    if (h + 3 < nh) kstep(h, I0{}, T_{}, T_{});
-    else if (h + 1 < nh) kstep(h, I0{}, T_{}, F_{});
-    else kstep(h, I0{}, F_{}, F_{});
-  }
-  if (h + 1 < nh) {  // (h + 1) + 3 < nh cannot hold here
-    if (h + 2 < nh) kstep(h + 1, I1{}, T_{}, F_{});
-    else kstep(h + 1, I1{}, F_{}, F_{});
-  }
-  if (h + 2 < nh) {
-    if (h + 3 < nh) kstep(h + 2, I0{}, T_{}, F_{});
-    else kstep(h + 2, I0{}, F_{}, F_{});
-  }
-  if (h + 3 < nh) kstep(h + 3, I1{}, F_{}, F_{});
 
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll

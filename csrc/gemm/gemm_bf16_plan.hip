@@ -248,6 +248,13 @@ bool gemm_bf16_supported(const GemmArgs& a) {
 void launch_gemm_bf16(const GemmArgs& a, hipStream_t s) {
   FAN_CHECK(gemm_bf16_supported(a), "gemm_bf16: unsupported shape/layout (need M, N, K % 8 == 0)");
   const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn, a.tile_waves);
+  if (a.c_bf16 && !a.wire) {  // the bf16 epilogue stores 8 columns (16 B) per lane (store_tile, epi8_bf16)
+    const bool mask = a.epilogue == kEpiReluMask;
+    const bool bias = a.epilogue == kEpiBias || a.epilogue == kEpiBiasRelu;
+    FAN_CHECK(((uintptr_t)a.C & 15) == 0 && a.ldc % 8 == 0 && (!bias || ((uintptr_t)a.bias & 15) == 0) &&
+                  (!mask || (((uintptr_t)a.aux & 15) == 0 && a.ldaux % 8 == 0)),
+              "gemm_bf16: bf16 output, bias and activation must be 16-B aligned with ldc, ldaux % 8 == 0");
+  }
   if (a.a_kcontig && a.b_kcontig) launch_tile<true, true>(a, p.bm, p.bn, p.waves, p.split_k, s);
   else if (a.a_kcontig && !a.b_kcontig) launch_tile<true, false>(a, p.bm, p.bn, p.waves, p.split_k, s);
   else if (!a.a_kcontig && a.b_kcontig) launch_tile<false, true>(a, p.bm, p.bn, p.waves, p.split_k, s);

@@ -79,6 +79,15 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
             _nn.col_sum(B.t() if b_t else B, colsum)
             return C
         if A.dtype == torch.bfloat16:
+            if C.dtype == torch.bfloat16 and not _aligned16(C, bias, aux):
+                # the bf16 epilogue stores 16 B per lane: stage misaligned operands through aligned copies
+                Ct = torch.empty(C.shape, dtype=C.dtype, device=C.device)
+                if accumulate:
+                    Ct.copy_(C)
+                _bf16(Cx, A, a_t, B, b_t, Ct, epilogue, None if bias is None else bias.clone(),
+                      None if aux is None else aux.contiguous().clone(), accumulate, split_k, tile, colsum, None)
+                C.copy_(Ct)
+                return C
             _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, None)
             return C
         M = A.shape[1] if a_t else A.shape[0]
@@ -107,6 +116,16 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     if colsum is not None:
         colsum.copy_(b.sum(0).to(colsum.dtype))
     return C
+
+
+def _aligned16(C, bias, aux) -> bool:
+    """A bf16 output's epilogue stores (and the bias / activation loads beside them) are 16 B per lane."""
+    ok = C.data_ptr() % 16 == 0 and C.stride(0) % 8 == 0
+    if bias is not None:
+        ok = ok and bias.data_ptr() % 16 == 0
+    if aux is not None:
+        ok = ok and aux.data_ptr() % 16 == 0 and aux.stride(0) % 8 == 0
+    return ok
 
 
 def _shares_storage(C, *ts) -> bool:

@@ -1,7 +1,9 @@
 """Probe: the bf16 GEMM epilogue's store width, A/B in one process. The epilogue writes 8 columns (16 B) per lane when
 C, bias and the activation are 16-B aligned (store_tile, epi8_bf16) and 4 columns (8 B) otherwise; a C view offset
 by 8 bytes forces the 8-B path with the same kernel, shape and operands. Also checks both paths give the same
-bits. Shapes: the flagship's bf16-output GEMMs (fwd with bias + ReLU, bwd-data with the ReLU mask)."""
+bits. Shapes: the flagship's bf16-output GEMMs (fwd with bias + ReLU, bwd-data with the ReLU mask).
+(Historical: the run in profiles/r4_gemm_store_width_ab.jsonl predates the removal of the 8-B path — keeping both
+spilled VGPRs — so today a misaligned C is staged through an aligned copy by ops/gemm.py and "us_8B" times that.)"""
 import json
 import os
 import statistics
