@@ -25,7 +25,7 @@ def _json_lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
 
 
-@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("world", [1, 2, 4])
 def test_bench_json_contract(world, tmp_path):
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
             "--mb-per-gpu", "16"]
@@ -51,6 +51,18 @@ def test_bench_json_contract(world, tmp_path):
     # value is the whole-job aggregate: global batch x steps / (max-over-ranks) elapsed time
     assert rec["value"] == pytest.approx(cfg["global_batch"] / (rec["ms_per_step"] / 1e3), rel=1e-2)
     assert rec["extra"]["final_loss"] > 0
+    ex = rec["extra"]
+    if world > 1:
+        # the self-selection machinery the driver's multi-GPU run relies on, rehearsed over gloo ranks: one A/B arm
+        # (the Python engine on CPU), chosen, gate-checked bit-exact on every rank; every extra recorded
+        ab = ex["schedule_ab"]
+        assert len(ab) == 1 and ab[0].get("chosen") and ab[0]["exact"] is True, ab
+        g = ex["dist"]["allreduce_gate"]
+        assert g["exact"] and g["checked"] and g["max_abs_diff"] == 0.0, g
+        assert ex["dist"]["replicas_identical"] is True
+        assert ex["uncompressed"]["torch_f32"]["ms_per_step"] > 0 and ex["uncompressed"]["speedup_vs_best_uncompressed"]
+        assert ex["config4"] == {"skipped": "CPU run"} and ex["config5"] == {"skipped": "CPU run"}
+        assert cfg["schedule"] == ab[0]["arm"]
 
 
 def test_bench_self_launches_ranks(tmp_path):
