@@ -19,6 +19,7 @@ Reference: the NIC ring links (hw/all_reduce.sv ETH ports; sw/setup_route.sh) + 
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from typing import Sequence
@@ -224,15 +225,35 @@ def try_p2p_comm(slot_bytes: int = 128 << 20, depth: int = 4):
         errs = [None] * world
         dist.all_gather_object(errs, err)
         return None, next((e for e in errs if e), "a rank could not create its arena")
-    try:
-        comm.connect(blobs)
-    except Exception as e:  # noqa: BLE001
-        err = f"rank {rank}: {e}"
+    # The IPC imports run in a helper thread with a bound (FAN_P2P_CONNECT_TIMEOUT, default 60 s): an import that
+    # never returns (as a 2 GiB arena's did on one GPU, p2p_comm.h kMaxArenaBytes) then costs this transport, not
+    # the run — every rank learns it below and the caller continues on the others. A stuck communicator is kept
+    # referenced (its destructor would close the handles the stuck call is opening).
+    out = {}
+
+    def _connect():
+        try:
+            comm.connect(blobs)  # releases the GIL
+        except Exception as e:  # noqa: BLE001
+            out["err"] = f"rank {rank}: {e}"
+
+    limit = float(os.environ.get("FAN_P2P_CONNECT_TIMEOUT", "60"))
+    th = threading.Thread(target=_connect, name="p2p-connect", daemon=True)
+    th.start()
+    th.join(limit)
+    if th.is_alive():
+        _STUCK.append(comm)
+        err = f"rank {rank}: P2P connect (IPC import of the peers' arenas) did not return within {limit:.0f} s"
+    else:
+        err = out.get("err")
     errs = [None] * world
     dist.all_gather_object(errs, err)
     if any(errs):
         return None, next(e for e in errs if e)
     return comm, None
+
+
+_STUCK: list = []  # communicators whose connect() never returned (never destroyed)
 
 
 def try_native_transport(force_collectives: bool = False):

@@ -110,3 +110,16 @@ def test_bench_survives_a_hung_transport(tmp_path):
     assert "exceeded" not in r.stderr, r.stderr[-4000:]  # the watchdog never fired
     assert "P2P transport unavailable: aborted after arm p2p_mesh_persistent" in r.stderr, r.stderr[-4000:]
     assert took < 150, took
+
+
+def test_bench_survives_a_stuck_p2p_connect(tmp_path):
+    """The P2P bootstrap's IPC imports are bounded (FAN_P2P_CONNECT_TIMEOUT; a 2 GiB arena's import once never
+    returned): with a zero bound every rank reports the connect as stuck, all ranks drop the P2P transport together
+    and its arms are excluded with that error instead of the run hanging in connect()."""
+    os.environ["FAN_P2P_CONNECT_TIMEOUT"] = "0"
+    try:
+        r, recs = _bench(tmp_path, "--extra-budget", "0", timeout=300)
+    finally:
+        os.environ.pop("FAN_P2P_CONNECT_TIMEOUT", None)
+    assert r.returncode not in (0, 124) and not recs, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+    assert "did not return within 0 s" in r.stderr, r.stderr[-4000:]
