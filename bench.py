@@ -313,6 +313,22 @@ def main(argv=None):
         finally:
             gc.enable()
 
+    def _finish(trainer, wait_s):
+        """trainer.finish(); with a bound (A/B arms) the outcome is agreed over every rank first, so a rank whose
+        request failed and a rank whose request completed (one rank's abort can release another's waits) raise at
+        the same point instead of meeting at different collectives."""
+        if wait_s is None:
+            trainer.finish()
+            return
+        err = None
+        try:
+            trainer.finish(wait_s)
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {rank}: {e}"
+        err = next((x for x in D.all_gather_object(err) if x), None)
+        if err:
+            raise RuntimeError(err[:600])
+
     def _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace, wait_s=None):
         trainer, model, engine = setup.trainer, setup.model, setup.engine
         x, y = batch(mb, seed)
@@ -321,7 +337,7 @@ def main(argv=None):
             time.sleep(float(os.environ.get("FAN_BENCH_STALL_S", "600")))
         for _ in range(warmup):
             trainer.step(x, y)
-        trainer.finish(wait_s)  # wait_s: an A/B arm's bound (a hung transport raises instead of parking the rank)
+        _finish(trainer, wait_s)  # wait_s: an A/B arm's bound (a hung transport raises instead of parking the rank)
         wd.arm(f"{tag} mb={mb}")
         step = lambda: trainer.step(x, y)  # noqa: E731
         graphed = False
@@ -349,7 +365,7 @@ def main(argv=None):
             step()
         loss_rows = model.loss_rows
         t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
-        trainer.finish(wait_s)
+        _finish(trainer, wait_s)
         if cuda:
             torch.cuda.synchronize()
         D.barrier()

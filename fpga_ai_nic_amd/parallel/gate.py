@@ -76,9 +76,16 @@ def allreduce_exactness(engine, *, n: int = 1 << 20, seed: int = 20260417, prepa
             _ext.require().wire_pack_range(g, buf, shard, 0, n, cid)
             kw["prepacked"] = (buf, L.n_pad)
             used_pre = True
-    engine.allreduce(g, out, n_valid=n, **kw).synchronize(timeout_s)
-    if g.is_cuda:
-        torch.cuda.synchronize(dev)
+    err = None
+    try:
+        engine.allreduce(g, out, n_valid=n, **kw).synchronize(timeout_s)
+        if g.is_cuda:
+            torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001 - agreed below: a rank whose request failed must not leave its peers
+        err = f"rank {rank}: {e}"  # at a different collective (one rank's abort can let another's request finish)
+    err = next((x for x in D.all_gather_object(err) if x), None)
+    if err:
+        raise RuntimeError(f"exactness gate request failed: {err}"[:600])
     got = out[:n].cpu().numpy()
     ref = reference_sum(engine, grads, n, rank)
     mine = {"checked": ref is not None, "exact": True, "max_abs_diff": 0.0}
