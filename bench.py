@@ -170,7 +170,7 @@ def main(argv=None):
 
     t_begin = time.perf_counter()
     # watchdog: every phase of the run is bounded; on expiry the engine state goes to stderr and the rank exits 124
-    held = {"engine": None, "comm": None, "transport": None}
+    held = {"engine": None, "comm": None, "transport": None, "record": None}
     env_rank = int(os.environ.get("RANK", "0"))
 
     def _dump():
@@ -183,6 +183,12 @@ def main(argv=None):
         return d
 
     def _abort():
+        ph = wd.phase or ""
+        if env_rank == 0 and held.get("record") is not None and (ph.startswith("extra") or ph == "verify"):
+            try:  # one JSON line with the headline measured before the phase that hung
+                print(json.dumps(held["record"](ph)), flush=True)
+            except Exception as e:  # noqa: BLE001
+                print(f"[bench] partial record unavailable: {e!r}", file=sys.stderr, flush=True)
         for k in ("comm", "transport"):
             if held[k] is not None and hasattr(held[k], "abort"):
                 held[k].abort()
@@ -514,6 +520,77 @@ def main(argv=None):
     log(f"headline: {ms:.4f} ms/step over {a.steps} steps")
     tr = run(main_setup, mb, 1234, 1, a.steps, "traced", trace=True)[3] if can_trace else None
 
+    def record(dist_rec, extras_s, aborted=None):
+        """The JSON record (rank 0). ``aborted``: the watchdog's phase when it ends the run during the extras or the
+        verification — the headline was measured by then, so the record is printed without what did not finish."""
+        global_batch = mb * world
+        value = global_batch * a.steps / elapsed
+        flops = model.flops_per_sample() * global_batch * a.steps / elapsed
+        info = main_setup.info
+        rec = {
+            "metric": "MLP training samples/sec (1024-4096-4096-1024, BFP all-reduce + fused SGD)",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (random inputs/labels, random-init weights)",
+            "config": {
+                "model": "mlp-1024-4096-4096-1024",
+                "global_batch": global_batch,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "mb_per_gpu": mb,
+                "compress": info["compress"],
+                "rounding": a.rounding,
+                "algo": info["algo"],
+                "rings": info["rings"],
+                "transport": info["transport"],
+                "engine": impl,
+                "schedule": main_setup.name if schedule_ab is not None else "fixed",
+                "gemm_inflight": info["gemm_inflight"],
+                "p2p_copy": info["copy"],
+                # release of the peer-storing kernels' stores before each ready flag: "cp" (command processor,
+                # one-GPU default) or "block" (in-kernel, chosen by P2PComm.connect when a peer is on another GPU)
+                "p2p_release": ({0: "none", 1: "block", 2: "thread", 3: "cp"}[_release_mode()]
+                                if info["copy"] is not None else None),
+                "p2p_cross_device": bool(ctx["p2p"].cross_device) if ctx["p2p"] is not None else None,
+                "hip_graph": graphed,
+                "fused_sgd": True,
+                # world 1: dW's BFP round trip + SGD inside the bwd-weight GEMM epilogue (no separate update pass)
+                "fused_update_in_gemm": bool(getattr(trainer, "fused_update", False)),
+                "epilogue_stream": ("compute" if getattr(engine, "epilogue_on_producer", False) else "comm")
+                if engine is not None and not getattr(engine, "inline", True) else "inline",
+            },
+            "extra": {
+                "achieved_tflops": round(flops / 1e12, 2),
+                "host_enqueue_ms_per_step": round(t_enqueue / a.steps * 1e3, 4),
+                "grad_bytes_f32_per_step": sum(l.n for l in model.layers) * 4,
+                "allreduce": _allreduce_report(tr, world),
+                f"mb{a.ref_mb}": ref,
+                "final_loss": round(loss, 5),
+                "schedule_ab": schedule_ab,
+                "gates_failed": [{"arm": g["arm"], "max_abs_diff": g.get("max_abs_diff"),
+                                  "mismatch_ranks": g.get("mismatch_ranks")} for g in gates_failed],
+                "dist": dist_rec,
+                **dict(extras),
+                "extras_s": round(extras_s, 2),
+                "run_s": round(time.perf_counter() - t_begin, 2),
+                "gemm_tuning": _tuning_report(),
+                # (not after an abort: the engine may be held by the thread the watchdog is ending)
+                **({"engine_counters": engine.counters()} if hasattr(engine, "counters") and not aborted else {}),
+                **({"aborted_in": aborted} if aborted else {}),
+            },
+        }
+        return rec
+
+    # the watchdog prints the measured headline if an extra or the verification never returns
+    held["record"] = lambda phase: record(None, time.perf_counter() - t_extra0, aborted=phase)
     # ------------------------------------------------------------------ extras (bounded)
     extras = {}
 
@@ -528,6 +605,9 @@ def main(argv=None):
             return
         wd.arm(f"extra {name}")
         log(f"extra {name}")
+        stall = os.environ.get("FAN_BENCH_STALL_EXTRA", "")  # test hook "<extra>:<rank>": that rank stops there
+        if stall and stall.rsplit(":", 1)[0] == name and int(stall.rsplit(":", 1)[1]) == rank:
+            time.sleep(600)
         try:
             extras[name] = fn()
         except Exception as ex:  # noqa: BLE001 - an extra never costs the headline its record
@@ -589,70 +669,8 @@ def main(argv=None):
     dist_rec = _dist_report(main_setup, world, rank, device, D, gate_rec)
     wd.disarm()
 
-    global_batch = mb * world
-    value = global_batch * a.steps / elapsed
-    flops = model.flops_per_sample() * global_batch * a.steps / elapsed
-    info = main_setup.info
     if rank == 0:
-        rec = {
-            "metric": "MLP training samples/sec (1024-4096-4096-1024, BFP all-reduce + fused SGD)",
-            "value": round(value, 2),
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(ms, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": a.dtype,
-            "data": "synthetic (random inputs/labels, random-init weights)",
-            "config": {
-                "model": "mlp-1024-4096-4096-1024",
-                "global_batch": global_batch,
-                "seq_len": None,
-                "parallelism": f"dp{world}",
-                "mb_per_gpu": mb,
-                "compress": info["compress"],
-                "rounding": a.rounding,
-                "algo": info["algo"],
-                "rings": info["rings"],
-                "transport": info["transport"],
-                "engine": impl,
-                "schedule": main_setup.name if schedule_ab is not None else "fixed",
-                "gemm_inflight": info["gemm_inflight"],
-                "p2p_copy": info["copy"],
-                # release of the peer-storing kernels' stores before each ready flag: "cp" (command processor,
-                # one-GPU default) or "block" (in-kernel, chosen by P2PComm.connect when a peer is on another GPU)
-                "p2p_release": ({0: "none", 1: "block", 2: "thread", 3: "cp"}[_release_mode()]
-                                if info["copy"] is not None else None),
-                "p2p_cross_device": bool(ctx["p2p"].cross_device) if ctx["p2p"] is not None else None,
-                "hip_graph": graphed,
-                "fused_sgd": True,
-                # world 1: dW's BFP round trip + SGD inside the bwd-weight GEMM epilogue (no separate update pass)
-                "fused_update_in_gemm": bool(getattr(trainer, "fused_update", False)),
-                "epilogue_stream": ("compute" if getattr(engine, "epilogue_on_producer", False) else "comm")
-                if engine is not None and not getattr(engine, "inline", True) else "inline",
-            },
-            "extra": {
-                "achieved_tflops": round(flops / 1e12, 2),
-                "host_enqueue_ms_per_step": round(t_enqueue / a.steps * 1e3, 4),
-                "grad_bytes_f32_per_step": sum(l.n for l in model.layers) * 4,
-                "allreduce": _allreduce_report(tr, world),
-                f"mb{a.ref_mb}": ref,
-                "final_loss": round(loss, 5),
-                "schedule_ab": schedule_ab,
-                "gates_failed": [{"arm": g["arm"], "max_abs_diff": g.get("max_abs_diff"),
-                                  "mismatch_ranks": g.get("mismatch_ranks")} for g in gates_failed],
-                "dist": dist_rec,
-                **extras,
-                "extras_s": round(extras_s, 2),
-                "run_s": round(time.perf_counter() - t_begin, 2),
-                "gemm_tuning": _tuning_report(),
-                **({"engine_counters": engine.counters()} if hasattr(engine, "counters") else {}),
-            },
-        }
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(record(dist_rec, extras_s)), flush=True)
     wd.arm("cleanup")
     D.cleanup()
     wd.close()

@@ -94,3 +94,21 @@ def test_bench_watchdog_ends_a_hung_run(tmp_path):
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode != 0 and not _json_lines(r.stdout)
     assert "phase 'warmup timed mb=16' exceeded 15 s" in r.stderr, r.stderr[-3000:]
+
+
+def test_bench_prints_the_headline_when_an_extra_hangs(tmp_path):
+    """Rank 1 stops inside an extra (test hook FAN_BENCH_STALL_EXTRA): rank 0 waits in that extra's next collective
+    until its watchdog fires — which prints the record of the headline measured before (one JSON line, the phase it
+    was aborted in) before ending the run, instead of losing the measurement."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--mb-per-gpu", "16", "--ref-mb", "0", "--timeout", "20"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               FAN_BENCH_STALL_EXTRA="uncompressed:1")
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, (r.stdout, r.stderr[-3000:])
+    rec = recs[0]
+    assert rec["extra"]["aborted_in"] == "extra uncompressed" and rec["value"] > 0 and rec["n_gpus"] == 2
+    assert "config4" in rec["extra"] and rec["extra"]["dist"] is None
