@@ -412,7 +412,8 @@ def main(argv=None):
             # last resort, never the fastest: the Python-issued engine over the control plane's own collectives
             # (torch.distributed), so a run whose native transports all fail their gate or hang still records a
             # gate-checked compressed step instead of no line at all
-            arms.append(dict(name="torch_mesh_python", kind="bfp", algo="mesh", transport="torch", engine="python"))
+            arms.append(dict(name="torch_mesh_python", kind="bfp", algo="mesh", transport="torch", engine="python",
+                             fallback=True))
         else:
             arms.append(dict(name=f"{impl}_{a.algo}", kind="bfp", algo=a.algo, rings=a.rings, transport="torch"))
         schedule_ab = []
@@ -420,6 +421,9 @@ def main(argv=None):
         best = None
         arm_wait = min(eng_timeout, a.arm_timeout)  # gate and A/B waits: below the watchdog's per-phase budget
         for spec in arms:
+            if spec.get("fallback") and best is not None:  # identical on every rank (agreed results and times)
+                schedule_ab.append({"arm": spec["name"], "skipped": "a faster exact arm passed"})
+                continue
             wd.arm(f"schedule A/B {spec['name']}")
             rec = {"arm": spec["name"]}
             setup = None
