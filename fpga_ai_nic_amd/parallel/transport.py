@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import os
 import threading
-import time
 from typing import Sequence
 
 import torch
