@@ -246,7 +246,7 @@ def main(argv=None):
         return ctx["p2p"]
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
-              force=False, panels=None, ring_sub=1, epi=None, engine=None):
+              force=False, panels=None, ring_sub=0, epi=None, engine=None):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default); engine: python | native (default: the run's)."""
         comm = None
