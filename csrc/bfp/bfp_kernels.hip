@@ -38,8 +38,10 @@ void set_p2p_release_mode(int mode) { release_mode_flag().store(mode < 0 ? 0 : m
 
 // Grid cap of the kernels that store into peers' receive arenas (FAN_P2P_GRID; 0 = auto): with the in-kernel
 // release forms every workgroup ends with one system-scope release, so fewer, longer-lived workgroups pay fewer of
-// them (512); with the command-processor release (default) nothing is paid per workgroup and the cap is the
-// ordinary one (profiles/r3_wire_store_bw.jsonl: 8 shards packed into the arena 18.95 us at 512 vs 17.39 at 2048).
+// them — "block" (the cross-device default) 128: 2 ranks, 2.27 ms/step at 64-128 workgroups vs 2.36 at 256, 2.49 at
+// 512, 2.63 at 1024, 2.83 at 2048, i.e. the whole cost of the in-kernel release over "cp" (2.27)
+// (profiles/r4_p2p_block_grid_sweep.jsonl); "thread" 512; with the command-processor release nothing is paid per
+// workgroup and the cap is the ordinary one (profiles/r3_wire_store_bw.jsonl: 18.95 us at 512 vs 17.39 at 2048).
 static std::atomic<int>& p2p_grid_flag() {
   static std::atomic<int> g{[] {
     const char* e = getenv("FAN_P2P_GRID");
@@ -51,7 +53,7 @@ int p2p_grid_cap() {
   const int g = p2p_grid_flag().load(std::memory_order_relaxed);
   if (g > 0) return g;
   const int m = p2p_release_mode();
-  return m == 1 || m == 2 ? 512 : wire_max_blocks();
+  return m == 1 ? 128 : m == 2 ? 512 : wire_max_blocks();
 }
 void set_p2p_grid_cap(int blocks) { p2p_grid_flag().store(blocks > 0 ? blocks : 0); }
 
