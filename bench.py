@@ -57,6 +57,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="GPU: before the headline's W warmup steps, untimed steps of the same batch until this much "
+                         "wall time has passed (the shader clock's ramp; extra.settle); 0 = off")
     # per-GPU minibatch (weak scaling). The reference fixes only the architecture for this config; 8192 rows per
     # GPU keeps the MFMA GEMMs out of the tile-quantisation regime (measured: 2048 -> 4.6M samples/s,
     # 8192 -> 7.2M samples/s on one MI355X) and gives the overlapped all-reduce a ~1.1 ms backward to hide in.
@@ -304,6 +307,7 @@ def main(argv=None):
         return x, y
 
     stall_rank = int(os.environ.get("FAN_BENCH_STALL_RANK", "-1"))
+    settle = {}  # the headline's untimed settle steps (extra.settle)
 
     def run(setup, mb, seed, warmup, steps, tag, graph_ok=False, trace=False, wait_s=None):
         """W warmup + K timed steps of ``setup`` at per-GPU batch mb: (elapsed s max over ranks, host enqueue s,
@@ -339,6 +343,21 @@ def main(argv=None):
         trainer, model, engine = setup.trainer, setup.model, setup.engine
         x, y = batch(mb, seed)
         wd.arm(f"warmup {tag} mb={mb}")
+        if tag == "timed" and cuda and a.settle_ms > 0:
+            # The shader clock needs ~50 ms of sustained load to reach the level a training run holds: the driver's
+            # 5 warmup + 20 steps read 1.038-1.047 ms/step where 50 + 20 read 0.989 and 5 + 100 0.996
+            # (profiles/r4_warmup_settle.jsonl). Untimed steps of the same batch in chunks of 10 until settle_ms
+            # passed (the chunk count agreed over ranks, so every rank runs the same steps); then W + K as ever.
+            t_s, n_s = time.perf_counter(), 0
+            while n_s < 5000:
+                for _ in range(10):
+                    trainer.step(x, y)
+                n_s += 10
+                _finish(trainer, wait_s)
+                torch.cuda.synchronize()
+                if D.max_over_ranks(time.perf_counter() - t_s) * 1e3 >= a.settle_ms:
+                    break
+            settle.update(steps=n_s, ms=round((time.perf_counter() - t_s) * 1e3, 1))
         if stall_rank == rank and tag == "timed":  # test hook: this rank stops taking part (a hung peer)
             time.sleep(float(os.environ.get("FAN_BENCH_STALL_S", "600")))
         for _ in range(warmup):
@@ -574,6 +593,7 @@ def main(argv=None):
             "extra": {
                 "achieved_tflops": round(flops / 1e12, 2),
                 "host_enqueue_ms_per_step": round(t_enqueue / a.steps * 1e3, 4),
+                "settle": settle or None,
                 "grad_bytes_f32_per_step": sum(l.n for l in model.layers) * 4,
                 "allreduce": _allreduce_report(tr, world),
                 f"mb{a.ref_mb}": ref,
