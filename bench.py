@@ -10,7 +10,8 @@ communication phase, ``extra.allreduce``).
 Contract: ``python bench.py --gpus N --steps K --warmup W``. Under torch.distributed.run (RANK / WORLD_SIZE set)
 every process is one rank on one GPU over RCCL. Without that environment and N > 1, this script starts
 ``torch.distributed.run --nproc-per-node N`` itself as a CHILD process before anything touches the GPU, and
-exits with its code (the parent never initialises HIP). W untimed warmup steps, then EXACTLY K timed steps
+exits with its code (the parent never initialises HIP). On the GPU, untimed steps of the headline batch for
+``--settle-ms`` (300 ms: the shader clock's ramp, ``extra.settle``); then W untimed warmup steps and EXACTLY K timed steps
 bracketed by barrier + torch.cuda.synchronize() on both sides; max time over ranks; rank 0 prints ONE JSON line.
 
 World > 1 (GPU): the run chooses its own schedule and checks it before timing anything (``--schedule auto``):
