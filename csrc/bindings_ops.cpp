@@ -204,6 +204,9 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_set_half_stage", [](int on) { gemm_half_stage_flag().store(on); },
         "256x256 persistent 4-wave loop: ring of four 32-k half-stages (1) or two 64-k stages (0)");
   m.def("gemm_half_stage", []() { return gemm_half_stage_flag().load(); });
+  m.def("gemm_set_fixup", [](int on) { gemm_fixup_flag().store(on); },
+        "split-K wire epilogues: in-GEMM last-workgroup fixup (1) or the separate slab reduce kernel (0)");
+  m.def("gemm_fixup", []() { return gemm_fixup_flag().load(); });
   m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {
           gemm_set_stamp_buffer(t ? t->data_ptr() : nullptr);
         },

@@ -85,6 +85,14 @@ std::atomic<int>& gemm_persist_flag();
 // 256x256 persistent 4-wave loop on the ring of four 32-k half-stages (gemm_pl4h_kernel) instead of two 64-k stages
 // (FAN_GEMM_HALF, gemm_set_half_stage)
 std::atomic<int>& gemm_half_stage_flag();
+// split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
+// separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
+// gemm_set_fixup); bit-identical either way
+std::atomic<int>& gemm_fixup_flag();
+// per-(device, stream) tile counters of that in-GEMM split-K fixup (kFixTiles entries, zero between launches: the
+// last workgroup of a tile resets its counter); nullptr while the stream is capturing and none exists yet
+unsigned* gemm_fix_counters(hipStream_t s);
+constexpr int kFixTiles = 4096;
 // diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
 void gemm_set_stamp_buffer(void* p);
 void* gemm_stamp_buffer();

@@ -261,6 +261,9 @@ struct WireOut {
   bf16_t* ulp;
   float* umom;
   SgdParams up;
+  // split-K with a wire epilogue: per-tile arrival counters of the in-GEMM fixup (split_fixup; nullptr: the slabs
+  // are reduced by splitk_reduce_wire_kernel)
+  unsigned* fix;
 #ifdef FAN_GEMM_STAMPS
   unsigned long long* stamps;  // diagnostic builds: s_memtime stamp buffer (see FAN_STAMP)
 #endif
@@ -370,6 +373,83 @@ __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict_
 #pragma unroll
     for (int u = 0; u < 16; u += 4)
       *reinterpret_cast<float4*>(C + f + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
+  }
+}
+
+// In-GEMM split-K fixup of the wire epilogues (gemm_pl4_kernel, wo.fix set): every workgroup of a tile has stored
+// its slab (and, in tile row 0, its bias partial sums); the LAST of the tile's split_k workgroups to get here — an
+// agent-scope arrival counter per tile, reset to 0 by that workgroup for the next launch — sums the tile's slabs in
+// split order and runs the epilogue of splitk_reduce_wire_kernel on them: the same sums in the same order, so the
+// result is bit-identical, without a second launch that re-reads every slab from memory after the GEMM drained.
+// No workgroup waits for another (the last one to arrive does the work), so co-residency is never assumed.
+// MEASURED SLOWER, so opt-in (FAN_GEMM_FIXUP=1): the flagship step 1.166-1.169 vs 1.020-1.027 ms/step
+// (profiles/r4_gemm_splitk_fixup_ab.jsonl). The 1024x4096 bwd-weight has 64 tiles, so 64 workgroups each stream
+// ~1.7 MB (four 256 KB slabs + the update planes) where the reduce kernel spreads the same bytes over every CU; and
+// every workgroup's agent-scope release writes back its XCD's L2. Bit-identical (tests/test_gpu_gemm_fixup.py).
+// The fences: each thread's slab stores are released at agent scope (written back past its XCD's L2) before the
+// counter increment; the last workgroup acquires at agent scope (its L2 invalidated) before reading the slabs that
+// workgroups on other XCDs wrote.
+template <int BMT, int BNT>
+__device__ __forceinline__ void split_fixup(int tile, int m0, int n0, const float* __restrict__ ws, int split_k,
+                                            float* __restrict__ C, int64_t ldc, int M, int N,
+                                            float* __restrict__ colsum, const WireOut& wo, char* smem) {
+  __threadfence();
+  __syncthreads();
+  int* last_flag = reinterpret_cast<int*>(smem);
+  if (threadIdx.x == 0) {
+    const unsigned old = atomicAdd(wo.fix + tile, 1u);
+    const int last = old == (unsigned)(split_k - 1);
+    if (last) atomicExch(wo.fix + tile, 0u);
+    *last_flag = last;
+  }
+  __syncthreads();
+  if (!*last_flag) return;
+  __threadfence();
+  const int64_t slab = (int64_t)M * N;
+  constexpr int GPR = BNT / 16;  // 16-column groups per tile row
+  for (int g = threadIdx.x; g < BMT * GPR; g += blockDim.x) {
+    const int row = m0 + g / GPR, col = n0 + (g % GPR) * 16;
+    const float* p = ws + (int64_t)row * N + col;
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(p + u);
+      v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
+    }
+    for (int k = 1; k < split_k; ++k) {
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(p + k * slab + u);
+        v[u] += q.x; v[u + 1] += q.y; v[u + 2] += q.z; v[u + 3] += q.w;
+      }
+    }
+    if (wo.um) wire_epi16<true>(v, C, ldc, wo, row, col);
+    else wire_epi16<false>(v, C, ldc, wo, row, col);
+  }
+  if (colsum && m0 == 0) {  // the bias partials of this tile's columns (written by tile row 0's workgroups)
+    for (int c = threadIdx.x; c < GPR; c += blockDim.x) {
+      const int col = n0 + c * 16;
+      const float* p = ws + (int64_t)split_k * slab + col;
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(p + u);
+        v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
+      }
+      for (int k = 1; k < split_k; ++k) {
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+          const float4 q = *reinterpret_cast<const float4*>(p + (int64_t)k * N + u);
+          v[u] += q.x; v[u + 1] += q.y; v[u + 2] += q.z; v[u + 3] += q.w;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) colsum[col + u] = v[u];
+      if (wo.bias_off > 0) {
+        if (wo.um) wire_store16<true>(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
+        else wire_store16<false>(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
+      }
+    }
   }
 }
 
@@ -1158,6 +1238,9 @@ __global__ void __launch_bounds__(256, 1)
   __syncthreads();  // every operand read retired before the epilogue reuses the LDS
   store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
                                                  aux, ldaux, M, N, ksplit, ws, wo);
+  if constexpr (SPLIT && is_wire_epi(EPI)) {
+    if (wo.fix) split_fixup<BM, BN>(tile, m0, n0, ws, split_k, reinterpret_cast<float*>(C), ldc, M, N, colsum, wo, smem);
+  }
   };
   if constexpr (COLSUM) {
     tile_body(blockIdx.x);
@@ -1358,6 +1441,9 @@ __global__ void __launch_bounds__(256, 1)
   __syncthreads();
   store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
                                                  aux, ldaux, M, N, ksplit, ws, wo);
+  if constexpr (SPLIT && is_wire_epi(EPI)) {
+    if (wo.fix) split_fixup<BM, BN>(tile, m0, n0, ws, split_k, reinterpret_cast<float*>(C), ldc, M, N, colsum, wo, smem);
+  }
   };
   if constexpr (COLSUM) {
     tile_body(blockIdx.x);
@@ -1494,9 +1580,16 @@ inline int persist_grid(int grid) {
 
 // Launches the main loop; returns the number of bias-gradient partial slabs it left in the workspace for an ordered
 // reduce (split_k with split-K; without: the pipelined loop's tile rows, 0 = colsum written by the kernel).
+// With wo.fix set (split-K wire epilogue), the 4-wave pipelined kernels reduce the slabs themselves (split_fixup)
+// and *fixed says so; every other kernel leaves them to the reduce kernel.
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
-int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
+int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, bool* fixed = nullptr) {
   const int grid = cdiv_i(a.M, BM) * cdiv_i(a.N, BN) * sk;
+  WireOut wo = wo_in;  // the kernels without the fixup get no counters
+  wo.fix = nullptr;
+  WireOut wf = wo_in;  // the 4-wave pipelined kernels'
+  if (!(SPLIT && is_wire_epi(EPI)) || grid / sk > kFixTiles) wf.fix = nullptr;
+  if (fixed) *fixed = false;
   if constexpr (BM == 256 && BN == 256 && WM * WN == 8) {
     // the pipelined loops have no edge path: aligned shapes only
     const int mode = main_loop_mode();
@@ -1517,7 +1610,8 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
                            (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
-                           (float*)a.workspace, a.colsum, wo);
+                           (float*)a.workspace, a.colsum, wf);
+        if (fixed) *fixed = wf.fix != nullptr;
       };
       const bool half = gemm_half_stage_flag().load(std::memory_order_relaxed) != 0;
       if constexpr (!BKC) {
@@ -1561,7 +1655,8 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda,
                            (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
-                           a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace, a.colsum, wo);
+                           a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace, a.colsum, wf);
+        if (fixed) *fixed = wf.fix != nullptr;
       };
       if constexpr (!BKC) {
         if (a.colsum) {
@@ -1585,7 +1680,8 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
                            (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
-                           (float*)a.workspace, a.colsum, wo);
+                           (float*)a.workspace, a.colsum, wf);
+        if (fixed) *fixed = wf.fix != nullptr;
       };
       if constexpr (!BKC) {
         if (a.colsum) {
@@ -1648,7 +1744,9 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_period, a.wire_codec,
                    a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
                    a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0,
-                   a.upd_master, a.upd_lp, a.upd_mom, a.upd
+                   a.upd_master, a.upd_lp, a.upd_mom, a.upd,
+                   sk > 1 && is_wire_epi(EPI) && gemm_fixup_flag().load(std::memory_order_relaxed) != 0
+                       ? gemm_fix_counters(s) : nullptr
 #ifdef FAN_GEMM_STAMPS
                    , (unsigned long long*)gemm_stamp_buffer()
 #endif
@@ -1658,8 +1756,10 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     // applies the epilogue (deterministic: slabs summed in split order)
     // (the split main loop only writes slabs: the wire / update variants share one kernel)
     constexpr int kMainEpi = EPI == kEpiWireUpd ? kEpiWire : EPI;
-    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, kMainEpi, TC, ACCUM, true>(a, sk, wo, s);
+    bool fixed = false;  // the slabs already reduced in the GEMM (split_fixup)
+    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, kMainEpi, TC, ACCUM, true>(a, sk, wo, s, &fixed);
     if constexpr (is_wire_epi(EPI)) {
+      if (fixed) return;
       const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
       with_split_count(sk, [&](auto skc) {
         hipLaunchKernelGGL((splitk_reduce_wire_kernel<EPI == kEpiWireUpd, decltype(skc)::value>), stream_grid(items),

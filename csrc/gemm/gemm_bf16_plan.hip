@@ -3,6 +3,8 @@
 #include "gemm/gemm_bf16_kernel.h"
 
 #include <cstdio>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace fan {
@@ -46,6 +48,32 @@ std::atomic<int>& gemm_half_stage_flag() {
     return e ? atoi(e) : 0;
   }()};
   return flag;
+}
+
+std::atomic<int>& gemm_fixup_flag() {
+  static std::atomic<int> flag{[] {
+    const char* e = getenv("FAN_GEMM_FIXUP");
+    return e ? atoi(e) : 0;
+  }()};
+  return flag;
+}
+
+unsigned* gemm_fix_counters(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> bufs;
+  int dev = 0;
+  FAN_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = bufs.find({dev, s});
+  if (it != bufs.end()) return it->second;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  FAN_HIP_CHECK(hipStreamIsCapturing(s, &st));
+  if (st != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture: the reduce kernel runs
+  unsigned* p = nullptr;
+  FAN_HIP_CHECK(hipMalloc(&p, kFixTiles * sizeof(unsigned)));
+  FAN_HIP_CHECK(hipMemset(p, 0, kFixTiles * sizeof(unsigned)));
+  bufs[{dev, s}] = p;
+  return p;
 }
 
 std::atomic<int>& gemm_persist_flag() {
