@@ -21,8 +21,10 @@ World > 1 (GPU): the run chooses its own schedule and checks it before timing an
   request vs the NumPy simulators, :mod:`fpga_ai_nic_amd.parallel.gate`) and is timed for a few steps;
   ``extra.schedule_ab`` lists every arm (ms/step, exactness, or the error that excluded it), ``extra.gates_failed``
   the arms whose all-reduce was not bit-exact (excluded; the run still records the fastest exact arm);
-* the headline runs on the fastest exact arm; ``extra.dist.allreduce_exact`` is its gate; the process exits 3 after
-  printing its line when any arm failed the gate;
+* the headline runs on the fastest exact arm; ``extra.dist.allreduce_exact`` is its gate. Exit codes: an A/B arm
+  that fails the gate is excluded and listed in ``extra.gates_failed`` (the run still exits 0 with the fastest exact
+  arm); only a failed gate of ``--schedule fixed``'s own engine exits 3 (after printing the line), diverged replicas
+  exit 2, and no exact arm at all exits 3 without a line;
 * after the headline (bounded by ``--extra-budget`` seconds): ``extra.config4`` (256 MB all-reduce + fused SGD:
   BFP mesh / ring, the uncompressed f32 all-reduce over the same transport and RCCL f32 + SGD kernel: algo- and
   bus-BW; BASELINE configs 2/4) and ``extra.uncompressed`` (the same MLP step with an uncompressed all-reduce:
@@ -94,7 +96,12 @@ def parse_args(argv=None):
                          "with the remaining backward) or on the compute stream after the last backward GEMM")
     ap.add_argument("--gemm-inflight", default="persistent", choices=["persistent", "grid"],
                     help="schedule fixed: GEMM form while a request is in flight (see DataParallelTrainer)")
-    ap.add_argument("--ab-steps", type=int, default=4, help="timed steps per arm of the schedule A/B")
+    ap.add_argument("--ab-steps", type=int, default=4, help="timed steps per arm of the schedule A/B (stage 1)")
+    ap.add_argument("--ab2-steps", type=int, default=10,
+                    help="schedule A/B stage 2: timed steps per round of each of the --ab2-top fastest stage-1 arms, "
+                         "3 interleaved rounds after a warmup; the arm with the lowest median is chosen (0: stage 1 "
+                         "decides)")
+    ap.add_argument("--ab2-top", type=int, default=3, help="arms kept for stage 2 of the schedule A/B")
     ap.add_argument("--no-trace", action="store_true",
                     help="skip the separate traced pass that measures the all-reduce phases (extra.allreduce)")
     ap.add_argument("--extra-budget", type=float, default=240.0,
@@ -250,7 +257,8 @@ def main(argv=None):
         return ctx["p2p"]
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
-              force=False, panels=None, ring_sub=0, epi=None, engine=None):
+              force=False, panels=None, ring_sub=0, epi=None, engine=None, sizes=None, mdtype=None, bias=True,
+              relu="hidden"):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default); engine: python | native (default: the run's)."""
         comm = None
@@ -273,7 +281,7 @@ def main(argv=None):
         if hasattr(eng, "epilogue_on_producer") and not getattr(eng, "inline", True):
             eng.epilogue_on_producer = (epi or a.epi) == "producer"
         pad_fn = (lambda n: eng.layout(n).n_pad) if eng is not None else None
-        model = MLP(SIZES, dtype=dtype, device=device, pad_fn=pad_fn, seed=1)
+        model = MLP(sizes or SIZES, dtype=mdtype or dtype, device=device, pad_fn=pad_fn, seed=1, bias=bias, relu=relu)
         if world > 1:
             for l in model.layers:
                 ctrl.broadcast_(l.master, 0)
@@ -344,11 +352,13 @@ def main(argv=None):
         trainer, model, engine = setup.trainer, setup.model, setup.engine
         x, y = batch(mb, seed)
         wd.arm(f"warmup {tag} mb={mb}")
-        if tag == "timed" and cuda and a.settle_ms > 0:
+        if tag in ("timed", "ref") and cuda and a.settle_ms > 0:
             # The shader clock needs ~50 ms of sustained load to reach the level a training run holds: the driver's
             # 5 warmup + 20 steps read 1.038-1.047 ms/step where 50 + 20 read 0.989 and 5 + 100 0.996
             # (profiles/r4_warmup_settle.jsonl). Untimed steps of the same batch in chunks of 10 until settle_ms
             # passed (the chunk count agreed over ranks, so every rank runs the same steps); then W + K as ever.
+            # Both timed cells (the headline and the reference batch, extra.mb<ref>) get it, so they are measured
+            # alike (extra.settle per cell).
             t_s, n_s = time.perf_counter(), 0
             while n_s < 5000:
                 for _ in range(10):
@@ -358,7 +368,7 @@ def main(argv=None):
                 torch.cuda.synchronize()
                 if D.max_over_ranks(time.perf_counter() - t_s) * 1e3 >= a.settle_ms:
                     break
-            settle.update(steps=n_s, ms=round((time.perf_counter() - t_s) * 1e3, 1))
+            settle[tag] = {"steps": n_s, "ms": round((time.perf_counter() - t_s) * 1e3, 1)}
         if stall_rank == rank and tag == "timed":  # test hook: this rank stops taking part (a hung peer)
             time.sleep(float(os.environ.get("FAN_BENCH_STALL_S", "600")))
         for _ in range(warmup):
@@ -417,8 +427,11 @@ def main(argv=None):
                 arms.append(dict(name=f"rccl_mesh_{gm}", kind="bfp", algo="mesh", transport="native", gemm=gm))
                 arms.append(dict(name=f"p2p_mesh_{gm}", kind="bfp", algo="mesh", transport="p2p", gemm=gm))
                 arms.append(dict(name=f"p2p_ring_{gm}", kind="bfp", algo="ring", rings=R, transport="p2p", gemm=gm))
-            arms.append(dict(name="p2p_mesh_sdma", kind="bfp", algo="mesh", transport="p2p", sdma=True))
-            arms.append(dict(name="p2p_ring_sdma", kind="bfp", algo="ring", rings=R, transport="p2p", sdma=True))
+            # pure copies on the copy engines: ~2x slower than the copy kernels at 2 ranks (profiles/
+            # r4_final_bench_2rank_1gpu.jsonl: 4.2 / 5.2 vs 2.6 ms/step), so only on request (FAN_AB_SDMA=1)
+            if os.environ.get("FAN_AB_SDMA", "0") == "1":
+                arms.append(dict(name="p2p_mesh_sdma", kind="bfp", algo="mesh", transport="p2p", sdma=True))
+                arms.append(dict(name="p2p_ring_sdma", kind="bfp", algo="ring", rings=R, transport="p2p", sdma=True))
             # each ring hop streamed in 3 sub-slices (a ready flag each; engine.cpp run_ring_direct)
             arms.append(dict(name="p2p_ring_stream3", kind="bfp", algo="ring", rings=R, transport="p2p", ring_sub=3))
             # layer 0's bucket as 4 row panels, each submitted right after its GEMM (the exchange of the last bucket,
@@ -438,10 +451,10 @@ def main(argv=None):
             arms.append(dict(name=f"{impl}_{a.algo}", kind="bfp", algo=a.algo, rings=a.rings, transport="torch"))
         schedule_ab = []
         arm_gates = {}
-        best = None
+        kept = []  # (record, setup) of the fastest exact arms of stage 1, fastest first (at most --ab2-top)
         arm_wait = min(eng_timeout, a.arm_timeout)  # gate and A/B waits: below the watchdog's per-phase budget
         for spec in arms:
-            if spec.get("fallback") and best is not None:  # identical on every rank (agreed results and times)
+            if spec.get("fallback") and kept:  # identical on every rank (agreed results and times)
                 schedule_ab.append({"arm": spec["name"], "skipped": "a faster exact arm passed"})
                 continue
             wd.arm(f"schedule A/B {spec['name']}")
@@ -489,23 +502,57 @@ def main(argv=None):
             if lost_any and "ms_per_step" in rec:  # its numbers came from a transport that is gone
                 rec["error"] = ctx[lost_any[0] + "_err"]
                 del rec["ms_per_step"]
-            if best is not None and best[0].get("transport") in lost_any:  # the fastest so far ran on a lost transport
-                best[0]["error"] = ctx[best[0]["transport"] + "_err"]
-                best[0].pop("ms_per_step", None)
-                release(best[1])
-                best = None
-            if "ms_per_step" in rec and (best is None or rec["ms_per_step"] < best[0]["ms_per_step"]):
-                release(best[1] if best else None)
-                best = (rec, setup)
+            for kr, ks in list(kept):  # a kept arm ran on a transport that is gone
+                if kr.get("transport") in lost_any:
+                    kr["error"] = ctx[kr["transport"] + "_err"]
+                    kr.pop("ms_per_step", None)
+                    release(ks)
+                    kept.remove((kr, ks))
+            if "ms_per_step" in rec:
+                kept.append((rec, setup))
+                kept.sort(key=lambda x: x[0]["ms_per_step"])
+                while len(kept) > max(1, a.ab2_top):
+                    release(kept.pop()[1])
             else:
                 release(setup)
-        if best is None:
+        if not kept:
             log("no arm of the schedule A/B passed: " + json.dumps(schedule_ab))
             return 3
-        chosen_rec, main_setup = best
+        if len(kept) > 1 and a.ab2_steps > 0:
+            # Stage 2: stage 1's 4 steps per arm (no settle) read ~15 % above the headline and its top arms swapped
+            # places between runs. The kept arms get a warmup each, then 3 interleaved rounds of
+            # --ab2-steps steps; the lowest median decides. An arm that fails here is dropped with its error.
+            wd.arm("schedule A/B stage 2")
+            st2 = {r["arm"]: [] for r, _ in kept}
+            for rnd in range(4):  # round 0: warmup (untimed in the decision)
+                for kr, ks in list(kept):
+                    try:
+                        e, _, _, _, _ = run(ks, mb, 99, 2 if rnd == 0 else 0, a.ab2_steps, f"ab2 {kr['arm']}",
+                                            wait_s=arm_wait)
+                        if rnd > 0:
+                            st2[kr["arm"]].append(round(e / a.ab2_steps * 1e3, 4))
+                    except Exception as ex:  # noqa: BLE001
+                        kr["error"] = f"stage 2: {str(ex)[:280]}"
+                        kr.pop("ms_per_step", None)
+                        release(ks)
+                        kept.remove((kr, ks))
+            import statistics
+
+            for kr, _ in kept:
+                kr["stage2_ms_per_step"] = st2[kr["arm"]]
+                kr["stage2_median"] = statistics.median(st2[kr["arm"]]) if st2[kr["arm"]] else None
+            kept.sort(key=lambda x: x[0]["stage2_median"] if x[0]["stage2_median"] is not None else 1e30)
+            if not kept:
+                log("no arm survived stage 2 of the schedule A/B: " + json.dumps(schedule_ab))
+                return 3
+        chosen_rec, main_setup = kept[0]
+        for _, ks in kept[1:]:
+            release(ks)
+        kept = kept[:1]
         chosen_rec["chosen"] = True
         gate_rec = dict(arm_gates[chosen_rec["arm"]], arm=chosen_rec["arm"])
-        log(f"schedule A/B: running {chosen_rec['arm']} ({chosen_rec['ms_per_step']} ms/step in the A/B)")
+        log(f"schedule A/B: running {chosen_rec['arm']} ({chosen_rec.get('stage2_median', chosen_rec['ms_per_step'])}"
+            f" ms/step in the A/B)")
     else:
         transport = "auto"
         if world > 1 or a.force_dist:
@@ -521,6 +568,21 @@ def main(argv=None):
             if not gate_rec["exact"]:
                 gates_failed.append({"arm": "main", **gate_rec})
     engine, model, trainer = main_setup.engine, main_setup.model, main_setup.trainer
+    if multi and engine is not None and gate_rec is not None and gate_rec.get("exact"):
+        # the chosen schedule once more, on every bucket layout the model actually trains (each layer's size at this
+        # world's arena slot: chunking and ring block geometry differ from the 1 Mi-element gate request)
+        wd.arm("layout gate")
+        try:
+            lg = gate.allreduce_exactness_layouts(engine, [l.n for l in model.layers],
+                                                  timeout_s=min(eng_timeout, a.arm_timeout))
+        except Exception as ex:  # noqa: BLE001
+            lg = {"exact": False, "error": str(ex)[:300], "layouts": []}
+        gate_rec = dict(gate_rec, layouts=lg.get("layouts"), layouts_exact=lg["exact"],
+                        n_checked=[gate_rec.get("n")] + [x["n"] for x in lg.get("layouts") or []])
+        if not lg["exact"]:
+            gates_failed.append({"arm": "main", "layouts": lg.get("layouts"), "max_abs_diff": lg.get("max_abs_diff"),
+                                 "mismatch_ranks": lg.get("mismatch_ranks"), "error": lg.get("error")})
+            gate_rec["exact"] = False
     held["engine"] = engine
     held["comm"] = ctx["p2p"] if main_setup.info.get("transport") == "p2p" else None
     held["transport"] = ctx["native"] or ctrl
@@ -659,6 +721,34 @@ def main(argv=None):
 
             extra("unfused_update_ms_per_step", lambda: split(False, False), 10)
             extra("forced_dist_ms_per_step", forced, 20)
+
+        def ref_workload():
+            """The reference's own benchmark (sw/run.sh:16: mlp_mpi_example_f32 20 5376 0 A 32 32 32 2048 x 11 over 3
+            ranks): 10 FC layers of 2048, f32, fuse_type 0 (no bias, no ReLU), 1792 rows per rank, BFP all-reduce +
+            SGD of every layer's gradient over this run's transport; the reference's report quantities (fp time =
+            s/iter, GFLOPS by its formula, sw/mlp_mpi_example_f32.cpp:794-808)."""
+            if not cuda:
+                return {"skipped": "CPU run"}
+            info = main_setup.info
+            tp = info.get("transport") if multi else "auto"
+            tp = tp if tp in ("p2p", "native", "torch") else ("auto" if not multi else "torch")
+            s = build("ref_workload", a.compress, algo=info.get("algo", "mesh"), rings=max(1, info.get("rings") or 1),
+                      transport=tp, sizes=[2048] * 11, mdtype=torch.float32, bias=False, relu="none")
+            try:
+                iters = 10
+                e, _, loss_r, _, _ = run(s, REF_MB_PER_RANK, 777, 3, iters, "ref_workload")
+                t_it = e / iters
+                gmb = REF_MB_PER_RANK * world
+                gflop = s.model.flops_per_sample() * gmb / 1e9
+                return {"sizes": [2048] * 11, "dtype": "f32", "fuse_type": 0, "mb_per_rank": REF_MB_PER_RANK,
+                        "global_mb": gmb, "iters": iters, "fp_time_s": round(t_it, 6), "GFLOP": round(gflop, 2),
+                        "GFLOPS": round(gflop / t_it, 1), "samples_per_s": round(gmb / t_it, 1),
+                        "final_loss": round(loss_r, 5), "transport": s.info["transport"], "algo": s.info["algo"],
+                        "compress": s.info["compress"]}
+            finally:
+                release(s)
+
+        extra("ref_workload", ref_workload, 15)
         if world > 1:
             extra("config4", lambda: _config4(a, world, rank, device, ctx, native_transport, p2p_comm, make_engine,
                                               ctrl, eng_timeout), 30)

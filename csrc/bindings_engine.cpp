@@ -20,6 +20,21 @@ size_t bytes_of(const at::Tensor& t) { return (size_t)t.numel() * t.element_size
 void register_engine(pybind11::module_& m) {
   m.def("nccl_unique_id", []() { return pybind11::bytes(nccl_unique_id_bytes()); });
   m.def("nccl_version", &nccl_version);
+  m.def("p2p_release_event_needed", &p2p_release_event_needed,
+        "whether a P2P round records the system-scope release event before its flags (release mode, copy-engine bytes)");
+  m.def("p2p_coalesce_copies",
+        [](const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>>& segs) {
+          std::vector<P2PCopy> in;
+          for (const auto& t : segs)
+            in.push_back({reinterpret_cast<const void*>(std::get<0>(t)), reinterpret_cast<void*>(std::get<1>(t)),
+                          (size_t)std::get<2>(t)});
+          std::vector<std::tuple<uint64_t, uint64_t, uint64_t>> out;
+          for (const P2PCopy& c : coalesce_copies(in))
+            out.emplace_back((uint64_t)reinterpret_cast<uintptr_t>(c.src), (uint64_t)reinterpret_cast<uintptr_t>(c.dst),
+                             (uint64_t)c.bytes);
+          return out;
+        },
+        "(src, dst, bytes) segments merged into the contiguous runs the copy-engine path issues (pure host logic)");
   pybind11::class_<Comm>(m, "Comm")
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)

@@ -3,6 +3,7 @@
 #include "bfp/bfp_format.h"
 #include "comm/planner.h"
 #include "gemm/gemm.h"
+#include "gemm/gemm_pair.h"
 #include "nn/nn.h"
 
 namespace fan {
@@ -137,6 +138,36 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
   }
 }
 
+// One layer's backward pair in one dispatch: dX = (dZ . W^T) * (X > 0) (bf16) and dW = X^T . dZ (f32).
+// X [M][cin], dZ [M][cout], W [cin][cout] (bf16); dX [M][cin] bf16; dW [cin][cout] f32.
+void gemm_bwd_pair(const at::Tensor& dZ, const at::Tensor& W, const at::Tensor& X, at::Tensor& dX, at::Tensor& dW,
+                   int64_t bw_bn, int64_t grid0, int64_t grid1) {
+  for (const at::Tensor* t : {&dZ, &W, &X, static_cast<const at::Tensor*>(&dX)})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->stride(1) == 1,
+                "gemm_bwd_pair: bf16 2-D GPU tensors");
+  TORCH_CHECK(dW.is_cuda() && dW.scalar_type() == at::kFloat && dW.dim() == 2 && dW.stride(1) == 1, "dW: f32 2-D");
+  const int64_t M = X.size(0), cin = X.size(1), cout = dZ.size(1);
+  TORCH_CHECK(dZ.size(0) == M && W.size(0) == cin && W.size(1) == cout && dX.size(0) == M && dX.size(1) == cin &&
+                  dW.size(0) == cin && dW.size(1) == cout,
+              "gemm_bwd_pair: shapes");
+  GemmArgs bd{};
+  bd.A = dZ.data_ptr(); bd.lda = ld_of(dZ);
+  bd.B = W.data_ptr(); bd.ldb = ld_of(W);
+  bd.C = dX.data_ptr(); bd.ldc = ld_of(dX);
+  bd.aux = X.data_ptr(); bd.ldaux = ld_of(X);
+  bd.M = (int)M; bd.N = (int)cin; bd.K = (int)cout;
+  bd.a_kcontig = true; bd.b_kcontig = true; bd.epilogue = kEpiReluMask; bd.c_bf16 = true;
+  GemmArgs bw{};
+  bw.A = X.data_ptr(); bw.lda = ld_of(X);
+  bw.B = dZ.data_ptr(); bw.ldb = ld_of(dZ);
+  bw.C = dW.data_ptr(); bw.ldc = ld_of(dW);
+  bw.M = (int)cin; bw.N = (int)cout; bw.K = (int)M;
+  bw.a_kcontig = false; bw.b_kcontig = false; bw.epilogue = kEpiNone; bw.c_bf16 = false;
+  bw.tile_bm = 256; bw.tile_bn = (int)bw_bn;
+  TORCH_CHECK(gemm_bwd_pair_supported(bd, bw, (int)grid0, (int)grid1), "gemm_bwd_pair: unsupported configuration");
+  launch_gemm_bwd_pair(bd, bw, (int)grid0, (int)grid1, fan_stream());
+}
+
 pybind11::tuple gemm_plan(int64_t M, int64_t N, int64_t K, int64_t split_k, int64_t tile_bm, int64_t tile_bn,
                           int64_t tile_waves) {
   GemmPlan p = gemm_bf16_plan((int)M, (int)N, (int)K, (int)split_k, (int)tile_bm, (int)tile_bn, (int)tile_waves);
@@ -192,6 +223,9 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("upd_grad_scale") = 1.0, pybind11::arg("upd_weight_decay") = 0.0,
         pybind11::arg("upd_momentum") = 0.0, pybind11::arg("upd_nesterov") = false);
   m.def("gemm_supported", &gemm_supported);
+  m.def("gemm_bwd_pair", &gemm_bwd_pair, "one layer's bwd-data (ReLU mask, bf16) + bwd-weight (f32) in one dispatch",
+        pybind11::arg("dZ"), pybind11::arg("W"), pybind11::arg("X"), pybind11::arg("dX"), pybind11::arg("dW"),
+        pybind11::arg("bw_bn") = 256, pybind11::arg("grid0") = 128, pybind11::arg("grid1") = 128);
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);
   m.def("gemm_set_main_loop", [](int mode) { gemm_main_loop_flag().store(mode); },

@@ -40,7 +40,11 @@ std::vector<FaultRule> parse_fault_spec(const std::string& spec) {
         bad(item, "delay_ms needs a number of milliseconds in [0, 3.6e6]");
       r.kind = "delay_ms";
       r.delay_ms = ms;
-    } else if (r.kind != "flip" && r.kind != "nan" && r.kind != "drop") {
+    } else if (r.kind == "drop") {
+      // only a sending site can lose its announcement (engine.cpp: the P2P rounds' flag writes); at a corrupting
+      // site 'drop' would silently do nothing
+      if (r.site != "p2p_publish") bad(item, "kind 'drop' applies to site 'p2p_publish' only");
+    } else if (r.kind != "flip" && r.kind != "nan") {
       bad(item, "unknown fault kind '" + r.kind + "'");
     }
     out.push_back(r);

@@ -97,8 +97,17 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes, int depth)
   FAN_HIP_CHECK(hipEventCreateWithFlags(&rel_ev_, hipEventDisableTiming | hipEventReleaseToSystem));
 }
 
+bool p2p_release_event_needed(int mode, bool copy_engine_bytes) {
+  // mode 3 (cp): the command processor's system-scope release orders every round's stores before its flags. In the
+  // in-kernel modes (1 block, 2 thread) the peer-storing kernels release their own stores, but bytes moved by the copy
+  // engines or by hipMemcpyAsync (SDMA arms, unaligned fallback) went through no such kernel: the event is still
+  // needed for that round, else a cross-device peer could see the flag before those bytes.
+  return mode == 3 || copy_engine_bytes;
+}
+
 void P2PComm::release_before_flags(hipStream_t s) {
-  if (p2p_release_mode() == 3) FAN_HIP_CHECK(hipEventRecord(rel_ev_, s));
+  if (p2p_release_event_needed(p2p_release_mode(), nonkernel_pending_)) FAN_HIP_CHECK(hipEventRecord(rel_ev_, s));
+  nonkernel_pending_ = false;
 }
 
 void P2PComm::wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool credit) {
@@ -262,8 +271,28 @@ void P2PComm::move(const std::vector<P2PCopy>& segs, hipStream_t s) {
     launch_multi_copy(segs, s);
     return;
   }
-  for (const P2PCopy& c : segs)
-    if (c.bytes) FAN_HIP_CHECK(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDeviceNoCU, s));
+  // copy engines: one command per contiguous run (segments whose source AND destination continue the previous one
+  // are merged), so a round costs one command per peer rather than one per segment
+  for (const P2PCopy& run : coalesce_copies(segs)) {
+    FAN_HIP_CHECK(hipMemcpyAsync(run.dst, run.src, run.bytes, hipMemcpyDeviceToDeviceNoCU, s));
+    nonkernel_pending_ = true;
+  }
+}
+
+std::vector<P2PCopy> coalesce_copies(const std::vector<P2PCopy>& segs) {
+  std::vector<P2PCopy> out;
+  for (const P2PCopy& c : segs) {
+    if (!c.bytes) continue;
+    if (!out.empty()) {
+      P2PCopy& b = out.back();
+      if (static_cast<const uint8_t*>(b.src) + b.bytes == c.src && static_cast<uint8_t*>(b.dst) + b.bytes == c.dst) {
+        b.bytes += c.bytes;
+        continue;
+      }
+    }
+    out.push_back(c);
+  }
+  return out;
 }
 
 void P2PComm::connect_local(const std::vector<P2PComm*>& ranks) {
@@ -403,8 +432,10 @@ void P2PComm::copy(const std::vector<P2PCopy>& segs, hipStream_t s) {
     launch_multi_copy(segs, s);
     return;
   }
-  for (const P2PCopy& c : segs)
-    if (c.bytes) FAN_HIP_CHECK(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, s));
+  for (const P2PCopy& c : coalesce_copies(segs)) {
+    FAN_HIP_CHECK(hipMemcpyAsync(c.dst, c.src, c.bytes, hipMemcpyDeviceToDevice, s));
+    nonkernel_pending_ = true;
+  }
 }
 
 void P2PComm::all_to_all(const void* send, void* recv, size_t bpp, hipStream_t s) {

@@ -60,6 +60,13 @@ struct P2PCopy {
 };
 // All segments in one (or few) kernel launches; segments 16-B aligned, sizes multiples of 16 B.
 void launch_multi_copy(const std::vector<P2PCopy>& segs, hipStream_t stream);
+// Segments merged into contiguous runs (source and destination both continue the previous segment); empty ones
+// dropped. The copy-engine path issues one command per run.
+std::vector<P2PCopy> coalesce_copies(const std::vector<P2PCopy>& segs);
+// Whether a round must record the system-scope release event before its flag writes: always in release mode 3
+// (cp); in the in-kernel modes only when bytes of the round were moved outside a peer-storing kernel (copy engines,
+// hipMemcpyAsync fallback), since no kernel released those.
+bool p2p_release_event_needed(int mode, bool copy_engine_bytes);
 
 class P2PComm : public Comm {
  public:
@@ -191,8 +198,9 @@ class P2PComm : public Comm {
   std::vector<int64_t> bytes_to_peer_;
   bool uncached_ = false;
   std::string arena_mem_;
-  hipEvent_t rel_ev_ = nullptr;  // system-scope release before the flag writes (release mode "cp")
+  hipEvent_t rel_ev_ = nullptr;  // system-scope release before the flag writes (release mode "cp", copy-engine bytes)
   bool sdma_ = false;
+  bool nonkernel_pending_ = false;  // bytes of the current round moved by the copy engines / hipMemcpyAsync
   bool cross_device_ = false;
   void release_before_flags(hipStream_t s);
 };

@@ -127,7 +127,7 @@ void FaultInjector::maybe_corrupt(const std::string& site, uint8_t* buf, size_t 
     if (r.site != site || r.index != k) continue;
     if (r.kind == "flip") launch_fault_byte(buf, bytes, 0, s);
     else if (r.kind == "nan") launch_fault_byte(buf, bytes, 1, s);
-    else {  // delay_ms: the request's producer-side progress stalls (what a slow link looks like to the peers)
+    else if (r.kind == "delay_ms") {  // the request's producer-side progress stalls (what a slow link looks like)
       FAN_HIP_CHECK(hipStreamSynchronize(s));
       std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(r.delay_ms * 1000.0)));
     }

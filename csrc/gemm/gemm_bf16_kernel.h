@@ -1067,13 +1067,17 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// The body of gemm_pl4_kernel as a device function: this workgroup runs virtual blocks v0, v0 + vstep, ... of the
+// problem's tiles * split_k (COLSUM: the one tile v0). gemm_pl4_kernel passes (blockIdx.x, gridDim.x); the grouped
+// kernel (gemm_group2_kernel) gives each of its two problems its own range of workgroups. vstep must be a multiple
+// of the XCD count so a virtual block stays on its workgroup's XCD (xcd_remap).
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
           int BM_ = 256>
-__global__ void __launch_bounds__(256, 1)
-    gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
-                    TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
-                    int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
-                    float* __restrict__ colsum, WireOut wo) {
+__device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
+                                        int64_t ldb, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
+                                        const TC* __restrict__ aux, int64_t ldaux, int M, int N, int K, int split_k,
+                                        float* __restrict__ ws, float* __restrict__ colsum, const WireOut& wo, int v0,
+                                        int vstep) {
   constexpr int BM = BM_, BN = BN_, NT = 256;
   constexpr int A_BYTES = OpTile<BM, NT>::BYTES;
   constexpr int STAGE = A_BYTES + OpTile<BN, NT>::BYTES;
@@ -1243,13 +1247,65 @@ __global__ void __launch_bounds__(256, 1)
   }
   };
   if constexpr (COLSUM) {
-    tile_body(blockIdx.x);
+    if (v0 < tiles * split_k) tile_body(v0);
   } else {
-    for (int v = blockIdx.x; v < tiles * split_k; v += gridDim.x) {
+    for (int v = v0; v < tiles * split_k; v += vstep) {
       tile_body(v);
       __syncthreads();  // every wave's staging reads done before the next tile's DMA overwrites the LDS
     }
   }
+}
+
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
+          int BM_ = 256>
+__global__ void __launch_bounds__(256, 1)
+    gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
+                    TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
+                    int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
+                    float* __restrict__ colsum, WireOut wo) {
+  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M, N, K, split_k,
+                                                           ws, colsum, wo, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Grouped launch of two independent GEMMs (e.g. a layer's bwd-data and bwd-weight, which the reference runs as one
+// libxsmm PASS_BWD call, sw/mlp_mpi_example_f32.cpp:741-742): workgroups [0, grid0) run problem 0's tiles, the rest
+// problem 1's, each persistent over its own tile list. One dispatch instead of two, and the two problems' epilogues
+// (HBM-write phases) fall at different times on different CUs instead of every CU writing at once.
+template <typename TC>
+struct PlProblem {
+  const bf16_t* A;
+  int64_t lda;
+  const bf16_t* B;
+  int64_t ldb;
+  TC* C;
+  int64_t ldc;
+  const bf16_t* bias;
+  const TC* aux;
+  int64_t ldaux;
+  int M, N, K, split_k;
+  float* ws;
+  float* colsum;
+  WireOut wo;
+};
+
+template <bool AK, bool BKC, int EPI, typename TC_, bool ACCUM, bool SPLIT, bool COLSUM, int BN_, int BM_ = 256>
+struct PlCfg {
+  using TC = TC_;
+  static constexpr int kLds = (BN_ == 128 ? 3 : 2) * (BM_ + BN_) * BK * 2;
+  static constexpr int kBM = BM_, kBN = BN_;
+  __device__ static __forceinline__ void run(const PlProblem<TC>& p, int v0, int vstep) {
+    pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_>(p.A, p.lda, p.B, p.ldb, p.C, p.ldc, p.bias, p.aux,
+                                                             p.ldaux, p.M, p.N, p.K, p.split_k, p.ws, p.colsum, p.wo,
+                                                             v0, vstep);
+  }
+};
+
+template <class P0, class P1>
+__global__ void __launch_bounds__(256, 1)
+    gemm_group2_kernel(PlProblem<typename P0::TC> p0, PlProblem<typename P1::TC> p1, int grid0) {
+  if ((int)blockIdx.x < grid0) P0::run(p0, (int)blockIdx.x, grid0);
+  else P1::run(p1, (int)blockIdx.x - grid0, (int)gridDim.x - grid0);
 }
 
 // ---------------------------------------------------------------------------------------------------------------

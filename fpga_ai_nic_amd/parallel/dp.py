@@ -233,54 +233,58 @@ class DataParallelTrainer:
             t1 = time.perf_counter()
             self.times["loss"] += t1 - t0
             t0 = t1
-        for i in reversed(range(m.L)):
-            l = m.layers[i]
-            if i in self.panel_plans and self.engine is not None:
+        try:
+            for i in reversed(range(m.L)):
+                l = m.layers[i]
+                if i in self.panel_plans and self.engine is not None:
+                    with tracing.range(f"bwd{i}"):
+                        hs = self._backward_weight_panels(i)
+                        m.backward_data(i)
+                        self.pending[i] = hs if self.commit_at_end else [h.commit_after_current() for h in hs]
+                        self.last_handle = hs[-1]
+                    continue
                 with tracing.range(f"bwd{i}"):
-                    hs = self._backward_weight_panels(i)
-                    m.backward_data(i)
-                    self.pending[i] = hs if self.commit_at_end else [h.commit_after_current() for h in hs]
-                    self.last_handle = hs[-1]
-                continue
-            with tracing.range(f"bwd{i}"):
-                # the bwd-weight GEMM encodes dW (and the fused bias gradient) straight into the wire buffer;
-                # the zero tail (padding, or the bias segment of a bias-free model) is encoded once
-                # (the wire epilogue encodes whole 16-column groups: output widths that are multiples of 16)
-                tgt = (self.engine.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout)
-                       if self.prepack and l.cout % 16 == 0 else None)
-                if tgt is not None and self.fused_update:
-                    # single-rank engine: bwd-data first (it reads W_i), then dW's BFP round trip + SGD in the
-                    # bwd-weight epilogue
-                    m.backward_data(i)
-                    upd = G.LocalUpdate(l.master, l.lp, l.mom, lr=self.lr, grad_scale=self.grad_scale,
-                                        weight_decay=self.wd, momentum=self.momentum, nesterov=self.nesterov)
-                    # (the bwd-weight GEMMs of layers >= 1 on a second stream, beside the next GEMM, measured 1.5-2 %
-                    # slower: profiles/r3_fused_update_ab.txt)
-                    m.backward_weight(i, wire=tgt, update=upd)
-                    self.fused_updates += 1
-                else:
-                    m.backward_weight(i, wire=tgt)
-                    h = None
-                    if self.engine is not None:
-                        kw = {"prepacked": (tgt[0], l.n_pad)} if tgt is not None else {}
-                        h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
-                                                      grad_scale=self.grad_scale, weight_decay=self.wd,
-                                                      momentum=self.momentum, nesterov=self.nesterov, defer=True,
-                                                      name=f"fc{i}", **kw)
-                        self._gemm_grid(True)
-                    m.backward_data(i)
-                    if h is not None:
-                        self.pending[i] = h if self.commit_at_end else h.commit_after_current()
-                        self.last_handle = self.pending[i]
+                    # the bwd-weight GEMM encodes dW (and the fused bias gradient) straight into the wire buffer;
+                    # the zero tail (padding, or the bias segment of a bias-free model) is encoded once
+                    # (the wire epilogue encodes whole 16-column groups: output widths that are multiples of 16)
+                    tgt = (self.engine.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout)
+                           if self.prepack and l.cout % 16 == 0 else None)
+                    if tgt is not None and self.fused_update:
+                        # single-rank engine: bwd-data first (it reads W_i), then dW's BFP round trip + SGD in the
+                        # bwd-weight epilogue
+                        m.backward_data(i)
+                        upd = G.LocalUpdate(l.master, l.lp, l.mom, lr=self.lr, grad_scale=self.grad_scale,
+                                            weight_decay=self.wd, momentum=self.momentum, nesterov=self.nesterov)
+                        # (the bwd-weight GEMMs of layers >= 1 on a second stream, beside the next GEMM, measured 1.5-2 %
+                        # slower: profiles/r3_fused_update_ab.txt)
+                        m.backward_weight(i, wire=tgt, update=upd)
+                        self.fused_updates += 1
                     else:
-                        self._sgd_local(l)
-            if prof and i == m.L - 1:
-                self._sync()
-                t1 = time.perf_counter()
-                self.times["bwd_first"] += t1 - t0
-                self.times["bwd"] += t1 - t0
-                t0 = t1
-        self._gemm_grid(False)
+                        m.backward_weight(i, wire=tgt)
+                        h = None
+                        if self.engine is not None:
+                            kw = {"prepacked": (tgt[0], l.n_pad)} if tgt is not None else {}
+                            h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
+                                                          grad_scale=self.grad_scale, weight_decay=self.wd,
+                                                          momentum=self.momentum, nesterov=self.nesterov, defer=True,
+                                                          name=f"fc{i}", **kw)
+                            self._gemm_grid(True)
+                        m.backward_data(i)
+                        if h is not None:
+                            self.pending[i] = h if self.commit_at_end else h.commit_after_current()
+                            self.last_handle = self.pending[i]
+                        else:
+                            self._sgd_local(l)
+                if prof and i == m.L - 1:
+                    self._sync()
+                    t1 = time.perf_counter()
+                    self.times["bwd_first"] += t1 - t0
+                    self.times["bwd"] += t1 - t0
+                    t0 = t1
+        finally:
+            # the grid GEMM form must not outlive this backward (an exception in between would leave every later
+            # GEMM of the process on one workgroup per tile while records report the persistent form)
+            self._gemm_grid(False)
         if self.commit_at_end:  # issue order L-1..0: the epilogues run in the order their all-reduces finish
             for i in reversed(range(m.L)):
                 h = self.pending[i]
@@ -315,6 +319,7 @@ class DataParallelTrainer:
 
     def finish(self, timeout: float | None = None):
         """Wait (host) for every outstanding all-reduce/update."""
+        self._gemm_grid(False)
         for i, h in enumerate(self.pending):
             if h is not None:
                 for x in (h if isinstance(h, list) else [h]):

@@ -105,3 +105,27 @@ def allreduce_exactness(engine, *, n: int = 1 << 20, seed: int = 20260417, prepa
         "mismatch_ranks": [r for r, e in enumerate(every) if not e["exact"]],
         "max_abs_diff": max(e["max_abs_diff"] for e in every),
     }
+
+
+def allreduce_exactness_layouts(engine, sizes, **kw) -> dict:
+    """:func:`allreduce_exactness` once per distinct bucket size of the trained model (each layer's ``n``): the
+    production layouts themselves — at this world's arena slot the engine chunks a bucket differently, and a ring
+    splits it into more blocks — not just one 1 Mi-element request. Same keys as the single gate (``n`` is the list
+    of sizes checked) plus ``layouts``: one entry per size."""
+    res = []
+    for n in sorted({int(x) for x in sizes}):
+        g = allreduce_exactness(engine, n=n, **kw)
+        L = engine.layout(n)
+        res.append({"n": n, "exact": g["exact"], "max_abs_diff": g["max_abs_diff"], "prepacked": g["prepacked"],
+                    "n_pad": int(L.n_pad), "shard": int(getattr(L, "shard", 0) or 0),
+                    "chunks": int(getattr(L, "chunks", 1) or 1), "blocks": int(getattr(L, "blocks", 0) or 0),
+                    "mismatch_ranks": g["mismatch_ranks"]})
+    return {
+        "exact": all(r["exact"] for r in res),
+        "checked": True,
+        "n": [r["n"] for r in res],
+        "prepacked": all(r["prepacked"] for r in res),
+        "mismatch_ranks": sorted({q for r in res for q in r["mismatch_ranks"]}),
+        "max_abs_diff": max((r["max_abs_diff"] for r in res), default=0.0),
+        "layouts": res,
+    }

@@ -38,12 +38,17 @@ int main() {
     EXPECT(r[2].site == "ring_send" && r[2].index == 3 && r[2].kind == "delay_ms" && r[2].delay_ms == 2.5, "rule 2");
   }
   EXPECT(parse_fault_spec("").empty(), "empty spec");
+  {  // 'drop' only where a message is announced (the P2P rounds' flag writes)
+    auto d = parse_fault_spec("p2p_publish:1:drop");
+    EXPECT(d.size() == 1 && d[0].kind == "drop" && d[0].index == 1, "p2p_publish drop");
+  }
   EXPECT(parse_fault_spec(",,,").empty(), "only separators");
   EXPECT(parse_fault_spec("a:999999999999999999:flip")[0].index == 999999999999999999LL, "18-digit index");
   for (const char* s : {"x", "a:1", "a:1:", ":1:flip", "a::flip", "a:-1:flip", "a:1x:flip", "a:1:boom",
                         "a:1:delay_ms=", "a:1:delay_ms=abc", "a:1:delay_ms=-3", "a:1:delay_ms=1e400",
                         "a:1:delay_ms=nan", "a:1:delay_ms=5ms", "a:9999999999999999999:flip", "a:1:flip,b",
-                        "a:1:delay_ms=inf", "a:1:FLIP", "\\x01:\\x02:\\x03"})
+                        "a:1:delay_ms=inf", "a:1:FLIP", "\\x01:\\x02:\\x03", "ring_send:0:drop",
+                        "mesh_pack:2:drop"})
     EXPECT(throws(s), "'%s' must be rejected", s);
   // every prefix of a long valid spec parses or throws cleanly (bounds / UB under the sanitizers)
   const std::string longspec = "mesh_pack:0:flip,mesh_reduce:7:nan,ring_send:42:delay_ms=0.125";
