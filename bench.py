@@ -258,7 +258,7 @@ def main(argv=None):
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
               force=False, panels=None, ring_sub=0, epi=None, engine=None, sizes=None, mdtype=None, bias=True,
-              relu="hidden"):
+              relu="hidden", shard=None):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default); engine: python | native (default: the run's)."""
         comm = None
@@ -277,7 +277,7 @@ def main(argv=None):
             t = NativeTransport(force_collectives=True)
         eng = make_engine(t, kind, rounding=a.rounding, algo=algo, rings=rings, force_comm=force or a.force_dist,
                           impl=eimpl, comm=comm, side_stream=a.side_stream and not multi, timeout_s=eng_timeout,
-                          **({"ring_sub": ring_sub} if eimpl == "native" else {}))
+                          **({"ring_sub": ring_sub, "shard_update": shard} if eimpl == "native" else {}))
         if hasattr(eng, "epilogue_on_producer") and not getattr(eng, "inline", True):
             eng.epilogue_on_producer = (epi or a.epi) == "producer"
         pad_fn = (lambda n: eng.layout(n).n_pad) if eng is not None else None
@@ -293,7 +293,8 @@ def main(argv=None):
                 "panels": tr.panel_plans[0]["chunks"] if tr.panel_plans else 0,
                 "ring_sub": int(getattr(eng, "ring_sub", 1)) if algo == "ring" else None,
                 "epilogue_stream": ("compute" if getattr(eng, "epilogue_on_producer", False) else "comm")
-                if eng is not None and not getattr(eng, "inline", True) else "inline"}
+                if eng is not None and not getattr(eng, "inline", True) else "inline",
+                "shard_update": bool(getattr(tr, "shard", False))}
         return Setup(name, eng, model, tr, info)
 
     def release(setup):
@@ -309,10 +310,12 @@ def main(argv=None):
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
 
-    def batch(mb, seed):
+    def batch(mb, seed, model=None):
         g = torch.Generator().manual_seed(seed + rank)
-        x = (torch.rand(mb, SIZES[0], generator=g) * 2 - 1).to(device=device, dtype=dtype)
-        y = torch.randint(0, SIZES[-1], (mb,), generator=g, dtype=torch.int32).to(device)
+        sizes = model.sizes if model is not None else SIZES
+        x = (torch.rand(mb, sizes[0], generator=g) * 2 - 1).to(device=device,
+                                                                dtype=model.dtype if model is not None else dtype)
+        y = torch.randint(0, sizes[-1], (mb,), generator=g, dtype=torch.int32).to(device)
         return x, y
 
     stall_rank = int(os.environ.get("FAN_BENCH_STALL_RANK", "-1"))
@@ -350,7 +353,7 @@ def main(argv=None):
 
     def _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace, wait_s=None):
         trainer, model, engine = setup.trainer, setup.model, setup.engine
-        x, y = batch(mb, seed)
+        x, y = batch(mb, seed, model)
         wd.arm(f"warmup {tag} mb={mb}")
         if tag in ("timed", "ref") and cuda and a.settle_ms > 0:
             # The shader clock needs ~50 ms of sustained load to reach the level a training run holds: the driver's
@@ -438,6 +441,10 @@ def main(argv=None):
             # which no backward is left to hide, starts a panel earlier; dp.py panels)
             arms.append(dict(name="rccl_mesh_panels4", kind="bfp", algo="mesh", transport="native", panels=4))
             arms.append(dict(name="p2p_mesh_panels4", kind="bfp", algo="mesh", transport="p2p", panels=4))
+            # sharded update (ZeRO-1 style): each owner reduces + applies SGD to its shard, the ranks all-gather the new
+            # bf16 weights into the layer's next weight buffer (no deferred epilogue, 1/N of the update pass per rank)
+            arms.append(dict(name="rccl_mesh_shard", kind="bfp", algo="mesh", transport="native", shard=True))
+            arms.append(dict(name="p2p_mesh_shard", kind="bfp", algo="mesh", transport="p2p", shard=True))
             # each request's decode + SGD epilogue on the comm stream as soon as its all-gather lands (overlapping the
             # rest of the backward) instead of on the compute stream after the last backward GEMM
             arms.append(dict(name="rccl_mesh_epicomm", kind="bfp", algo="mesh", transport="native", epi="comm"))
@@ -464,11 +471,19 @@ def main(argv=None):
                 setup = build(spec["name"], spec["kind"], algo=spec.get("algo", "mesh"), rings=spec.get("rings", 1),
                               transport=spec["transport"], gemm=spec.get("gemm", "persistent"),
                               sdma=spec.get("sdma", False), panels=spec.get("panels", 0),
-                              ring_sub=spec.get("ring_sub", 1), epi=spec.get("epi"), engine=spec.get("engine"))
+                              ring_sub=spec.get("ring_sub", 1), epi=spec.get("epi"), engine=spec.get("engine"),
+                              shard=spec.get("shard", False))
                 rec.update(setup.info)
                 t_arm = time.perf_counter()
                 log(f"arm {spec['name']}: built, running the exactness gate")
                 g = gate.allreduce_exactness(setup.engine, timeout_s=arm_wait)
+                if g["exact"] and cuda and hasattr(setup.engine, "C"):
+                    # the update half too (seeded master / momentum, one allreduce_sgd): the sharded arms' owner
+                    # SGD + weight all-gather, the others' decode + SGD epilogue, bit for bit against the oracle
+                    gu = gate.update_exactness(setup.engine, timeout_s=arm_wait)
+                    g = dict(g, update_exact=gu["exact"], update_sharded=gu["sharded"],
+                             exact=g["exact"] and gu["exact"],
+                             mismatch_ranks=sorted(set(g["mismatch_ranks"]) | set(gu["mismatch_ranks"])))
                 rec["exact"] = g["exact"]
                 log(f"arm {spec['name']}: gate exact={g['exact']} ({time.perf_counter() - t_arm:.1f} s)")
                 arm_gates[spec["name"]] = g
@@ -589,21 +604,18 @@ def main(argv=None):
     can_trace = (not a.no_trace and hasattr(engine, "trace") and not getattr(engine, "inline", True))
 
     # ------------------------------------------------------------------ reference batch, headline, traced pass
+    elapsed, t_enqueue, loss, _, graphed = run(main_setup, mb, 1234, a.warmup, a.steps, "timed", graph_ok=True)
+    ms = elapsed / a.steps * 1e3
+    log(f"headline: {ms:.4f} ms/step over {a.steps} steps")
     ref = None
     if a.ref_mb and a.ref_mb != mb:
-        # The reference-batch measurement runs first. A short step: a longer window on the GPU (a host hiccup is then
-        # a smaller share of it). Its ~50 ms of sustained load also brings the shader clock to the level a training
-        # run holds, which a short headline window right after start-up would otherwise partly miss (same box:
-        # 5 warmup + 20 steps read 1.080-1.100 ms/step, 40 + 20 read 1.039-1.051, 5 + 200 read 1.029;
-        # profiles/r3_warmup_clock_ramp.txt). The headline still times exactly W warmup + K steps of its own batch.
+        # The reference-batch cell runs after the headline, with its own settle phase (both cells are measured alike);
+        # a short step, so a longer window (a host hiccup is then a smaller share of it).
         ref_steps = max(a.steps, REF_STEPS) if cuda else a.steps
         e2, _, _, _, _ = run(main_setup, a.ref_mb, 4321, a.warmup, ref_steps, "ref")
         ref = {"mb_per_gpu": a.ref_mb, "global_batch": a.ref_mb * world, "steps": ref_steps,
                "samples_per_s": round(a.ref_mb * world * ref_steps / e2, 2),
                "ms_per_step": round(e2 / ref_steps * 1e3, 4)}
-    elapsed, t_enqueue, loss, _, graphed = run(main_setup, mb, 1234, a.warmup, a.steps, "timed", graph_ok=True)
-    ms = elapsed / a.steps * 1e3
-    log(f"headline: {ms:.4f} ms/step over {a.steps} steps")
     tr = run(main_setup, mb, 1234, 1, a.steps, "traced", trace=True)[3] if can_trace else None
 
     def record(dist_rec, extras_s, aborted=None):
@@ -652,6 +664,7 @@ def main(argv=None):
                 "fused_update_in_gemm": bool(getattr(trainer, "fused_update", False)),
                 "epilogue_stream": ("compute" if getattr(engine, "epilogue_on_producer", False) else "comm")
                 if engine is not None and not getattr(engine, "inline", True) else "inline",
+                "shard_update": info.get("shard_update", False),
             },
             "extra": {
                 "achieved_tflops": round(flops / 1e12, 2),
@@ -704,23 +717,35 @@ def main(argv=None):
     t_extra0 = time.perf_counter()
     if a.extra_budget > 0:
         if world == 1 and not a.force_dist and engine is not None:
-            def split(fused, force):
-                s = build("split", a.compress, transport="auto", fused=fused, force=force)
+            def split(fused, force, shard=None):
+                s = build("split", a.compress, transport="auto", fused=fused, force=force, shard=shard)
                 try:
                     e, _, _, _, _ = run(s, mb, 1234, 3, a.steps, "split")
                     return round(e / a.steps * 1e3, 4)
                 finally:
                     release(s)
 
-            def forced():
+            def forced(shard=False):
                 if not (torch.distributed.is_initialized()):
                     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                     os.environ["MASTER_PORT"] = str(_free_port())
                     D.init_distributed(force=True)
-                return split(None, True)
+                return split(None, True, shard)
 
             extra("unfused_update_ms_per_step", lambda: split(False, False), 10)
             extra("forced_dist_ms_per_step", forced, 20)
+            # the same multi-rank path with the sharded update (owner reduce + SGD fused, weight all-gather)
+            extra("forced_dist_shard_ms_per_step", lambda: forced(True), 20)
+
+            def config5_forced():
+                if not torch.distributed.is_initialized():
+                    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                    os.environ["MASTER_PORT"] = str(_free_port())
+                    D.init_distributed(force=True)
+                return _config5(a, world, device, main_setup.info, ctx, native_transport, p2p_comm, make_engine, ctrl,
+                                eng_timeout, forced=NativeTransport(force_collectives=True))
+
+            extra("config5", config5_forced, 30)
 
         def ref_workload():
             """The reference's own benchmark (sw/run.sh:16: mlp_mpi_example_f32 20 5376 0 A 32 32 32 2048 x 11 over 3
@@ -802,26 +827,29 @@ def main(argv=None):
     return 0
 
 
-def _config5(a, world, device, info, ctx, native_transport, p2p_comm, make_engine, ctrl, timeout_s):
-    """BASELINE config 5 at world > 1: BERT-base backward GEMMs overlapped with each layer bucket's BFP all-reduce +
-    fused SGD over the headline's transport and algorithm (bench/bert_overlap.py measure(): compute only, comm only,
-    both; 3 rounds, max over ranks). At world 1 the "comm" is CU work with no link time to hide,
-    so the record carries it only where links are."""
+def _config5(a, world, device, info, ctx, native_transport, p2p_comm, make_engine, ctrl, timeout_s, forced=None):
+    """BASELINE config 5: a BERT-base backward whose bwd-weight GEMMs encode each layer bucket's gradient for its BFP
+    all-reduce + fused SGD, issued right after the layer (bench/bert_overlap.py measure(): compute only, comm only,
+    both; 3 rounds, max over ranks), over the headline's transport and algorithm; at world 1 (``forced``: the 1-rank
+    native transport) through the full multi-rank path with its side-stream engine."""
     if device.type != "cuda":
         return {"skipped": "CPU run"}
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench"))
     import bert_overlap
 
     comm, t = None, ctrl
-    if info.get("transport") == "p2p":
+    if forced is not None:
+        t = forced
+    elif info.get("transport") == "p2p":
         comm = p2p_comm()
         comm.sdma = info.get("copy") == "sdma"
     else:
         t = native_transport() or ctrl
     eng = make_engine(t, "bfp", rounding=a.rounding, algo=info.get("algo", "mesh"), rings=max(1, info.get("rings", 1)),
-                      impl="native", comm=comm, timeout_s=timeout_s)
+                      impl="native", comm=comm, timeout_s=timeout_s, force_comm=forced is not None)
     r = bert_overlap.measure(eng, device, world, tokens=4096, layers=12, rounds=3)
-    r.update(transport="p2p" if comm is not None else getattr(t, "name", "torch"), algo=info.get("algo", "mesh"))
+    r.update(transport="p2p" if comm is not None else getattr(t, "name", "torch"), algo=info.get("algo", "mesh"),
+             forced_1rank=forced is not None)
     return r
 
 
@@ -949,6 +977,8 @@ def _dist_report(setup, world, rank, device, D, gate_rec):
 
     engine, model = setup.engine, setup.model
     C = getattr(engine, "C", None)
+    if getattr(setup.trainer, "shard", False):  # owner-sharded master / momentum: gather them before comparing
+        setup.trainer.gather_state()
     mine = {
         "digest": replica_digest([l.master for l in model.layers]),
         "comm_ranks": int(C.comm_ranks) if C is not None else (world if engine is not None else 1),
@@ -970,6 +1000,7 @@ def _dist_report(setup, world, rank, device, D, gate_rec):
         "allreduce_exact": gate_rec["exact"] if gate_rec is not None else None,
         "allreduce_gate": gate_rec,
         "replicas_identical": ident,
+        "master_gathered_from_owners": bool(getattr(setup.trainer, "shard", False)),
         "replica_digests": digests if not ident else digests[0],
     }
 

@@ -28,49 +28,107 @@ from fpga_ai_nic_amd.parallel.transport import ThreadFabric, TorchDistTransport 
 from fpga_ai_nic_amd.utils import dist as D  # noqa: E402
 
 
+def _offsets(bucket):
+    """tensor name -> (flat offset in the bucket, shape)"""
+    off, out = 0, {}
+    for nm, shp in bucket.tensors:
+        k = 1
+        for d in shp:
+            k *= d
+        out[nm] = (off, shp)
+        off += k
+    return out
+
+
+# (linear, tensor prefix inside the layer bucket, fin, fout) in backward order
+_LINEARS = (("ffn_out", "output.dense", bert.FFN, bert.HIDDEN), ("ffn_in", "intermediate.dense", bert.HIDDEN, bert.FFN),
+            ("attn_out", "attention.output.dense", bert.HIDDEN, bert.HIDDEN),
+            ("qkv", "attention.self.qkv", bert.HIDDEN, 3 * bert.HIDDEN))
+
+
 def measure(eng, dev, world, tokens=4096, layers=12, rounds=5, only=""):
-    """Config 5 on an engine: the BERT-base layers' backward GEMMs (compute stream) and each layer bucket's
-    all-reduce + fused SGD (the engine's stream), as compute only, comm only and both; medians over ``rounds``
-    (max over ranks). Also called by bench.py at world > 1 (``extra.config5``)."""
+    """Config 5 on an engine: a BERT-base backward whose gradients ARE the all-reduce's input. Per encoder layer (last
+    first) the four projections' bwd-data GEMM (bf16 dX) and bwd-weight GEMM run on the compute stream; each
+    bwd-weight GEMM writes its dW — and, fused, its bias gradient — straight into the layer's gradient bucket, BFP-
+    encoded by the GEMM epilogue into the engine's wire buffer when the engine takes producer-encoded input (the
+    MLP's dp.py path; otherwise f32 into the bucket and the engine encodes). The LayerNorm gradients (no GEMM) are
+    encoded after the layer's GEMMs, and the bucket's all-reduce + fused SGD is issued right after that, on the
+    engine's stream, consuming exactly what the GEMMs produced. The pooler bucket is issued first and the embedding
+    bucket last, where a real backward produces them (their producers — the pooler's tiny GEMM, the embedding
+    scatter-add — are modelled as the encode of their buckets). Timed as compute only (GEMMs + encodes), comm only
+    (the all-reduces of the encoded buckets) and both; medians over ``rounds`` (max over ranks). Also called by
+    bench.py (``extra.config5``)."""
+    from fpga_ai_nic_amd import _ext
+
+    C = _ext.require()
     buckets = bert.gradient_buckets(layers)
+    T = tokens
+    acts = {}  # per projection: X [T, fin] (ReLU-free layer input) and dY [T, fout], shared by every layer
+    for name, _, fin, fout in _LINEARS:
+        acts[name] = ((torch.rand(T, fin, device=dev) * 2 - 1).to(torch.bfloat16),
+                      ((torch.rand(T, fout, device=dev) * 2 - 1) * 1e-2).to(torch.bfloat16),
+                      ((torch.rand(fin, fout, device=dev) * 2 - 1) * 0.02).to(torch.bfloat16),
+                      torch.empty(T, fin, device=dev, dtype=torch.bfloat16))
     bufs = []
+    prepacked_buckets = 0
     for b in buckets:
         L = eng.layout(b.numel)
-        g = (torch.randn(L.n_pad, device=dev) * 1e-3).to(torch.bfloat16)
+        g = torch.randn(L.n_pad, device=dev) * 1e-3
         g[b.numel:] = 0
         w = torch.randn(L.n_pad, device=dev) * 0.02
-        bufs.append((b, g, w, w.to(torch.bfloat16)))
-    T = tokens
-    gemms = []
-    for name, M, N, K, a_t, b_t in bert.layer_backward_gemms(T):
-        A = torch.randn(K, M, device=dev).to(torch.bfloat16) if a_t else torch.randn(M, K, device=dev).to(torch.bfloat16)
-        B = torch.randn(N, K, device=dev).to(torch.bfloat16) if b_t else torch.randn(K, N, device=dev).to(torch.bfloat16)
-        C = torch.empty(M, N, device=dev, dtype=torch.float32 if "wgrad" in name else torch.bfloat16)
-        gemms.append((A, a_t, B, b_t, C))
+        tgt = eng.prepack_target(g, b.numel) if getattr(eng, "prepack", False) else None
+        prepacked_buckets += tgt is not None
+        bufs.append((b, g, w, w.to(torch.bfloat16), L, tgt, _offsets(b)))
 
-    def layer_bwd():
-        for A, a_t, B, b_t, C in gemms:
-            G.gemm(A, a_t, B, b_t, C)
+    def encode_range(g, tgt, lo, hi):
+        if tgt is not None and hi > lo:
+            C.wire_pack_range(g, tgt[0], tgt[1], lo, hi, tgt[3])
 
-    def comm(b, g, w, lp):
-        return eng.allreduce_sgd(g, w, lp, n_valid=b.numel, lr=1e-4, grad_scale=1.0 / world, name=b.name)
+    def produce(bi):
+        """bucket bi's gradient, produced into the bucket (and its wire buffer)"""
+        b, g, _, _, L, tgt, offs = bufs[bi]
+        if not b.name.startswith("layer"):
+            encode_range(g, tgt, 0, b.numel)
+            return
+        pre = f"encoder.layer.{b.name[5:]}."
+        for name, tn, fin, fout in _LINEARS:
+            X, dY, W, dX = acts[name]
+            G.gemm(dY, False, W, True, dX)  # bwd-data dX = dY . W^T
+            woff, _ = offs[pre + tn + ".weight"]
+            boff, _ = offs[pre + tn + ".bias"]
+            dW = g[woff: woff + fin * fout].view(fin, fout)
+            db = g[boff: boff + fout]
+            if tgt is not None:
+                G.gemm(X, True, dY, False, dW, G.EPI_WIRE, colsum=db,
+                       wire=(tgt[0], tgt[1], tgt[2], tgt[3], tgt[4], woff))
+            else:
+                G.gemm(X, True, dY, False, dW, G.EPI_NONE, colsum=db)
+        for ln in ("attention.output.LayerNorm", "output.LayerNorm"):  # [weight | bias], no GEMM
+            lo, _ = offs[pre + ln + ".weight"]
+            encode_range(g, tgt, lo, lo + 2 * bert.HIDDEN)
+
+    def comm(bi):
+        b, g, w, lp, L, tgt, _ = bufs[bi]
+        kw = {"prepacked": (tgt[0], L.n_pad)} if tgt is not None else {}
+        return eng.allreduce_sgd(g, w, lp, n_valid=b.numel, lr=1e-4, grad_scale=1.0 / world, name=b.name, **kw)
 
     def run(do_compute, do_comm):
         D.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         hs = []
-        for li, (b, g, w, lp) in enumerate(bufs):
-            if do_compute and b.name.startswith("layer"):
-                layer_bwd()
+        for bi in range(len(bufs)):
+            if do_compute:
+                produce(bi)
             if do_comm:
-                hs.append(comm(b, g, w, lp))
+                hs.append(comm(bi))
         for h in hs:
             h.wait()
         torch.cuda.synchronize()
         return D.max_over_ranks(time.perf_counter() - t0)
 
     kinds = {"compute": (True, False), "comm": (False, True), "overlap": (True, True)}
+    run(True, False)  # the buckets' wire buffers hold a producer's encoding before any comm-only round
     run(*kinds[only or "overlap"])  # warmup (GEMM plan tuning, engine scratch): in --only mode of that kind only
     res = {"compute": [], "comm": [], "overlap": []}
     for _ in range(rounds):
@@ -87,6 +145,8 @@ def measure(eng, dev, world, tokens=4096, layers=12, rounds=5, only=""):
     flops = bert.layer_backward_flops(T) * layers
     return {"tokens_per_gpu": T, "params": bert.num_params(layers), "t_compute_ms": round(tc, 3),
             "t_comm_ms": round(tm, 3), "t_overlap_ms": round(to, 3), "overlap_efficiency": round(eff, 3),
+            "overlap_vs_compute": round(to / tc, 3) if tc > 0 else None,
+            "producer_encoded_buckets": prepacked_buckets, "buckets": len(bufs),
             "bwd_gemm_tflops": round(flops / (tc / 1e3) / 1e12, 1) if tc > 0 else None,
             "comm_algo_bw_GBps": round(bert.num_params(layers) * 4 / (tm / 1e3) / 1e9, 1) if tm > 0 else None}
 

@@ -310,5 +310,15 @@ void launch_wire_pack_to(int codec, int in_dtype, const void* in, const WirePtrs
 // release at the end (the owner's reduced shard goes straight into every peer's receive slot).
 void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots, int self_pos,
                            const void* local, const WirePtrs& dst, int n_dst, size_t n_s, hipStream_t stream);
+// Sharded update of the owner's shard (engine shard_update mode, ZeRO-1 style): sum the N received wire shards
+// (slot self_pos replaced by the dense local operand), take the sum through the wire codec's round trip in registers
+// (exactly the values every rank would decode from the re-encoded owner shard in the unsharded schedule), apply SGD to
+// `master` / `mom` (this shard's planes; elements at or past n_valid keep their values) and write the updated
+// weights in bf16 to every non-null dst.p[i] (i < n_dst: this rank's own copy and, on the direct P2P transport,
+// every peer's receive slot), ending with the P2P release of `rel` (-1: none, a local output). Same arithmetic in
+// the same order as wire_reduce (re-encode) + wire_sgd, so the weights are bit-identical to the unsharded schedule.
+void launch_wire_reduce_sgd(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots,
+                            int self_pos, const void* local, float* master, float* mom, SgdParams p, size_t n_valid,
+                            const WirePtrs& dst, int n_dst, size_t n_s, bool peers, hipStream_t stream);
 
 }  // namespace fan

@@ -197,6 +197,74 @@ __global__ void __launch_bounds__(kBlock)
   p2p_release(rel);
 }
 
+// The value a rank decodes after the owner re-encodes `v` (one 16-value group) with codec C.
+template <int C>
+__device__ __forceinline__ void codec_roundtrip16(float v[16]) {
+  if constexpr (C == kBfpTrunc || C == kBfpRne) {
+    uint32_t mx = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mx = max(mx, __float_as_uint(v[j]) & 0x7FFFFFFFu);
+    const uint32_t E = mx >> 23;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int32_t q = (C == kBfpTrunc) ? bfp_encode_trunc(__float_as_uint(v[j]), E) : bfp_encode_rne(v[j], E);
+      const int32_t q8 = (int32_t)(int8_t)(uint8_t)((uint32_t)q & 0xFFu);  // the stored byte, as the decoder reads it
+      v[j] = (C == kBfpTrunc) ? bfp_decode_trunc(q8, E) : bfp_decode_rne(q8, E);
+    }
+  } else if constexpr (C == kRawBf16) {
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      const uint32_t u = pack_bf16x2(v[j], v[j + 1]);
+      v[j] = __uint_as_float(u << 16);
+      v[j + 1] = __uint_as_float(u & 0xFFFF0000u);
+    }
+  }
+}
+
+template <typename TL, int C, bool HAS_MOM>
+__global__ void __launch_bounds__(kBlock)
+    wire_reduce_sgd_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
+                           const TL* __restrict__ local, float* __restrict__ master, float* __restrict__ mom,
+                           SgdParams p, size_t n_valid, WirePtrs dst, int n_dst, size_t n_s, int rel) {
+  const size_t tasks = n_s >> 4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+    const size_t le = t << 4;
+    float acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.0f;
+    for (int r = 0; r < n_slots; ++r) {
+      float v[16];
+      if (r == self_pos) DenseLane16<TL>::load16(local, le, v);
+      else WireLane16<C>::load16(slots + (size_t)r * slot_stride, n_s, le, v);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] += v[j];
+    }
+    codec_roundtrip16<C>(acc);
+    float w[16], m[16];
+    DenseLane16<float>::load16(master, le, w);
+    if (HAS_MOM) DenseLane16<float>::load16(mom, le, m);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {  // wire_sgd_kernel's operations, in its order
+      if (le + j >= n_valid) continue;
+      float gj = acc[j] * p.grad_scale;
+      if (p.weight_decay != 0.0f) gj = fmaf(p.weight_decay, w[j], gj);
+      if (HAS_MOM) {
+        m[j] = fmaf(p.momentum, m[j], gj);
+        gj = p.nesterov ? fmaf(p.momentum, m[j], gj) : m[j];
+      }
+      w[j] = fmaf(-p.lr, gj, w[j]);
+    }
+    if (le < n_valid) {
+      DenseLane16<float>::store16(master, le, w);
+      if (HAS_MOM) DenseLane16<float>::store16(mom, le, m);
+    }
+    for (int i = 0; i < n_dst; ++i)
+      if (dst.p[i] != nullptr) DenseLane16<bf16_t>::store16(reinterpret_cast<bf16_t*>(dst.p[i]), le, w);
+  }
+  if (rel >= 0) p2p_release(rel);
+}
+
 template <typename TOUT, int C>
 __global__ void __launch_bounds__(kBlock) wire_unpack_strided_kernel(const uint8_t* __restrict__ in,
                                                                     size_t shard_stride, TOUT* __restrict__ out,
@@ -436,6 +504,44 @@ void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t
       hipLaunchKernelGGL((wire_reduce_to_kernel<bf16_t, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,
                          slot_stride, n_slots, self_pos, (const bf16_t*)local, dst, n_dst, n_s, p2p_release_mode());
   });
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+template <int C>
+static void reduce_sgd_dispatch(int local_dtype, int grid, const void* slots, size_t slot_stride, int n_slots,
+                                int self_pos, const void* local, float* master, float* mom, SgdParams p,
+                                size_t n_valid, const WirePtrs& dst, int n_dst, size_t n_s, int rel,
+                                hipStream_t stream) {
+  const uint8_t* sl = (const uint8_t*)slots;
+  if (local_dtype == kF32) {
+    if (mom)
+      hipLaunchKernelGGL((wire_reduce_sgd_kernel<float, C, true>), grid, kBlock, 0, stream, sl, slot_stride, n_slots,
+                         self_pos, (const float*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+    else
+      hipLaunchKernelGGL((wire_reduce_sgd_kernel<float, C, false>), grid, kBlock, 0, stream, sl, slot_stride, n_slots,
+                         self_pos, (const float*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+  } else {
+    if (mom)
+      hipLaunchKernelGGL((wire_reduce_sgd_kernel<bf16_t, C, true>), grid, kBlock, 0, stream, sl, slot_stride, n_slots,
+                         self_pos, (const bf16_t*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+    else
+      hipLaunchKernelGGL((wire_reduce_sgd_kernel<bf16_t, C, false>), grid, kBlock, 0, stream, sl, slot_stride,
+                         n_slots, self_pos, (const bf16_t*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+  }
+}
+
+void launch_wire_reduce_sgd(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots,
+                            int self_pos, const void* local, float* master, float* mom, SgdParams p, size_t n_valid,
+                            const WirePtrs& dst, int n_dst, size_t n_s, bool peers, hipStream_t stream) {
+  check_ns(n_s);
+  FAN_CHECK(n_dst <= kMaxPeers && local != nullptr && master != nullptr,
+            "reduce_sgd: local operand, master shard and at most 16 destinations");
+  if (n_s == 0) return;
+  const int cap = peers ? std::min(wire_max_blocks(), p2p_grid_cap()) : wire_max_blocks();
+  const int grid = stream_grid(n_s / 16, kBlock, cap);
+  const int rel = peers ? p2p_release_mode() : -1;
+  FAN_CODEC_SWITCH(codec, reduce_sgd_dispatch<C>(local_dtype, grid, slots, slot_stride, n_slots, self_pos, local,
+                                                 master, mom, p, n_valid, dst, n_dst, n_s, rel, stream));
   FAN_HIP_CHECK(hipGetLastError());
 }
 

@@ -160,7 +160,8 @@ void register_engine(pybind11::module_& m) {
   py::class_<AllReduceEngine>(m, "AllReduceEngine")
       .def(py::init([](Comm* comm, int rank, int world, int codec, int algo, int rings, int64_t max_slice,
                        bool compat, double timeout_s, int priority, bool force_comm, int device, int verify,
-                       int64_t chunk_elems, c10::optional<std::vector<std::vector<int>>> links, int ring_sub) {
+                       int64_t chunk_elems, c10::optional<std::vector<std::vector<int>>> links, int ring_sub,
+                       int shard_update) {
              EngineConfig c;
              c.codec = codec;
              c.algo = algo;
@@ -173,6 +174,7 @@ void register_engine(pybind11::module_& m) {
              c.verify = verify;
              c.chunk_elems = chunk_elems;
              c.ring_sub = ring_sub;
+             c.shard_update = shard_update;
              if (links) {
                TORCH_CHECK((int)links->size() == world, "links: world x world expected");
                c.links.assign((size_t)world * world, 0);
@@ -186,8 +188,19 @@ void register_engine(pybind11::module_& m) {
            py::keep_alive<1, 2>(), py::arg("comm").none(true), py::arg("rank"), py::arg("world"), py::arg("codec"),
            py::arg("algo"), py::arg("rings"), py::arg("max_slice_elems"), py::arg("compat_owner_fp32"),
            py::arg("timeout_s"), py::arg("stream_priority"), py::arg("force_comm"), py::arg("device"),
-           py::arg("verify") = -1, py::arg("chunk_elems") = 0, py::arg("links") = py::none(), py::arg("ring_sub") = 0)
+           py::arg("verify") = -1, py::arg("chunk_elems") = 0, py::arg("links") = py::none(), py::arg("ring_sub") = 0,
+           py::arg("shard_update") = -1)
       .def_property_readonly("ring_sub", &AllReduceEngine::ring_sub, "sub-slices per direct-ring hop message")
+      .def_property_readonly("shard_update", &AllReduceEngine::shard_update,
+                             "sharded weight update in force (owner reduce + SGD, all-gather of the bf16 weights)")
+      .def("gather_owned",
+           [](AllReduceEngine& e, at::Tensor& plane, int64_t n) {
+             FAN_T_CUDA_CONTIG(plane);
+             TORCH_CHECK(plane.scalar_type() == at::kFloat && plane.numel() >= e.layout(n).n_pad, "f32 bucket plane");
+             py::gil_scoped_release nogil;
+             e.gather_owned(plane.data_ptr<float>(), n);
+           },
+           "all-gather an owner-sharded f32 plane (master / momentum of a sharded-update engine) in place")
       .def("layout",
            [](AllReduceEngine& e, int64_t n, int64_t shard, int64_t chunks) {
              const EngineLayout L = e.layout(n, shard, chunks);
@@ -340,6 +353,7 @@ void register_engine(pybind11::module_& m) {
              d["forced_commits"] = c.forced_commits;
              d["verified_rows"] = c.verified_rows;
              d["direct_rounds"] = c.direct_rounds;
+             d["sharded_updates"] = c.sharded_updates;
              d["peer_bytes"] = c.peer_bytes;
              return d;
            },

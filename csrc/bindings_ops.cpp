@@ -30,7 +30,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux, bool accumulate,
           int64_t split_k, const c10::optional<at::Tensor>& workspace, int64_t tile_bm, int64_t tile_bn,
           const c10::optional<at::Tensor>& colsum, int64_t tile_waves, const c10::optional<at::Tensor>& wire,
-          int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period,
+          int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period, int64_t wire_off,
           const c10::optional<at::Tensor>& upd_master, const c10::optional<at::Tensor>& upd_lp,
           const c10::optional<at::Tensor>& upd_mom, double upd_lr, double upd_grad_scale, double upd_weight_decay,
           double upd_momentum, bool upd_nesterov) {
@@ -79,7 +79,8 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
                 "wire epilogue needs a contiguous uint8 GPU wire buffer");
     TORCH_CHECK(wire_shard > 0 && wire_shard % 256 == 0, "wire_shard must be a positive multiple of 256");
     // with colsum the encoded bias segment follows C: flat M*ldc .. M*ldc + N - 1
-    const int64_t last = g.colsum ? (int64_t)g.M * g.ldc + g.N - 1 : (int64_t)(g.M - 1) * g.ldc + g.N - 1;
+    TORCH_CHECK(wire_off >= 0 && wire_off % 16 == 0, "wire_off must be a non-negative multiple of 16");
+    const int64_t last = wire_off + (g.colsum ? (int64_t)g.M * g.ldc + g.N - 1 : (int64_t)(g.M - 1) * g.ldc + g.N - 1);
     const int64_t need = (last / wire_shard + 1) * (int64_t)wire_shard_bytes((int)wire_codec, (size_t)wire_shard);
     TORCH_CHECK(wire->numel() >= need, "wire buffer too small: ", wire->numel(), " < ", need);
     g.wire = wire->data_ptr<uint8_t>();
@@ -87,6 +88,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     g.wire_own = (int)wire_own;
     g.wire_period = (int)wire_period;
     g.wire_codec = (int)wire_codec;
+    g.wire_off = wire_off;
     if (upd_master) {  // fused local update: the bucket planes cover every flat index the epilogue touches
       auto plane = [&](const at::Tensor& t, at::ScalarType st, const char* what) {
         TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == st && t.numel() > last &&
@@ -217,7 +219,7 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("workspace") = pybind11::none(), pybind11::arg("tile_bm") = 0, pybind11::arg("tile_bn") = 0,
         pybind11::arg("colsum") = pybind11::none(), pybind11::arg("tile_waves") = 0,
         pybind11::arg("wire") = pybind11::none(), pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1,
-        pybind11::arg("wire_codec") = 1, pybind11::arg("wire_period") = 0,
+        pybind11::arg("wire_codec") = 1, pybind11::arg("wire_period") = 0, pybind11::arg("wire_off") = 0,
         pybind11::arg("upd_master") = pybind11::none(), pybind11::arg("upd_lp") = pybind11::none(),
         pybind11::arg("upd_mom") = pybind11::none(), pybind11::arg("upd_lr") = 0.0,
         pybind11::arg("upd_grad_scale") = 1.0, pybind11::arg("upd_weight_decay") = 0.0,

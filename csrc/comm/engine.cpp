@@ -32,6 +32,11 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
     for (int i = 0; i < world; ++i) orders_[0][i] = i;
   }
   inline_ = world == 1 && !cfg.force_comm;
+  if (cfg_.shard_update < 0) {
+    const char* su = std::getenv("FAN_SHARD_UPDATE");
+    cfg_.shard_update = su && su[0] == '1' ? 1 : 0;
+  }
+  shard_upd_ = cfg_.shard_update > 0 && cfg.algo == 0 && !inline_ && !cfg.compat_owner_fp32;
   bool side_epi = false;
   if (inline_) {
     const char* se = std::getenv("FAN_SIDE_EPI");
@@ -154,7 +159,9 @@ EngineLayout AllReduceEngine::layout(int64_t n, int64_t shard, int64_t chunks) c
     int64_t chunk = cfg_.chunk_elems;
     if (P2PComm* d = comm_ ? comm_->direct() : nullptr) {
       // a P2P message (one wire shard) must fit one arena slot: chunk the bucket so that it does
-      const int64_t max_shard = (int64_t)(d->payload_bytes() / wire_shard_bytes(cfg_.codec, 256)) * 256;
+      // (sharded update: round 2 carries 2 B per element of bf16 weights)
+      const size_t per256 = std::max<size_t>(wire_shard_bytes(cfg_.codec, 256), shard_upd_ ? 512 : 0);
+      const int64_t max_shard = (int64_t)(d->payload_bytes() / per256) * 256;
       FAN_CHECK(max_shard >= 256, "p2p arena slot smaller than one 256-element wire shard");
       chunk = std::min<int64_t>(chunk, max_shard * N);
     }
@@ -293,6 +300,26 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     }
   }
   mark(kTpExchanged);
+  if (shard_upd_ && update && out_sum == nullptr && lp != nullptr) {
+    // sharded update: the owner's reduce + round trip + SGD of shard r writes its new bf16 weights into lp's shard r,
+    // then the weights are all-gathered in place (every rank's lp shard q comes from rank q)
+    {
+      RoctxRange rr("fan/mesh/reduce_sgd");
+      const int64_t nv = std::max<int64_t>(0, std::min<int64_t>(n_valid - (int64_t)r * s, s));
+      WirePtrs out{};
+      out.p[0] = reinterpret_cast<uint8_t*>(lp + (size_t)r * s);
+      launch_wire_reduce_sgd(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), master + (size_t)r * s,
+                             mom ? mom + (size_t)r * s : nullptr, p, (size_t)nv, out, 1, (size_t)s, false, st);
+    }
+    mark(kTpReduced);
+    {
+      RoctxRange rr("fan/mesh/all_gather_weights");
+      comm_->all_gather(lp + (size_t)r * s, lp, (size_t)s * 2, st);
+      count_peers((size_t)s * 2);
+    }
+    counters_.sharded_updates++;
+    return {};
+  }
   {
     RoctxRange rr("fan/mesh/reduce");
     launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
@@ -339,21 +366,21 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
   const bool zero_copy = (c == kRawF32 && gdt == kF32) || (c == kRawBf16 && gdt == kBF16);
   // verify / fault hooks of one direct round: tag what this rank stored into each peer's slot (trailer tag 0), and
   // the receiver's check of every peer's message once its flag is up
-  auto tag_sent = [&](const P2PComm::Round& rd, const char* fault_site) {
+  auto tag_sent = [&](const P2PComm::Round& rd, const char* fault_site, size_t bytes) {
     bool first = true;
     for (int q = 0; q < N; ++q) {
       if (q == r) continue;
-      if (verify_) tag_direct(d->dst(rd, q), sb, d->dst_tag(rd, q, 0), (uint32_t)rd.seq, st);
-      if (first) fault_.maybe_corrupt(fault_site, d->dst(rd, q), sb, st);  // in flight: after its tag
+      if (verify_) tag_direct(d->dst(rd, q), bytes, d->dst_tag(rd, q, 0), (uint32_t)rd.seq, st);
+      if (first) fault_.maybe_corrupt(fault_site, d->dst(rd, q), bytes, st);  // in flight: after its tag
       first = false;
     }
   };
-  auto check_received = [&](const P2PComm::Round& rd, uint32_t site) {
+  auto check_received = [&](const P2PComm::Round& rd, uint32_t site, size_t bytes) {
     for (int q = 0; q < N; ++q) {
       if (q == r) continue;
       uint8_t* m = const_cast<uint8_t*>(d->src(rd, q));
-      fault_.maybe_corrupt("p2p_recv", m, sb, st);  // test hook: the slot changes after its flag was raised
-      if (verify_) verify_direct(m, sb, d->src_tag(rd, q, 0), (uint32_t)rd.seq, site, (uint32_t)q, st);
+      fault_.maybe_corrupt("p2p_recv", m, bytes, st);  // test hook: the slot changes after its flag was raised
+      if (verify_) verify_direct(m, bytes, d->src_tag(rd, q, 0), (uint32_t)rd.seq, site, (uint32_t)q, st);
     }
   };
   P2PComm::Round r1 = d->begin(st);
@@ -369,15 +396,48 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
     }
     if (prepacked || zero_copy) d->move(segs, st);
     else launch_wire_pack_to(c, gdt, g, to, (size_t)s, N, st);
-    tag_sent(r1, "mesh_pack");
+    tag_sent(r1, "mesh_pack", sb);
   }
   mark(kTpPacked);
   if (!fault_.maybe_drop("p2p_publish")) d->publish(r1, st);  // test hook: the round is never announced
   count_peers(sb, d);
   d->wait(r1, st);
-  check_received(r1, kSiteMeshDirectSend);
+  check_received(r1, kSiteMeshDirectSend, sb);
   mark(kTpExchanged);
   P2PComm::Round r2 = d->begin(st);
+  if (shard_upd_ && update && out_sum == nullptr && lp != nullptr) {
+    // sharded update: the owner reduces the received shards in place, takes the sum through the codec round trip,
+    // applies SGD to its master shard and stores its new bf16 weights straight into every peer's round-2 slot and
+    // into its own lp shard; each rank then copies the peers' weight shards into lp (the layer's next weights)
+    const size_t wb = (size_t)s * 2;
+    {
+      RoctxRange rr("fan/mesh/direct_reduce_sgd");
+      WirePtrs out{};
+      for (int q = 0; q < N; ++q) out.p[q] = q == r ? reinterpret_cast<uint8_t*>(lp + (size_t)r * s) : d->dst(r2, q);
+      const int64_t nv = std::max<int64_t>(0, std::min<int64_t>(n_valid - (int64_t)r * s, s));
+      launch_wire_reduce_sgd(c, gdt, d->src_base(r1), d->src_stride(), N, r, g + (size_t)r * s * esize(gdt),
+                             master + (size_t)r * s, mom ? mom + (size_t)r * s : nullptr, p, (size_t)nv, out, N,
+                             (size_t)s, true, st);
+      d->release(r1, st);
+      tag_sent(r2, "mesh_reduce", wb);
+    }
+    mark(kTpReduced);
+    if (!fault_.maybe_drop("p2p_publish")) d->publish(r2, st);
+    count_peers(wb, d);
+    d->wait(r2, st);
+    check_received(r2, kSiteMeshDirectGather, wb);
+    {
+      RoctxRange rr("fan/mesh/direct_weights");
+      std::vector<P2PCopy> segs;
+      for (int q = 0; q < N; ++q)
+        if (q != r) segs.push_back({d->src(r2, q), lp + (size_t)q * s, wb});
+      d->move(segs, st);
+    }
+    d->release(r2, st);
+    counters_.direct_rounds += 2;
+    counters_.sharded_updates++;
+    return {};
+  }
   {
     RoctxRange rr("fan/mesh/direct_reduce");
     WirePtrs out{};
@@ -385,13 +445,13 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh_direct(P2PComm* d, const EngineL
     launch_wire_reduce_to(c, gdt, d->src_base(r1), d->src_stride(), N, r, g + (size_t)r * s * esize(gdt), out, N,
                           (size_t)s, st);
     d->release(r1, st);
-    tag_sent(r2, "mesh_reduce");
+    tag_sent(r2, "mesh_reduce", sb);
   }
   mark(kTpReduced);
   if (!fault_.maybe_drop("p2p_publish")) d->publish(r2, st);
   count_peers(sb, d);
   d->wait(r2, st);
-  check_received(r2, kSiteMeshDirectGather);
+  check_received(r2, kSiteMeshDirectGather, sb);
   counters_.direct_rounds += 2;
   const uint8_t* Gv = d->src_base(r2);
   const size_t gstride = d->src_stride();
@@ -865,6 +925,33 @@ std::vector<EpiThunk> AllReduceEngine::run_ring_direct(P2PComm* d, const EngineL
     thunks.push_back([=](hipStream_t es) { epilogue(c, es, G, Sp, (int)nsh, off, part, master, lp, mom, n_valid, p, update, out_sum); });
   }
   return thunks;
+}
+
+void AllReduceEngine::gather_owned(float* plane, int64_t n) {
+  if (!shard_upd_ || world_ == 1 || comm_ == nullptr) return;
+  const EngineLayout L = layout(n);
+  if (L.algo != 0 || L.chunks != 1) return;  // the sharded schedule runs on unchunked mesh buckets only
+  FAN_HIP_CHECK(hipSetDevice(device_));
+  const int N = world_, r = rank_;
+  const int64_t s = L.shard;
+  hipStream_t st = stream_;
+  // every request that updated the plane has finished (its SGD ran on this engine's streams; not a device-wide sync:
+  // virtual ranks in one process would wait on each other's streams parked on this rank's coming flags)
+  FAN_HIP_CHECK(hipStreamSynchronize(stream_));
+  FAN_HIP_CHECK(hipStreamSynchronize(aux_stream_));
+  size_t max_bytes = (size_t)s * 4;
+  if (P2PComm* d = comm_->direct()) max_bytes = std::min(max_bytes, d->payload_bytes() / 256 * 256);
+  const int64_t piece = std::max<int64_t>(64, (int64_t)(max_bytes / 4) / 64 * 64);
+  uint8_t* G = scratch("gather_owned", (size_t)N * piece * 4);
+  for (int64_t off = 0; off < s; off += piece) {
+    const int64_t k = std::min(piece, s - off);
+    comm_->all_gather(plane + (size_t)r * s + off, G, (size_t)k * 4, st);
+    std::vector<P2PCopy> segs;
+    for (int q = 0; q < N; ++q)
+      if (q != r) segs.push_back({G + (size_t)q * k * 4, plane + (size_t)q * s + off, (size_t)k * 4});
+    launch_multi_copy(segs, st);
+  }
+  FAN_HIP_CHECK(hipStreamSynchronize(st));
 }
 
 void AllReduceEngine::tag_direct(const uint8_t* msg, size_t bytes, uint8_t* trailer, uint32_t seq, hipStream_t st) {

@@ -52,6 +52,12 @@ struct EngineConfig {
   // hw/all_reduce.sv:1155-1166) instead of after the whole slice; capped by the P2P arena depth - 1. 0: from
   // FAN_RING_SUB (default 1: lock-step hops).
   int ring_sub = 0;
+  // mesh, multi-rank: sharded weight update (ZeRO-1 style). The owner of shard q fuses its reduce with the BFP round
+  // trip + SGD of that shard (master / momentum of shard q are kept current on its owner only) and the ranks
+  // all-gather the updated bf16 WEIGHTS instead of the reduced gradient; the request writes its submit's `lp`
+  // (the trainer passes the layer's next weight buffer), so no epilogue waits for the bwd-data GEMM. Bit-identical
+  // weights to the unsharded schedule. Update requests of bf16 models without out_sum only. -1: FAN_SHARD_UPDATE.
+  int shard_update = -1;
 };
 
 struct EngineLayout {
@@ -80,6 +86,7 @@ struct EngineCounters {
   uint64_t forced_commits = 0;  // deferred epilogues committed because their slot was needed (> kSlots deferred)
   uint64_t verified_rows = 0;   // verify mode: message rows whose tags were checked on arrival
   uint64_t direct_rounds = 0;   // direct P2P rounds (kernels stored into / read from peer receive slots in place)
+  uint64_t sharded_updates = 0; // requests that ran the sharded update (owner reduce + SGD, weight all-gather)
   std::vector<int64_t> peer_bytes;  // message bytes sent to each peer (all-to-all, all-gather, ring hops, direct)
 };
 
@@ -163,6 +170,10 @@ class AllReduceEngine {
   bool is_inline() const { return table_->config().inline_mode; }
   int codec() const { return cfg_.codec; }
   int ring_sub() const;  // sub-slices per ring hop this engine runs (1 unless direct P2P ring streaming)
+  bool shard_update() const { return shard_upd_; }  // sharded weight update (EngineConfig::shard_update) in force
+  // All-gather an f32 bucket plane whose shard q is current on rank q only (a sharded-update engine's master /
+  // momentum) in place, in pieces that fit the transport; checkpoints and replica checks call it. Host-blocking.
+  void gather_owned(float* plane, int64_t n);
 
   // Enqueue the communication phase of a request. grad: padded flat buffer (f32 or bf16) ready on `producer`.
   // If `defer`, the weight update is enqueued later by commit(); otherwise immediately. Returns the slot.
@@ -286,6 +297,7 @@ class AllReduceEngine {
   // world 1 without forced collectives: nothing to overlap, so requests run inline on the producer's
   // stream (no cross-stream event packets); run_stream_ is the stream of the request being issued.
   bool inline_ = false;
+  bool shard_upd_ = false;
   hipStream_t run_stream_ = nullptr;
   volatile uint32_t* flags_host_ = nullptr;  // host-mapped done words (one 64-B line per slot)
   uint32_t* flags_dev_ = nullptr;

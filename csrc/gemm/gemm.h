@@ -57,6 +57,7 @@ struct GemmArgs {
   int wire_own = -1;
   int wire_period = 0;  // > 0: every shard s with s % wire_period == wire_own is owned (chunked mesh buckets)
   int wire_codec = 1;  // kBfpTrunc or kBfpRne
+  int64_t wire_off = 0;  // flat bucket index of C(0, 0): f = wire_off + m*ldc + n (a tensor inside a larger bucket)
   // kEpiWire fused local update (single-rank engine): instead of storing the wire, every encoded group is decoded
   // in registers and applied by SGD to the bucket planes at the same flat indices (upd_master f32, upd_lp bf16
   // copy, upd_mom optional; wire_own must be -1). See WireOut::um (gemm_bf16_kernel.h).

@@ -267,6 +267,9 @@ struct WireOut {
 #ifdef FAN_GEMM_STAMPS
   unsigned long long* stamps;  // diagnostic builds: s_memtime stamp buffer (see FAN_STAMP)
 #endif
+  // flat bucket index of C(0, 0) (GemmArgs::wire_off): a weight matrix that is not the first tensor of its bucket
+  // (a transformer layer's bucket holds several; bench/bert_overlap.py). bias_off is absolute (includes it).
+  uint32_t off;
 };
 
 // flat index -> (shard, position); f < 2^31, shard >= 256: the float estimate is off by at most one
@@ -367,12 +370,12 @@ __device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const
 template <bool UPD = false>
 __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
                                            int row, int col) {
-  const uint32_t f = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
-  const int sh = wire_store16<UPD>(v, f, wo);
+  const uint32_t loc = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
+  const int sh = wire_store16<UPD>(v, wo.off + loc, wo);
   if (sh >= 0 && (wo.own == kWireOwnAll || (wo.period > 0 ? sh % wo.period : sh) == wo.own)) {
 #pragma unroll
     for (int u = 0; u < 16; u += 4)
-      *reinterpret_cast<float4*>(C + f + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
+      *reinterpret_cast<float4*>(C + loc + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
   }
 }
 
@@ -1797,9 +1800,9 @@ void with_split_count(int sk, F&& f) {
 
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
 void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
-  const WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_period, a.wire_codec,
+  WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_period, a.wire_codec,
                    a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
-                   a.colsum && a.wire ? (int)((int64_t)a.M * a.ldc) : 0,
+                   a.colsum && a.wire ? (int)(a.wire_off + (int64_t)a.M * a.ldc) : 0,
                    a.upd_master, a.upd_lp, a.upd_mom, a.upd,
                    sk > 1 && is_wire_epi(EPI) && gemm_fixup_flag().load(std::memory_order_relaxed) != 0
                        ? gemm_fix_counters(s) : nullptr
@@ -1807,6 +1810,8 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
                    , (unsigned long long*)gemm_stamp_buffer()
 #endif
   };
+  wo.off = (uint32_t)a.wire_off;
+
   if (sk > 1) {
     // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + p*N]), then an ordered reduce that
     // applies the epilogue (deterministic: slabs summed in split order)

@@ -268,7 +268,8 @@ bool gemm_bf16_supported(const GemmArgs& a) {
     if (a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire || a.N % 16) return false;
     if (a.wire_shard <= 0 || a.wire_shard % 256 || a.ldc % 16) return false;
     if (a.wire_codec != kBfpTrunc && a.wire_codec != kBfpRne) return false;
-    if ((int64_t)a.M * a.ldc + a.N >= (int64_t(1) << 31)) return false;
+    if (a.wire_off < 0 || a.wire_off % 16 || a.wire_off + (int64_t)a.M * a.ldc + a.N >= (int64_t(1) << 31))
+      return false;
   }
   return true;
 }

@@ -57,9 +57,10 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
     ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only).
     ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N]).
-    ``wire=(buf_u8, shard_elems, own_shard, codec_id[, period])``: BFP-encode the f32 result straight into all-reduce
-    wire shards (flat index m*ldc + n; shard ``own_shard`` — with ``period``, every shard s with s % period ==
-    own_shard — is also written to C) — bf16 bwd-weight only.
+    ``wire=(buf_u8, shard_elems, own_shard, codec_id[, period[, off]])``: BFP-encode the f32 result straight into
+    all-reduce wire shards (flat index off + m*ldc + n: ``off`` places a tensor inside a larger bucket; shard
+    ``own_shard`` — with ``period``, every shard s with s % period == own_shard — is also written to C) — bf16
+    bwd-weight only.
     ``update`` (with ``wire``, single-rank engine): a :class:`LocalUpdate` — the encoded groups are not stored but
     decoded in registers and applied by SGD to the bucket planes in place (the fused local update, see
     csrc/gemm/gemm_bf16_kernel.h WireOut::um)."""
@@ -166,6 +167,7 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
     if wire is not None:
         buf, shard, own, codec = wire[:4]
         period = int(wire[4]) if len(wire) > 4 else 0
+        woff = int(wire[5]) if len(wire) > 5 else 0
 
     def run(plan, waves=0, upd=None):
         bm, bn, sk = plan  # launch exactly this tile (re-planning with an explicit split_k differs)
@@ -173,7 +175,7 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
         ws = _workspace(C.device, need) if need else None
         if wire is not None:
             Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, bm, bn, colsum, waves, buf, int(shard),
-                    int(own), int(codec), period, **(upd.kwargs() if upd is not None else {}))
+                    int(own), int(codec), period, woff, **(upd.kwargs() if upd is not None else {}))
         else:
             Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, bm, bn, colsum, waves)
 

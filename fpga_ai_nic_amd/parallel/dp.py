@@ -54,7 +54,7 @@ class RcclAllReduce(CompressedAllReduce):
 def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str = "rne", algo: str = "mesh",
                 rings: int = 1, max_slice_elems: int = 1 << 22, compat_owner_fp32: bool = False,
                 timeout_s: float = 600.0, force_comm: bool = False, impl: str = "python", comm=None,
-                side_stream: bool = False, ring_sub: int = 0):
+                side_stream: bool = False, ring_sub: int = 0, shard_update: bool | None = None):
     """kind: 'bfp' (compressed engine), 'raw' (engine, uncompressed fp32 wire), 'rccl' (baseline),
     'local' (no communication: world 1). impl: 'python' (request path issued from Python over any
     transport) or 'native' (C++ engine over its own RCCL communicator, or over ``comm``, e.g. the direct P2P
@@ -69,7 +69,7 @@ def make_engine(transport: Transport | None, kind: str = "bfp", *, rounding: str
 
         return NativeAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
                                compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm,
-                               comm=comm, side_stream=side_stream, ring_sub=ring_sub)
+                               comm=comm, side_stream=side_stream, ring_sub=ring_sub, shard_update=shard_update)
     return CompressedAllReduce(transport, codec=codec, algo=algo, rings=rings, max_slice_elems=max_slice_elems,
                                compat_owner_fp32=compat_owner_fp32, timeout_s=timeout_s, force_comm=force_comm)
 
@@ -130,6 +130,11 @@ class DataParallelTrainer:
         self.gemm_inflight = gi if (self.cuda and engine is not None and not getattr(engine, "inline", True)) \
             else "persistent"
         self._persist_saved = None
+        # sharded-update engine (bf16 model): each request writes the layer's NEXT weight buffer (lp_next), which no
+        # GEMM of this step reads, so it needs no ordering after the layer's bwd-data GEMM; the buffers swap once the
+        # step's backward is enqueued (the next forward waits for its layer's request, _wait_layer)
+        self.shard = bool(getattr(engine, "shard_update", False)) and self.cuda and model.dtype == torch.bfloat16
+        self.lp_next = [l.lp.clone() if self.shard else None for l in model.layers]
         self.panel_submit = panel_submit
         self.panel_plans: dict[int, dict] = {}
         # opt-in (FAN_PANELS=4): measured on the one-GPU pool the split costs more than it hides — each panel adds a
@@ -138,7 +143,7 @@ class DataParallelTrainer:
         # GPU: 5.06-5.30 vs 4.61-4.70 ms/step, profiles/r3_panels_ab.txt). It stays off until an 8-GPU run shows
         # the layer-0 exchange it is built to overlap.
         P = int(os.environ.get("FAN_PANELS", "0")) if panels is None else int(panels)
-        if self.prepack and P >= 2 and hasattr(engine, "panel_plan"):
+        if self.prepack and P >= 2 and hasattr(engine, "panel_plan") and not self.shard:
             l0 = model.layers[0]
             pp = engine.panel_plan(l0.cin, l0.cout, P)
             if pp is not None:
@@ -264,7 +269,8 @@ class DataParallelTrainer:
                         h = None
                         if self.engine is not None:
                             kw = {"prepacked": (tgt[0], l.n_pad)} if tgt is not None else {}
-                            h = self.engine.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, lr=self.lr,
+                            lp_out = self.lp_next[i] if self.shard else l.lp
+                            h = self.engine.allreduce_sgd(l.grad, l.master, lp_out, l.mom, n_valid=l.n, lr=self.lr,
                                                           grad_scale=self.grad_scale, weight_decay=self.wd,
                                                           momentum=self.momentum, nesterov=self.nesterov, defer=True,
                                                           name=f"fc{i}", **kw)
@@ -285,6 +291,9 @@ class DataParallelTrainer:
             # the grid GEMM form must not outlive this backward (an exception in between would leave every later
             # GEMM of the process on one workgroup per tile while records report the persistent form)
             self._gemm_grid(False)
+        if self.shard:  # this step's requests write lp_next: it holds the weights the next forward uses
+            for i, l in enumerate(m.layers):
+                l.lp, self.lp_next[i] = self.lp_next[i], l.lp
         if self.commit_at_end:  # issue order L-1..0: the epilogues run in the order their all-reduces finish
             for i in reversed(range(m.L)):
                 h = self.pending[i]
@@ -316,6 +325,17 @@ class DataParallelTrainer:
         """GPU-side: order the current stream after every outstanding update (no host wait; usable while
         capturing a HIP graph)."""
         self._wait_updates()
+
+    def gather_state(self):
+        """Sharded-update engine: collect every layer's owner-sharded master (and momentum) onto every rank, so the
+        planes are whole again (checkpoint, replica check). Collective; a no-op for other engines."""
+        if not self.shard:
+            return
+        self.finish()
+        for l in self.m.layers:
+            self.engine.gather_owned(l.master, l.n)
+            if l.mom is not None:
+                self.engine.gather_owned(l.mom, l.n)
 
     def finish(self, timeout: float | None = None):
         """Wait (host) for every outstanding all-reduce/update."""

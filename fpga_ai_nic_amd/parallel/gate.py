@@ -129,3 +129,58 @@ def allreduce_exactness_layouts(engine, sizes, **kw) -> dict:
         "max_abs_diff": max((r["max_abs_diff"] for r in res), default=0.0),
         "layouts": res,
     }
+
+
+def update_exactness(engine, *, n: int = 1 << 18, seed: int = 20261018, lr: float = 0.05, momentum: float = 0.9,
+                     timeout_s: float = 120.0) -> dict:
+    """The weight-update half of a request, checked bit for bit: every rank starts from the same seeded master /
+    momentum planes, runs ONE all-reduce + SGD request of its seeded gradient through the engine's production
+    ``allreduce_sgd`` (the sharded-update schedule when the engine runs it: owner reduce + SGD, bf16 weight
+    all-gather), then compares its bf16 weights and — gathered from their owners when sharded — its master and
+    momentum with the oracle: the simulator's decoded sum through fp32 SGD (:func:`..ops.bfp_oracle.sgd`, the
+    kernel's operation order). Collective. ``{"exact", "checked", "n", "sharded", "mismatch_ranks"}``."""
+    from ..ops import bfp_oracle as O
+    from ..utils import dist as D
+
+    world = engine.world
+    rank = getattr(engine, "rank", 0)
+    dev = getattr(engine, "device", torch.device("cuda" if torch.cuda.is_available() else "cpu"))
+    grads = seeded_gradients(n, world, seed)
+    rng = np.random.default_rng(seed + 1)
+    w0 = rng.standard_normal(n).astype(np.float32)
+    m0 = (rng.standard_normal(n) * 0.01).astype(np.float32)
+    L = engine.layout(n)
+    g = torch.zeros(L.n_pad, dtype=torch.float32, device=dev)
+    g[:n] = torch.from_numpy(grads[rank]).to(dev)
+    w = torch.zeros(L.n_pad, dtype=torch.float32, device=dev)
+    w[:n] = torch.from_numpy(w0).to(dev)
+    mom = torch.zeros(L.n_pad, dtype=torch.float32, device=dev)
+    mom[:n] = torch.from_numpy(m0).to(dev)
+    lp = torch.zeros(L.n_pad, dtype=torch.bfloat16, device=dev)
+    err = None
+    try:
+        engine.allreduce_sgd(g, w, lp, mom, n_valid=n, lr=lr, grad_scale=1.0 / world, momentum=momentum
+                             ).synchronize(timeout_s)
+        if g.is_cuda:
+            torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {e}"
+    err = next((x for x in D.all_gather_object(err) if x), None)
+    if err:
+        raise RuntimeError(f"update gate request failed: {err}"[:600])
+    sharded = bool(getattr(engine, "shard_update", False))
+    if sharded:
+        engine.gather_owned(w, n)
+        engine.gather_owned(mom, n)
+    ref = reference_sum(engine, grads, n, rank)
+    mine = {"checked": ref is not None, "exact": True}
+    if ref is not None:
+        w_ref, m_ref = O.sgd(w0, ref[:n], lr, grad_scale=1.0 / world, momentum=momentum, mom=m0)
+        lp_ref = O.f32_to_bf16_bits(w_ref)
+        got_lp = lp[:n].view(torch.int16).cpu().numpy().view(np.uint16)
+        mine["exact"] = bool(np.array_equal(w[:n].cpu().numpy().view(np.uint32), w_ref.view(np.uint32))
+                             and np.array_equal(mom[:n].cpu().numpy().view(np.uint32), m_ref.view(np.uint32))
+                             and np.array_equal(got_lp, lp_ref.astype(np.uint16)))
+    every = D.all_gather_object(mine)
+    return {"exact": all(e["exact"] for e in every), "checked": all(e["checked"] for e in every), "n": n,
+            "sharded": sharded, "mismatch_ranks": [r for r, e in enumerate(every) if not e["exact"]]}

@@ -104,7 +104,7 @@ class NativeAllReduce:
                  max_slice_elems: int = 1 << 22, device=None, compat_owner_fp32: bool = False,
                  timeout_s: float = 600.0, stream_priority: int = -1, force_comm: bool = False, comm=None,
                  side_stream: bool = False, verify: bool | None = None, fault: str | None = None,
-                 chunk_elems: int = 0, links="auto", ring_sub: int = 0):
+                 chunk_elems: int = 0, links="auto", ring_sub: int = 0, shard_update: bool | None = None):
         """``comm``: an explicit ``_C.Comm`` (e.g. ``_C.LoopbackFabric(N).comm(r)`` for virtual ranks on one
         GPU); otherwise the engine's own RCCL communicator is created from ``transport``. ``side_stream``
         (world 1): run requests on the engine's comm stream instead of inline (overlap measurements).
@@ -117,7 +117,11 @@ class NativeAllReduce:
         :func:`~fpga_ai_nic_amd.utils.topology.link_matrix`; None: fully connected). ``ring_sub`` (direct-P2P ring):
         each hop's message streams in this many sub-slices with a ready flag each, so the downstream rank starts on
         sub-slice s while this one still encodes the rest (0: env FAN_RING_SUB, default 1 = lock-step hops; capped at
-        the P2P arena depth - 1)."""
+        the P2P arena depth - 1). ``shard_update`` (mesh, multi-rank; default env FAN_SHARD_UPDATE): the owner of each
+        shard fuses its reduce with the SGD of that shard and the ranks all-gather the updated bf16 weights (ZeRO-1
+        style: master / momentum current on the owner only, :meth:`gather_owned` collects them); update requests of
+        bf16 buckets write the ``lp`` they are given (the trainer's next weight buffer) and need no deferred
+        epilogue."""
         if algo not in _ALGOS:
             raise ValueError(f"unknown algo {algo!r}")
         C = _ext.require()
@@ -148,8 +152,9 @@ class NativeAllReduce:
         self.C = C.AllReduceEngine(comm, self.rank, self.world, self.codec_id, _ALGOS[algo], rings, max_slice_elems,
                                    compat_owner_fp32, timeout_s, stream_priority, force_comm or side_stream,
                                    self.device.index, -1 if verify is None else int(bool(verify)), int(chunk_elems),
-                                   links, int(ring_sub))
+                                   links, int(ring_sub), -1 if shard_update is None else int(bool(shard_update)))
         self.ring_sub = int(self.C.ring_sub)
+        self.shard_update = bool(self.C.shard_update)
         if fault is not None:
             self.C.set_fault(fault)
         self.verify = bool(self.C.verify)
@@ -167,6 +172,12 @@ class NativeAllReduce:
         # FAN_EPI=comm runs them on the comm stream, committed per layer. Both train bit-identically to the
         # inline engine since commit() stopped reading torch's default stream (handle 0) as "no producer".
         self.epilogue_on_producer = os.environ.get("FAN_EPI", "producer") != "comm"
+
+    def gather_owned(self, plane: torch.Tensor, n: int):
+        """Sharded-update engines: all-gather an owner-sharded f32 bucket plane (a layer's master or momentum) in
+        place, so every rank holds the whole plane (checkpoints, replica checks). Collective; no-op otherwise."""
+        if self.shard_update:
+            self.C.gather_owned(plane.view(-1), int(n))
 
     @property
     def timing(self):
