@@ -223,7 +223,7 @@ void register_engine(pybind11::module_& m) {
               c10::optional<at::Tensor> mom, int64_t n_valid, double lr, double grad_scale, double wd,
               double momentum, bool nesterov, bool defer, bool update, c10::optional<at::Tensor> out_sum,
               c10::optional<at::Tensor> prepacked, int64_t prepacked_elems, int64_t layout_shard,
-              int64_t layout_chunks) {
+              int64_t layout_chunks, bool on_producer) {
              FAN_T_CUDA_CONTIG(grad);
              TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
                          "gradients must be f32 or bf16");
@@ -268,14 +268,14 @@ void register_engine(pybind11::module_& m) {
              SgdParams p{(float)lr, (float)grad_scale, (float)wd, (float)momentum, nesterov ? 1 : 0};
              return e.submit(grad.data_ptr(), grad.scalar_type() == at::kFloat ? kF32 : kBF16,
                              update ? master.data_ptr<float>() : nullptr, lpp, momp, n_valid, p, fan_stream(), defer,
-                             update, outp, pre, prepacked_elems, layout_shard, layout_chunks);
+                             update, outp, pre, prepacked_elems, layout_shard, layout_chunks, on_producer);
            },
            py::arg("grad"), py::arg("master"), py::arg("lp") = py::none(), py::arg("mom") = py::none(),
            py::arg("n_valid"), py::arg("lr"), py::arg("grad_scale") = 1.0, py::arg("weight_decay") = 0.0,
            py::arg("momentum") = 0.0, py::arg("nesterov") = false, py::arg("defer") = false,
            py::arg("update") = true, py::arg("out_sum") = py::none(), py::arg("prepacked") = py::none(),
            py::arg("prepacked_elems") = 0, py::arg("layout_shard") = 0, py::arg("layout_chunks") = 0,
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("on_producer") = false, py::call_guard<py::gil_scoped_release>())
       .def("prepack_shape", [](AllReduceEngine& e, int64_t n) {
         const auto s = e.prepack_shape(n);
         return py::make_tuple(s[0], s[1], s[2]);

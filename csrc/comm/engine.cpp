@@ -287,8 +287,13 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     P = Pb;
   }
   mark(kTpPacked);
-  uint8_t* R = scratch("mesh_R" + std::to_string(sb * N), sb * N);
-  {
+  // A 1-rank group (world 1 through the multi-rank path) moves nothing: its all-to-all is the identity and the
+  // all-gather of the owner shard is the owner shard, so neither is issued (RCCL's 1-rank collectives are copies with
+  // ~25-30 us of hand-off each around them, profiles/r5_forced_step_timeline.txt) — unless verify mode or a fault rule
+  // wants to see the messages.
+  const bool ident = N == 1 && !verify_ && !fault_.active();
+  uint8_t* R = ident ? const_cast<uint8_t*>(P) : scratch("mesh_R" + std::to_string(sb * N), sb * N);
+  if (!ident) {
     RoctxRange rr("fan/mesh/all_to_all");
     if (verify_) launch_msg_tags(P, sb, sb, N, req_seq_, tag_region(0), st);
     fault_.maybe_corrupt("mesh_pack", const_cast<uint8_t*>(P), sb * N, st);  // in flight: after the tags
@@ -312,7 +317,7 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
                              mom ? mom + (size_t)r * s : nullptr, p, (size_t)nv, out, 1, (size_t)s, false, st);
     }
     mark(kTpReduced);
-    {
+    if (!ident) {
       RoctxRange rr("fan/mesh/all_gather_weights");
       comm_->all_gather(lp + (size_t)r * s, lp, (size_t)s * 2, st);
       count_peers((size_t)s * 2);
@@ -320,13 +325,14 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     counters_.sharded_updates++;
     return {};
   }
-  {
-    RoctxRange rr("fan/mesh/reduce");
-    launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), S, nullptr, (size_t)s, st);
-  }
-  mark(kTpReduced);
   uint8_t* G = epi_scratch("mesh_G" + std::to_string(sb * N), sb * N);
   {
+    RoctxRange rr("fan/mesh/reduce");
+    // (1-rank group: the reduced shard is the gathered bucket, so the reduce writes the epilogue's buffer directly)
+    launch_wire_reduce(c, gdt, R, sb, N, r, g + (size_t)r * s * esize(gdt), ident ? G : S, nullptr, (size_t)s, st);
+  }
+  mark(kTpReduced);
+  if (!ident) {
     RoctxRange rr("fan/mesh/all_gather");
     if (verify_) launch_msg_tags(S, sb, sb, 1, req_seq_, tag_region(3), st);
     fault_.maybe_corrupt("mesh_reduce", S, sb, st);
@@ -984,13 +990,13 @@ void AllReduceEngine::hop_mark(int point) {
 int AllReduceEngine::submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
                             SgdParams sgd, hipStream_t producer, bool defer, bool update, float* out_sum,
                             const uint8_t* prepacked, int64_t prepacked_elems, int64_t layout_shard,
-                            int64_t layout_chunks) {
+                            int64_t layout_chunks, bool on_producer) {
   RoctxRange rr("fan/allreduce/submit");
   FAN_HIP_CHECK(hipSetDevice(device_));
   // slot state machine (slot_table.h): the next slot (a still-deferred occupant is committed first, ordered after
   // the producer: the NIC's 8-deep command queue never drops a request), ordering after anything that may still
   // read the slot's buffers, and the stream this request's communication phase runs on
-  const SlotTable<HipSlotDevice>::Begin b = table_->begin(producer);
+  const SlotTable<HipSlotDevice>::Begin b = table_->begin(producer, on_producer && !inline_);
   const int slot = b.slot;
   req_seq_ = b.seq;  // the sequence number this request will get (its messages' tags carry it)
   submitted_++;

@@ -176,6 +176,7 @@ class AllReduceEngine {
   void gather_owned(float* plane, int64_t n);
 
   // Enqueue the communication phase of a request. grad: padded flat buffer (f32 or bf16) ready on `producer`.
+  // on_producer (multi-rank): the phase runs on the producer stream itself (SlotTable::begin), not the comm stream.
   // If `defer`, the weight update is enqueued later by commit(); otherwise immediately. Returns the slot.
   // prepacked (BFP codecs): the producer already encoded flat elements [0, prepacked_elems) of the bucket into
   // `prepacked` (shard layout of prepack_shape(): mesh shards, or ring slices ring-major); the engine packs the
@@ -185,7 +186,7 @@ class AllReduceEngine {
   int submit(const void* grad, int grad_dtype, float* master, bf16_t* lp, float* mom, int64_t n_valid,
              SgdParams sgd, hipStream_t producer, bool defer, bool update = true, float* out_sum = nullptr,
              const uint8_t* prepacked = nullptr, int64_t prepacked_elems = 0, int64_t layout_shard = 0,
-             int64_t layout_chunks = 0);
+             int64_t layout_chunks = 0, bool on_producer = false);
   // (shard elements, shards, owner shard whose f32 values the reduce needs or -1) for a prepacked bucket,
   // or shard elements 0 when this configuration cannot take prepacked input.
   std::array<int64_t, 3> prepack_shape(int64_t n) const;

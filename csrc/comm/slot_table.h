@@ -93,7 +93,11 @@ class SlotTable {
     Stream run;
     uint32_t seq;  // the sequence number this request will carry
   };
-  Begin begin(Stream producer) {
+  // on_producer (multi-rank): this request's communication phase runs on the producer stream itself instead of the
+  // comm stream — for the last request of a backward, which nothing is left to overlap with: it saves the two
+  // cross-stream hand-offs (producer -> comm, comm -> the next forward; ~25-30 us each on MI355X,
+  // profiles/r5_forced_step_timeline.txt) on the critical path. Ordering then is the producer's own stream order.
+  Begin begin(Stream producer, bool on_producer = false) {
     const int s = next_;
     next_ = (s + 1) % kSlots;
     Slot& sl = slots_[s];
@@ -101,7 +105,7 @@ class SlotTable {
       if (on_forced_commit) on_forced_commit(s);
       commit_slot(s, true, producer);
     }
-    const Stream run = cfg_.inline_mode ? producer : cfg_.comm;
+    const Stream run = (cfg_.inline_mode || on_producer) ? producer : cfg_.comm;
     // I2: the slot's previous epilogue may run on another stream than this request and read this slot's
     // buffers (a side epilogue, or one committed on another producer stream). A multi-rank request waits for
     // `ready` on the producer below, which covers an epilogue enqueued there.
@@ -111,7 +115,7 @@ class SlotTable {
     }
     sl.stream = run;
     sl.keep_done = false;
-    if (!cfg_.inline_mode) {
+    if (!cfg_.inline_mode && !(run == producer)) {
       dev_.record(sl.ready, producer);
       dev_.wait(run, sl.ready);
     }

@@ -135,6 +135,10 @@ class DataParallelTrainer:
         # step's backward is enqueued (the next forward waits for its layer's request, _wait_layer)
         self.shard = bool(getattr(engine, "shard_update", False)) and self.cuda and model.dtype == torch.bfloat16
         self.lp_next = [l.lp.clone() if self.shard else None for l in model.layers]
+        # multi-rank native engine: layer 0's request (the backward's last) on the compute stream itself
+        # (FAN_LAST_ON_PRODUCER=0: on the comm stream like the others)
+        self.last_on_producer = (self.cuda and engine is not None and not getattr(engine, "inline", True)
+                                 and hasattr(engine, "C") and os.environ.get("FAN_LAST_ON_PRODUCER", "1") != "0")
         self.panel_submit = panel_submit
         self.panel_plans: dict[int, dict] = {}
         # opt-in (FAN_PANELS=4): measured on the one-GPU pool the split costs more than it hides — each panel adds a
@@ -270,6 +274,10 @@ class DataParallelTrainer:
                         if self.engine is not None:
                             kw = {"prepacked": (tgt[0], l.n_pad)} if tgt is not None else {}
                             lp_out = self.lp_next[i] if self.shard else l.lp
+                            if i == 0 and self.last_on_producer:
+                                # the backward's last request: nothing left to overlap it with, so it runs on this
+                                # stream (no hand-off to the comm stream and back before the next forward)
+                                kw["on_producer"] = True
                             h = self.engine.allreduce_sgd(l.grad, l.master, lp_out, l.mom, n_valid=l.n, lr=self.lr,
                                                           grad_scale=self.grad_scale, weight_decay=self.wd,
                                                           momentum=self.momentum, nesterov=self.nesterov, defer=True,

@@ -269,10 +269,12 @@ class NativeAllReduce:
                       mom: torch.Tensor | None = None, *, n_valid: int | None = None, lr: float,
                       grad_scale: float = 1.0, weight_decay: float = 0.0, momentum: float = 0.0,
                       nesterov: bool = False, update_after=None, defer: bool = False,
-                      name: str = "bucket", prepacked=None, layout=None) -> NativeHandle:
+                      name: str = "bucket", prepacked=None, layout=None, on_producer: bool = False) -> NativeHandle:
         """``prepacked=(wire_u8, elems)``: flat elements [0, elems) were already encoded into ``wire_u8``
         (from :meth:`prepack_target`); the engine encodes the rest and skips its pack pass. ``layout=(shard,
-        chunks)``: an explicit chunked mesh layout (see :meth:`panel_plan`)."""
+        chunks)``: an explicit chunked mesh layout (see :meth:`panel_plan`). ``on_producer``: run the request on the
+        current (producer) stream instead of the engine's comm stream — the last request of a backward, which has
+        nothing left to overlap with (saves two cross-stream hand-offs on the critical path)."""
         n_valid = int(n_valid if n_valid is not None else master.numel())
         pre, pre_n = (None, 0) if prepacked is None else prepacked
         ls, lc = (0, 0) if layout is None else (int(layout[0]), int(layout[1]))
@@ -281,7 +283,7 @@ class NativeAllReduce:
         eng_defer = defer or update_after is not None
         slot = self.C.submit(grad.view(-1), master.view(-1), None if lp is None else lp.view(-1),
                              None if mom is None else mom.view(-1), n_valid, lr, grad_scale, weight_decay, momentum,
-                             nesterov, eng_defer, True, None, pre, int(pre_n), ls, lc)
+                             nesterov, eng_defer, True, None, pre, int(pre_n), ls, lc, bool(on_producer))
         h = NativeHandle(self, slot, self.C.slot_seq(slot), name, pending=eng_defer)
         self._account(n_valid)
         return h if defer else h.commit(update_after)

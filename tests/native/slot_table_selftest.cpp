@@ -160,7 +160,10 @@ static void run_case(int mode, unsigned seed, bool wrap) {
     if (kind <= 3) {  // submit a request from a producer
       const int P = producer();
       dev.work(P, next_work++);  // the producer's GEMM that wrote the gradient
-      const auto b = t.begin(P);
+      // (multi-rank: sometimes the request runs on the producer stream itself, SlotTable::begin on_producer)
+      const bool onp = !cfg.inline_mode && rng() % 5 == 0;
+      const auto b = t.begin(P, onp);
+      EXPECT(!onp || b.run == P, "an on-producer request must run on its producer stream");
       Req r;
       r.slot = b.slot;
       r.seq = b.seq;
