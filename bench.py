@@ -758,7 +758,8 @@ def main(argv=None):
             tp = info.get("transport") if multi else "auto"
             tp = tp if tp in ("p2p", "native", "torch") else ("auto" if not multi else "torch")
             s = build("ref_workload", a.compress, algo=info.get("algo", "mesh"), rings=max(1, info.get("rings") or 1),
-                      transport=tp, sizes=[2048] * 11, mdtype=torch.float32, bias=False, relu="none")
+                      transport=tp, sizes=[2048] * 11, mdtype=torch.float32, bias=False, relu="none",
+                      engine="python" if tp == "torch" else None)
             try:
                 iters = 10
                 e, _, loss_r, _, _ = run(s, REF_MB_PER_RANK, 777, 3, iters, "ref_workload")
@@ -844,7 +845,9 @@ def _config5(a, world, device, info, ctx, native_transport, p2p_comm, make_engin
         comm = p2p_comm()
         comm.sdma = info.get("copy") == "sdma"
     else:
-        t = native_transport() or ctrl
+        t = native_transport()
+        if t is None:  # the headline ran on the control plane's collectives (the last-resort arm): no native engine
+            return {"skipped": f"no native transport: {ctx['native_err']}"}
     eng = make_engine(t, "bfp", rounding=a.rounding, algo=info.get("algo", "mesh"), rings=max(1, info.get("rings", 1)),
                       impl="native", comm=comm, timeout_s=timeout_s, force_comm=forced is not None)
     r = bert_overlap.measure(eng, device, world, tokens=4096, layers=12, rounds=3)

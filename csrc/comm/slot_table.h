@@ -60,6 +60,7 @@ class SlotTable {
     Stream epi_stream{};         // stream the epilogue was enqueued on
     bool done_lazy = false;      // inline request whose done event is not recorded yet
     bool keep_done = false;      // the engine times / traces this request: record its done event at commit
+    bool on_producer = false;    // multi-rank request that ran on its producer stream (begin(.., true))
     std::vector<Thunk> thunks;
   };
 
@@ -115,9 +116,17 @@ class SlotTable {
     }
     sl.stream = run;
     sl.keep_done = false;
+    sl.on_producer = !cfg_.inline_mode && on_producer;
     if (!cfg_.inline_mode && !(run == producer)) {
       dev_.record(sl.ready, producer);
       dev_.wait(run, sl.ready);
+    } else if (!cfg_.inline_mode) {
+      // on-producer request: the communicator's earlier requests (on the comm stream) finish first, so its
+      // collectives / P2P rounds never run beside theirs (RCCL serialises a communicator's operations by issue order;
+      // a P2P flag wait parked on this stream would otherwise block a comm-stream round a peer needs, when the two
+      // streams share a hardware queue). Usually already complete when the backward's last GEMM ends.
+      dev_.record(sl.ready, cfg_.comm);
+      dev_.wait(producer, sl.ready);
     }
     return Begin{s, run, following(seq_)};
   }
@@ -167,7 +176,7 @@ class SlotTable {
       return dev_.query(sl.done);
     }
     if (sl.pending) return false;
-    if (cfg_.inline_mode || !(sl.epi_stream == sl.stream)) return dev_.query(sl.done);
+    if (cfg_.inline_mode || sl.on_producer || !(sl.epi_stream == sl.stream)) return dev_.query(sl.done);
     return dev_.read_done(s) == sl.seq;
   }
 
@@ -231,12 +240,14 @@ class SlotTable {
     if (on_epilogue) on_epilogue(s, sl.epi_stream);
     // multi-rank requests finishing on the comm stream: the GPU writes the done word ("write 1 to done_addr +
     // done_id"); requests finishing on the critical compute stream skip that packet: their completion is the event
-    if (sl.epi_stream == sl.stream && !cfg_.inline_mode) dev_.write_done(sl.stream, s, sl.seq);
+    // (on-producer requests too: the host-memory write cost ~50 us before the next forward's first kernel,
+    // profiles/r5_forced_step_timeline.txt)
+    if (sl.epi_stream == sl.stream && !cfg_.inline_mode && !sl.on_producer) dev_.write_done(sl.stream, s, sl.seq);
     // Lazy done event: the epilogue ran in its own stream's order (inline requests; multi-rank epilogues on the
     // producer stream), so nothing needs the event unless the host polls the request or another stream waits on
     // it; ensure_done() records it then. Each eager record is a marker packet on the critical compute stream.
     sl.done_lazy = cfg_.lazy_done && !sl.keep_done &&
-                   ((cfg_.inline_mode && sl.epi_stream == sl.stream) || on_producer);
+                   ((cfg_.inline_mode && sl.epi_stream == sl.stream) || on_producer || sl.on_producer);
     if (!sl.done_lazy) dev_.record(sl.done, sl.epi_stream);
     sl.pending = false;
   }
