@@ -80,6 +80,10 @@ def parse_args(argv=None):
     ap.add_argument("--transport", default="native", choices=["torch", "native", "p2p"],
                     help="torch/native: RCCL collectives; p2p: direct HIP-IPC peer writes + stream flags "
                          "(C++ engine only)")
+    ap.add_argument("--p2p-copy", default="kernel", choices=["kernel", "sdma"],
+                    help="--schedule fixed over --transport p2p: pure copies on CUs (kernel) or the copy engines")
+    ap.add_argument("--shard-update", type=int, default=-1, choices=[-1, 0, 1],
+                    help="--schedule fixed: sharded weight update (1), the gathered-gradient update (0), env default (-1)")
     ap.add_argument("--engine", default="native", choices=["python", "native"],
                     help="request path: Python-issued engine or the C++ engine (csrc/comm/engine.cpp)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
@@ -404,11 +408,28 @@ def main(argv=None):
             step()
         loss_rows = model.loss_rows
         t_enqueue = time.perf_counter() - t0  # host time to issue K steps (GPU may still be running)
-        _finish(trainer, wait_s)
-        if cuda:
-            torch.cuda.synchronize()
-        D.barrier()
-        elapsed = D.max_over_ranks(time.perf_counter() - t0)
+        if wait_s is None:
+            _finish(trainer, wait_s)
+            if cuda:
+                torch.cuda.synchronize()
+            D.barrier()
+            elapsed = D.max_over_ranks(time.perf_counter() - t0)
+        else:
+            # an A/B arm: each rank's clock stops when its own work has drained; the ranks agree on the outcome
+            # after that (the agreement is a control-plane all_gather_object, ~1 ms: inside the window it read
+            # stage 2's 10-step rounds 10-13 % above the headline, profiles/r5_ab_stability.jsonl)
+            err = None
+            try:
+                trainer.finish(wait_s)
+            except Exception as ex:  # noqa: BLE001
+                err = f"rank {rank}: {ex}"
+            if cuda and err is None:
+                torch.cuda.synchronize()
+            t_local = time.perf_counter() - t0
+            err = next((x for x in D.all_gather_object(err) if x), None)
+            if err:
+                raise RuntimeError(err[:600])
+            elapsed = D.max_over_ranks(t_local)
         tr = None
         if trace:
             tr = engine.trace_summary()
@@ -542,7 +563,7 @@ def main(argv=None):
             for rnd in range(4):  # round 0: warmup (untimed in the decision)
                 for kr, ks in list(kept):
                     try:
-                        e, _, _, _, _ = run(ks, mb, 99, 2 if rnd == 0 else 0, a.ab2_steps, f"ab2 {kr['arm']}",
+                        e, _, _, _, _ = run(ks, mb, 99, 2 if rnd == 0 else 1, a.ab2_steps, f"ab2 {kr['arm']}",
                                             wait_s=arm_wait)
                         if rnd > 0:
                             st2[kr["arm"]].append(round(e / a.ab2_steps * 1e3, 4))
@@ -577,7 +598,9 @@ def main(argv=None):
                 log(f"native communicator unavailable ({ctx['native_err']}); using torch.distributed")
                 transport = "torch"
         main_setup = build("main", a.compress, algo=a.algo, rings=a.rings, transport=transport,
-                           gemm=a.gemm_inflight, force=a.force_dist and impl == "native" and transport == "auto")
+                           gemm=a.gemm_inflight, force=a.force_dist and impl == "native" and transport == "auto",
+                           sdma=a.p2p_copy == "sdma" and transport == "p2p",
+                           shard=None if a.shard_update < 0 else bool(a.shard_update))
         if multi and main_setup.engine is not None:
             gate_rec = gate.allreduce_exactness(main_setup.engine)
             if not gate_rec["exact"]:

@@ -355,6 +355,7 @@ void register_engine(pybind11::module_& m) {
              d["direct_rounds"] = c.direct_rounds;
              d["sharded_updates"] = c.sharded_updates;
              d["peer_bytes"] = c.peer_bytes;
+             d["skipped_waits"] = e.skipped_waits();
              return d;
            },
            "perf counters (the NIC's latency / host-stall registers): requests, bytes, host wait, device time")

@@ -226,6 +226,7 @@ class AllReduceEngine {
   void set_fault(const std::string& spec) { fault_ = FaultInjector(spec); }
   uint64_t requests() const { return submitted_; }
   const EngineCounters& counters() const { return counters_; }
+  uint64_t skipped_waits() const { return table_->skipped_waits(); }  // redundant cross-stream waits elided
   void reset_counters() { counters_ = EngineCounters{}; }
   int64_t wire_bytes(const EngineLayout& L) const;
   // device scratch the engine holds (wire staging buffers; per-slot gathered wire of deferred requests)

@@ -47,6 +47,7 @@ class SlotTable {
     bool epi_on_producer = false; // multi-rank: epilogue on the committing (compute) stream after comm_done
     bool side_epi = false;        // world 1: epilogue on the side stream after the producer's enqueued work
     bool lazy_done = true;        // inline: record the done event only when something needs it
+    bool elide_waits = true;      // skip cross-stream waits implied by an earlier wait on the comm stream
     Stream comm{};                // the engine's communication stream (multi-rank)
     Stream side{};                // the world-1 side-epilogue stream (side_epi)
   };
@@ -61,6 +62,8 @@ class SlotTable {
     bool done_lazy = false;      // inline request whose done event is not recorded yet
     bool keep_done = false;      // the engine times / traces this request: record its done event at commit
     bool on_producer = false;    // multi-rank request that ran on its producer stream (begin(.., true))
+    uint64_t comm_done_mark = 0; // comm-stream order of the last comm_done / done record (0: not on the comm stream)
+    uint64_t done_mark = 0;
     std::vector<Thunk> thunks;
   };
 
@@ -85,6 +88,7 @@ class SlotTable {
   uint32_t last_seq() const { return seq_; }
   int next_slot() const { return next_; }
   const Slot& slot(int i) const { return slots_.at(i); }
+  uint64_t skipped_waits() const { return skipped_waits_; }
 
   // A new request from `producer`: takes the next slot (force-committing a still-deferred occupant), orders the
   // request after anything that may still read that slot's buffers, and returns (slot, stream its communication
@@ -112,7 +116,7 @@ class SlotTable {
     // `ready` on the producer below, which covers an epilogue enqueued there.
     if (sl.used && !(sl.epi_stream == run) && !(!cfg_.inline_mode && sl.epi_stream == producer)) {
       ensure_done(sl);
-      dev_.wait(run, sl.done);
+      wait_m(run, sl.done, sl.done_mark);
     }
     sl.stream = run;
     sl.keep_done = false;
@@ -125,8 +129,9 @@ class SlotTable {
       // collectives / P2P rounds never run beside theirs (RCCL serialises a communicator's operations by issue order;
       // a P2P flag wait parked on this stream would otherwise block a comm-stream round a peer needs, when the two
       // streams share a hardware queue). Usually already complete when the backward's last GEMM ends.
-      dev_.record(sl.ready, cfg_.comm);
+      const uint64_t m = record_m(sl.ready, cfg_.comm);
       dev_.wait(producer, sl.ready);
+      cover(producer, m, true);
     }
     return Begin{s, run, following(seq_)};
   }
@@ -135,7 +140,7 @@ class SlotTable {
   // stream. Immediate requests commit now (in the comm stream's order).
   uint32_t end(int s, std::vector<Thunk> thunks, bool defer) {
     Slot& sl = slots_.at(s);
-    if (!cfg_.inline_mode) dev_.record(sl.comm_done, sl.stream);
+    if (!cfg_.inline_mode) sl.comm_done_mark = record_m(sl.comm_done, sl.stream);
     sl.thunks = std::move(thunks);
     sl.pending = true;
     sl.used = true;
@@ -162,7 +167,7 @@ class SlotTable {
     if (own && sl.pending) commit_slot(s, true, st);
     if (!(st == sl.epi_stream) || !own) {
       ensure_done(sl);
-      dev_.wait(st, sl.done);
+      wait_m(st, sl.done, sl.done_mark);
     }
   }
 
@@ -190,7 +195,7 @@ class SlotTable {
   // polls it or another stream waits on it: record it then (later in that stream = a conservative completion point).
   void ensure_done(Slot& sl) {
     if (!sl.done_lazy) return;
-    dev_.record(sl.done, sl.epi_stream);
+    sl.done_mark = record_m(sl.done, sl.epi_stream);
     sl.done_lazy = false;
   }
   void ensure_done(int s) { ensure_done(slots_.at(s)); }
@@ -218,7 +223,7 @@ class SlotTable {
     if (cfg_.epi_on_producer && !cfg_.inline_mode && after_producer && !(producer == sl.stream)) {
       // epilogue on the producer (compute) stream, after the request's communication phase: it runs after
       // everything already enqueued there and never concurrently with the producer's GEMMs
-      dev_.wait(producer, sl.comm_done);
+      wait_m(producer, sl.comm_done, sl.comm_done_mark);
       sl.epi_stream = producer;
       on_producer = true;
     } else if (cfg_.side_epi && after_producer) {
@@ -227,7 +232,7 @@ class SlotTable {
       dev_.record(sl.update, producer);
       dev_.wait(cfg_.side, sl.update);
       if (!(producer == sl.stream)) {
-        dev_.record(sl.comm_done, sl.stream);
+        sl.comm_done_mark = record_m(sl.comm_done, sl.stream);
         dev_.wait(cfg_.side, sl.comm_done);
       }
       sl.epi_stream = cfg_.side;
@@ -248,8 +253,39 @@ class SlotTable {
     // it; ensure_done() records it then. Each eager record is a marker packet on the critical compute stream.
     sl.done_lazy = cfg_.lazy_done && !sl.keep_done &&
                    ((cfg_.inline_mode && sl.epi_stream == sl.stream) || on_producer || sl.on_producer);
-    if (!sl.done_lazy) dev_.record(sl.done, sl.epi_stream);
+    if (!sl.done_lazy) sl.done_mark = record_m(sl.done, sl.epi_stream);
     sl.pending = false;
+  }
+
+  // Redundant cross-stream waits. Each event record on the comm stream gets the next comm-stream mark; a wait of
+  // stream st on such a record orders st after everything enqueued on the comm stream up to that mark. A later wait
+  // of st on a comm-stream record with a mark at or below it is then implied (in-order streams) and skipped: each
+  // such wait is a barrier packet costing ~25-30 us on the critical compute stream even when its event is long
+  // complete (profiles/r5_forced_step_timeline.txt). The case it is for: the backward's last request runs on the
+  // producer after a wait on the comm stream (begin on_producer), so the next forward's waits on the step's earlier
+  // requests, and their epilogues committed on the producer after it, need no packets of their own. One stream is
+  // tracked (the producer of the latest on-producer request).
+  uint64_t record_m(Event e, Stream s) {
+    dev_.record(e, s);
+    return (!cfg_.inline_mode && s == cfg_.comm) ? ++comm_mark_ : 0;
+  }
+  void cover(Stream st, uint64_t m, bool take) {
+    if (m == 0) return;
+    if (cover_valid_ && st == cover_stream_) {
+      if (m > cover_mark_) cover_mark_ = m;
+    } else if (take || !cover_valid_) {
+      cover_valid_ = true;
+      cover_stream_ = st;
+      cover_mark_ = m;
+    }
+  }
+  void wait_m(Stream st, Event e, uint64_t m) {
+    if (cfg_.elide_waits && m != 0 && cover_valid_ && st == cover_stream_ && m <= cover_mark_) {
+      ++skipped_waits_;
+      return;
+    }
+    dev_.wait(st, e);
+    cover(st, m, false);
   }
 
   D& dev_;
@@ -257,6 +293,11 @@ class SlotTable {
   std::array<Slot, kSlots> slots_;
   uint32_t seq_ = 0;
   int next_ = 0;
+  uint64_t comm_mark_ = 0;
+  bool cover_valid_ = false;
+  Stream cover_stream_{};
+  uint64_t cover_mark_ = 0;
+  uint64_t skipped_waits_ = 0;
 };
 
 }  // namespace fan
