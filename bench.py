@@ -871,11 +871,14 @@ def _config5(a, world, device, info, ctx, native_transport, p2p_comm, make_engin
         t = native_transport()
         if t is None:  # the headline ran on the control plane's collectives (the last-resort arm): no native engine
             return {"skipped": f"no native transport: {ctx['native_err']}"}
+    # the headline's update form (the sharded update at world 1: the owner reduce + SGD is the whole exchange)
+    shard = True if forced is not None else bool(info.get("shard_update"))
     eng = make_engine(t, "bfp", rounding=a.rounding, algo=info.get("algo", "mesh"), rings=max(1, info.get("rings", 1)),
-                      impl="native", comm=comm, timeout_s=timeout_s, force_comm=forced is not None)
+                      impl="native", comm=comm, timeout_s=timeout_s, force_comm=forced is not None,
+                      shard_update=shard if info.get("algo", "mesh") == "mesh" else None)
     r = bert_overlap.measure(eng, device, world, tokens=4096, layers=12, rounds=3)
     r.update(transport="p2p" if comm is not None else getattr(t, "name", "torch"), algo=info.get("algo", "mesh"),
-             forced_1rank=forced is not None)
+             forced_1rank=forced is not None, shard_update=bool(getattr(eng, "shard_update", False)))
     return r
 
 

@@ -46,7 +46,7 @@ _LINEARS = (("ffn_out", "output.dense", bert.FFN, bert.HIDDEN), ("ffn_in", "inte
             ("qkv", "attention.self.qkv", bert.HIDDEN, 3 * bert.HIDDEN))
 
 
-def measure(eng, dev, world, tokens=4096, layers=12, rounds=5, only=""):
+def measure(eng, dev, world, tokens=4096, layers=12, rounds=5, only="", last_on_producer=True, group_wgrad=None):
     """Config 5 on an engine: a BERT-base backward whose gradients ARE the all-reduce's input. Per encoder layer (last
     first) the four projections' bwd-data GEMM (bf16 dX) and bwd-weight GEMM run on the compute stream; each
     bwd-weight GEMM writes its dW — and, fused, its bias gradient — straight into the layer's gradient bucket, BFP-
@@ -91,26 +91,43 @@ def measure(eng, dev, world, tokens=4096, layers=12, rounds=5, only=""):
             encode_range(g, tgt, 0, b.numel)
             return
         pre = f"encoder.layer.{b.name[5:]}."
+        probs = []
         for name, tn, fin, fout in _LINEARS:
             X, dY, W, dX = acts[name]
             G.gemm(dY, False, W, True, dX)  # bwd-data dX = dY . W^T
             woff, _ = offs[pre + tn + ".weight"]
             boff, _ = offs[pre + tn + ".bias"]
-            dW = g[woff: woff + fin * fout].view(fin, fout)
-            db = g[boff: boff + fout]
-            if tgt is not None:
-                G.gemm(X, True, dY, False, dW, G.EPI_WIRE, colsum=db,
-                       wire=(tgt[0], tgt[1], tgt[2], tgt[3], tgt[4], woff))
-            else:
-                G.gemm(X, True, dY, False, dW, G.EPI_NONE, colsum=db)
+            probs.append((X, dY, g[woff: woff + fin * fout].view(fin, fout), g[boff: boff + fout], woff))
+        wire = (tgt[0], tgt[1], tgt[2], tgt[3], tgt[4]) if tgt is not None else None
+        if group_wgrad:
+            # the layer's four bwd-weight GEMMs in one dispatch, after its bwd-data chain (each projection's dW
+            # needs only its own X and dY)
+            G.gemm_wgrad_group(probs, wire=wire)
+        else:
+            for X, dY, dW, db, woff in probs:
+                if wire is not None:
+                    G.gemm(X, True, dY, False, dW, G.EPI_WIRE, colsum=db, wire=wire + (woff,))
+                else:
+                    G.gemm(X, True, dY, False, dW, G.EPI_NONE, colsum=db)
         for ln in ("attention.output.LayerNorm", "output.LayerNorm"):  # [weight | bias], no GEMM
             lo, _ = offs[pre + ln + ".weight"]
             encode_range(g, tgt, lo, lo + 2 * bert.HIDDEN)
 
+    on_producer_ok = last_on_producer and hasattr(eng, "C") and not getattr(eng, "inline", True)
+    if group_wgrad is None:
+        group_wgrad = os.environ.get("FAN_GROUP_WGRAD", "1") != "0" and G.wgrad_group_supported(
+            [(acts[nm][0], acts[nm][1]) for nm, _, _, _ in _LINEARS])
+
     def comm(bi):
         b, g, w, lp, L, tgt, _ = bufs[bi]
         kw = {"prepacked": (tgt[0], L.n_pad)} if tgt is not None else {}
+        if on_producer_ok and bi == len(bufs) - 1:
+            # the backward's last bucket (embeddings): nothing left to overlap it with, so on the compute stream (the
+            # trainer's schedule, dp.py last_on_producer)
+            kw["on_producer"] = True
         return eng.allreduce_sgd(g, w, lp, n_valid=b.numel, lr=1e-4, grad_scale=1.0 / world, name=b.name, **kw)
+
+    enq = {}
 
     def run(do_compute, do_comm):
         D.barrier()
@@ -124,6 +141,8 @@ def measure(eng, dev, world, tokens=4096, layers=12, rounds=5, only=""):
                 hs.append(comm(bi))
         for h in hs:
             h.wait()
+        # host time to issue the round (close to the total: the round is launch-bound, not GPU-bound)
+        enq.setdefault((do_compute, do_comm), []).append(time.perf_counter() - t0)
         torch.cuda.synchronize()
         return D.max_over_ranks(time.perf_counter() - t0)
 
@@ -146,9 +165,10 @@ def measure(eng, dev, world, tokens=4096, layers=12, rounds=5, only=""):
     return {"tokens_per_gpu": T, "params": bert.num_params(layers), "t_compute_ms": round(tc, 3),
             "t_comm_ms": round(tm, 3), "t_overlap_ms": round(to, 3), "overlap_efficiency": round(eff, 3),
             "overlap_vs_compute": round(to / tc, 3) if tc > 0 else None,
-            "producer_encoded_buckets": prepacked_buckets, "buckets": len(bufs),
+            "producer_encoded_buckets": prepacked_buckets, "buckets": len(bufs), "grouped_wgrad": bool(group_wgrad),
             "bwd_gemm_tflops": round(flops / (tc / 1e3) / 1e12, 1) if tc > 0 else None,
-            "comm_algo_bw_GBps": round(bert.num_params(layers) * 4 / (tm / 1e3) / 1e9, 1) if tm > 0 else None}
+            "comm_algo_bw_GBps": round(bert.num_params(layers) * 4 / (tm / 1e3) / 1e9, 1) if tm > 0 else None,
+            "enqueue_ms": {k: round(statistics.median(enq.get(v, [0.0])) * 1e3, 3) for k, v in kinds.items()}}
 
 
 def main():
@@ -160,12 +180,20 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--engine", default="native", choices=["python", "native"])
+    ap.add_argument("--forced", action="store_true",
+                    help="world 1 through the multi-rank path (1-rank RCCL group, sharded update: bench.py extra.config5)")
     ap.add_argument("--only", default="", choices=["", "compute", "comm", "overlap"],
                     help="profiling: run only rounds of this kind (one kernel trace per kind, for tools/overlap_report.py)")
     a = ap.parse_args()
-    rank, world, _, dev = D.init_distributed()
+    rank, world, _, dev = D.init_distributed(force=a.forced)
     transport = TorchDistTransport() if world > 1 else ThreadFabric(1).transport(0)
-    if a.engine == "native" and a.compress != "rccl":
+    if a.forced:
+        from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce
+        from fpga_ai_nic_amd.parallel.transport import NativeTransport
+
+        eng = NativeAllReduce(NativeTransport(force_collectives=True), codec="bfp_rne", algo="mesh", force_comm=True,
+                              shard_update=True)
+    elif a.engine == "native" and a.compress != "rccl":
         from fpga_ai_nic_amd.parallel.native_engine import NativeAllReduce
 
         codec = {"bfp": "bfp_rne", "raw": "raw_f32"}[a.compress]

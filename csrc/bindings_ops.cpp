@@ -170,6 +170,69 @@ void gemm_bwd_pair(const at::Tensor& dZ, const at::Tensor& W, const at::Tensor& 
   launch_gemm_bwd_pair(bd, bw, (int)grid0, (int)grid1, fan_stream());
 }
 
+// Up to kGroupMax bwd-weight GEMMs C_i = X_i^T . dY_i (+ colsum_i = sum of dY_i's rows) in one dispatch, f32 out or
+// BFP-encoded into one wire buffer at flat offsets offs[i] (the bias segment right after each C_i).
+void gemm_wgrad_group(const std::vector<at::Tensor>& Xs, const std::vector<at::Tensor>& dYs,
+                      const std::vector<at::Tensor>& Cs, const std::vector<at::Tensor>& colsums,
+                      const std::vector<int64_t>& offs, at::Tensor& workspace, const c10::optional<at::Tensor>& wire,
+                      int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period) {
+  const size_t n = Xs.size();
+  TORCH_CHECK(n >= 1 && n <= (size_t)kGroupMax && dYs.size() == n && Cs.size() == n && colsums.size() == n &&
+                  (offs.empty() || offs.size() == n),
+              "gemm_wgrad_group: 1..", kGroupMax, " problems, one X, dY, C, colsum (and wire offset) each");
+  TORCH_CHECK(workspace.is_cuda() && workspace.scalar_type() == at::kFloat && workspace.is_contiguous(),
+              "gemm_wgrad_group: f32 GPU workspace");
+  std::vector<GemmArgs> g(n);
+  int64_t ws_off = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const at::Tensor &X = Xs[i], &dY = dYs[i], &C = Cs[i], &cs = colsums[i];
+    TORCH_CHECK(X.is_cuda() && dY.is_cuda() && C.is_cuda() && cs.is_cuda(), "gemm_wgrad_group: GPU tensors");
+    TORCH_CHECK(X.scalar_type() == at::kBFloat16 && dY.scalar_type() == at::kBFloat16 &&
+                    C.scalar_type() == at::kFloat && cs.scalar_type() == at::kFloat && cs.is_contiguous(),
+                "gemm_wgrad_group: bf16 X / dY, f32 C / colsum");
+    TORCH_CHECK(X.dim() == 2 && dY.dim() == 2 && X.size(0) == dY.size(0) && C.dim() == 2 && C.size(0) == X.size(1) &&
+                    C.size(1) == dY.size(1) && cs.numel() >= dY.size(1),
+                "gemm_wgrad_group: shapes (X [K][M], dY [K][N], C [M][N], colsum [N])");
+    GemmArgs& a = g[i];
+    a.A = X.data_ptr(); a.lda = ld_of(X);
+    a.B = dY.data_ptr(); a.ldb = ld_of(dY);
+    a.C = C.data_ptr(); a.ldc = ld_of(C);
+    a.M = (int)X.size(1); a.N = (int)dY.size(1); a.K = (int)X.size(0);
+    a.a_kcontig = false; a.b_kcontig = false; a.c_bf16 = false;
+    a.colsum = cs.data_ptr<float>();
+    a.epilogue = wire ? kEpiWire : kEpiNone;
+    a.workspace = workspace.data_ptr<float>() + ws_off;
+    ws_off += (gemm_wgrad_group_ws(a) + 3) / 4 * 4;
+    if (wire) {
+      TORCH_CHECK(wire->is_cuda() && wire->is_contiguous() && wire->scalar_type() == at::kByte,
+                  "wire epilogue needs a contiguous uint8 GPU wire buffer");
+      TORCH_CHECK(wire_shard > 0 && wire_shard % 256 == 0, "wire_shard must be a positive multiple of 256");
+      const int64_t off = offs.empty() ? 0 : offs[i];
+      TORCH_CHECK(off >= 0 && off % 16 == 0, "wire offsets must be non-negative multiples of 16");
+      const int64_t last = off + (int64_t)a.M * a.ldc + a.N - 1;
+      const int64_t need = (last / wire_shard + 1) * (int64_t)wire_shard_bytes((int)wire_codec, (size_t)wire_shard);
+      TORCH_CHECK(wire->numel() >= need, "wire buffer too small: ", wire->numel(), " < ", need);
+      a.wire = wire->data_ptr<uint8_t>();
+      a.wire_shard = wire_shard;
+      a.wire_own = (int)wire_own;
+      a.wire_period = (int)wire_period;
+      a.wire_codec = (int)wire_codec;
+      a.wire_off = off;
+    }
+  }
+  TORCH_CHECK(workspace.numel() >= ws_off, "gemm_wgrad_group: workspace of ", ws_off, " floats needed");
+  TORCH_CHECK(gemm_wgrad_group_supported(g.data(), (int)n),
+              "gemm_wgrad_group: unsupported (M % 256, N % 128, K % 64, aligned operands, at most ", 64 * kNumCU,
+              " workgroups)");
+  launch_gemm_wgrad_group(g.data(), (int)n, fan_stream());
+}
+
+int64_t gemm_wgrad_group_ws_floats(const std::vector<std::pair<int64_t, int64_t>>& mn) {
+  int64_t w = 0;
+  for (const auto& p : mn) w += ((p.first / 256) * p.second + 3) / 4 * 4;
+  return w;
+}
+
 pybind11::tuple gemm_plan(int64_t M, int64_t N, int64_t K, int64_t split_k, int64_t tile_bm, int64_t tile_bn,
                           int64_t tile_waves) {
   GemmPlan p = gemm_bf16_plan((int)M, (int)N, (int)K, (int)split_k, (int)tile_bm, (int)tile_bn, (int)tile_waves);
@@ -228,6 +291,13 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_bwd_pair", &gemm_bwd_pair, "one layer's bwd-data (ReLU mask, bf16) + bwd-weight (f32) in one dispatch",
         pybind11::arg("dZ"), pybind11::arg("W"), pybind11::arg("X"), pybind11::arg("dX"), pybind11::arg("dW"),
         pybind11::arg("bw_bn") = 256, pybind11::arg("grid0") = 128, pybind11::arg("grid1") = 128);
+  m.def("gemm_wgrad_group", &gemm_wgrad_group,
+        "up to 8 bwd-weight GEMMs (+ fused bias gradients, f32 or BFP wire epilogue) in one dispatch",
+        pybind11::arg("Xs"), pybind11::arg("dYs"), pybind11::arg("Cs"), pybind11::arg("colsums"),
+        pybind11::arg("offs"), pybind11::arg("workspace"), pybind11::arg("wire") = pybind11::none(),
+        pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1, pybind11::arg("wire_codec") = 1,
+        pybind11::arg("wire_period") = 0);
+  m.def("gemm_wgrad_group_ws", &gemm_wgrad_group_ws_floats, "f32 workspace elements for a group of (M, N) problems");
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);
   m.def("gemm_set_main_loop", [](int mode) { gemm_main_loop_flag().store(mode); },

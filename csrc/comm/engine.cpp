@@ -78,6 +78,8 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
   if (const char* ld = std::getenv("FAN_LAZY_DONE")) lazy_done = ld[0] != '0';
   bool elide_waits = true;  // FAN_ELIDE_WAITS=0: issue every cross-stream wait (A/B of the slot table's skip)
   if (const char* ew = std::getenv("FAN_ELIDE_WAITS")) elide_waits = ew[0] != '0';
+  bool done_words = false;  // FAN_DONE_WORDS=1: comm-stream requests also write their host-mapped done word
+  if (const char* dw = std::getenv("FAN_DONE_WORDS")) done_words = dw[0] != '0';
   const char* ve = std::getenv("FAN_VERIFY");
   verify_ = cfg.verify >= 0 ? cfg.verify > 0 : (ve && ve[0] == '1');
   if (verify_) {
@@ -101,6 +103,7 @@ AllReduceEngine::AllReduceEngine(Comm* comm, int rank, int world, EngineConfig c
   tc.side_epi = side_epi;
   tc.lazy_done = lazy_done;
   tc.elide_waits = elide_waits;
+  tc.done_words = done_words;
   tc.comm = stream_;
   tc.side = epi_stream_;
   table_ = std::make_unique<SlotTable<HipSlotDevice>>(dev_, tc, slot_events_);

@@ -48,6 +48,11 @@ class SlotTable {
     bool side_epi = false;        // world 1: epilogue on the side stream after the producer's enqueued work
     bool lazy_done = true;        // inline: record the done event only when something needs it
     bool elide_waits = true;      // skip cross-stream waits implied by an earlier wait on the comm stream
+    // multi-rank requests finishing on the comm stream: the GPU writes the slot's done word into host memory (the
+    // NIC's done write). Off: their completion is the done event like every other request's — the write is a blit
+    // dispatch on the comm stream (hipStreamWriteValue32, ~20 us of stream time with its two dispatch gaps per
+    // request, profiles/r5_config5_comm_trace.txt)
+    bool done_words = true;
     Stream comm{};                // the engine's communication stream (multi-rank)
     Stream side{};                // the world-1 side-epilogue stream (side_epi)
   };
@@ -177,11 +182,12 @@ class SlotTable {
     ensure_done(sl);  // a lazily recorded done event (this request's, or a superseded one's: conservative)
     if (seq != 0 && seq != sl.seq) {
       // superseded: done if the newer request's done word has passed it (wrap-safe), else the slot's done event
-      if (!cfg_.inline_mode && ((dev_.read_done(s) - seq) & 0xFFFFFFFFu) < (1u << 31)) return true;
+      if (!cfg_.inline_mode && cfg_.done_words && ((dev_.read_done(s) - seq) & 0xFFFFFFFFu) < (1u << 31)) return true;
       return dev_.query(sl.done);
     }
     if (sl.pending) return false;
-    if (cfg_.inline_mode || sl.on_producer || !(sl.epi_stream == sl.stream)) return dev_.query(sl.done);
+    if (cfg_.inline_mode || sl.on_producer || !cfg_.done_words || !(sl.epi_stream == sl.stream))
+      return dev_.query(sl.done);
     return dev_.read_done(s) == sl.seq;
   }
 
@@ -247,7 +253,8 @@ class SlotTable {
     // done_id"); requests finishing on the critical compute stream skip that packet: their completion is the event
     // (on-producer requests too: the host-memory write cost ~50 us before the next forward's first kernel,
     // profiles/r5_forced_step_timeline.txt)
-    if (sl.epi_stream == sl.stream && !cfg_.inline_mode && !sl.on_producer) dev_.write_done(sl.stream, s, sl.seq);
+    if (cfg_.done_words && sl.epi_stream == sl.stream && !cfg_.inline_mode && !sl.on_producer)
+      dev_.write_done(sl.stream, s, sl.seq);
     // Lazy done event: the epilogue ran in its own stream's order (inline requests; multi-rank epilogues on the
     // producer stream), so nothing needs the event unless the host polls the request or another stream waits on
     // it; ensure_done() records it then. Each eager record is a marker packet on the critical compute stream.

@@ -1311,6 +1311,27 @@ __global__ void __launch_bounds__(256, 1)
   else P1::run(p1, (int)blockIdx.x - grid0, (int)gridDim.x - grid0);
 }
 
+// Grouped launch of up to kMaxGroup GEMMs of ONE configuration P, one tile per workgroup (P with the fused bias
+// gradient): problem i owns workgroups [first[i], first[i + 1]), a range padded to a multiple of the XCD count so
+// its local tile index keeps blockIdx.x's XCD (xcd_remap); the padding workgroups find no tile and exit. For a
+// transformer layer's four bwd-weight GEMMs (dW = X^T . dY over the same tokens): each alone fills a fraction of
+// the CUs and needs split-K slabs + a reduce pass, together they fill the chip once (bench/bert_overlap.py).
+constexpr int kMaxGroup = 8;
+template <typename TC>
+struct PlGroup {
+  PlProblem<TC> p[kMaxGroup];
+  int first[kMaxGroup + 1];
+  int n;
+};
+
+template <class P>
+__global__ void __launch_bounds__(256, 1) gemm_groupn_kernel(PlGroup<typename P::TC> g) {
+  const int b = (int)blockIdx.x;
+  int i = 0;
+  while (i + 1 < g.n && b >= g.first[i + 1]) ++i;  // workgroup-uniform
+  P::run(g.p[i], b - g.first[i], g.first[i + 1] - g.first[i]);
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // The same 256x256 4-wave AGPR loop on a ring of FOUR half-stages (32 k each, 32 KiB: the LDS of the two 64-k
 // stages above) with one barrier per k-step instead of per K-tile. Why: the LDS-DMA issue is the loop's limiter
@@ -1584,12 +1605,12 @@ __global__ void __launch_bounds__(256)
 // bias segment of the [W | b] bucket (flat wo.bias_off + n). One block per 64 columns: 16 lanes x float4 columns by
 // 16 part classes (p % 16), each summed in p order, then the classes summed in class order (deterministic).
 template <bool WIRE, bool UPD = false>
-__global__ void __launch_bounds__(256)
-    colsum_reduce_kernel(const float* __restrict__ part, int parts, float* __restrict__ colsum, int N, WireOut wo) {
+__device__ __forceinline__ void colsum_reduce_block(const float* __restrict__ part, int parts,
+                                                    float* __restrict__ colsum, int N, const WireOut& wo, int blk) {
   __shared__ float4 red[16][16];
   __shared__ float fin[64];
   const int t = threadIdx.x, cg = t & 15, pc = t >> 4;
-  const int col = blockIdx.x * 64 + cg * 4;
+  const int col = blk * 64 + cg * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < N) {
     for (int p = pc; p < parts; p += 16) {
@@ -1610,7 +1631,7 @@ __global__ void __launch_bounds__(256)
   }
   if constexpr (WIRE) {
     __syncthreads();
-    const int c16 = blockIdx.x * 64 + t * 16;
+    const int c16 = blk * 64 + t * 16;
     if (t < 4 && c16 < N && wo.bias_off > 0) {  // N % 16 == 0
       float v[16];
 #pragma unroll
@@ -1618,6 +1639,31 @@ __global__ void __launch_bounds__(256)
       wire_store16<UPD>(v, (uint32_t)wo.bias_off + (uint32_t)c16, wo);
     }
   }
+}
+
+template <bool WIRE, bool UPD = false>
+__global__ void __launch_bounds__(256)
+    colsum_reduce_kernel(const float* __restrict__ part, int parts, float* __restrict__ colsum, int N, WireOut wo) {
+  colsum_reduce_block<WIRE, UPD>(part, parts, colsum, N, wo, (int)blockIdx.x);
+}
+
+// The grouped GEMM's bias gradients: problem i's blocks [first[i], first[i + 1]) reduce its partial slabs.
+struct ColsumGroup {
+  const float* part[kMaxGroup];
+  float* colsum[kMaxGroup];
+  WireOut wo[kMaxGroup];
+  int parts[kMaxGroup];
+  int N[kMaxGroup];
+  int first[kMaxGroup + 1];
+  int n;
+};
+
+template <bool WIRE>
+__global__ void __launch_bounds__(256) colsum_reduce_group_kernel(ColsumGroup g) {
+  const int b = (int)blockIdx.x;
+  int i = 0;
+  while (i + 1 < g.n && b >= g.first[i + 1]) ++i;
+  colsum_reduce_block<WIRE>(g.part[i], g.parts[i], g.colsum[i], g.N[i], g.wo[i], b - g.first[i]);
 }
 
 template <int BM, int BN>

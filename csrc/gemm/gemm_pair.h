@@ -1,4 +1,5 @@
-// Grouped backward GEMMs of one layer (bwd-data + bwd-weight in one dispatch). See gemm_pair.hip.
+// Grouped GEMM launches: one layer's bwd-data + bwd-weight in one dispatch, and up to kGroupMax bwd-weight GEMMs of
+// one configuration in one dispatch. See gemm_pair.hip.
 #pragma once
 #include "gemm/gemm.h"
 
@@ -8,5 +9,14 @@ namespace fan {
 // B dZ MN-contiguous, f32 out, tile_bn 128 or 256). grid0 / grid1: workgroups of each (multiples of the XCD count).
 bool gemm_bwd_pair_supported(const GemmArgs& bd, const GemmArgs& bw, int grid0, int grid1);
 void launch_gemm_bwd_pair(const GemmArgs& bd, const GemmArgs& bw, int grid0, int grid1, hipStream_t stream);
+
+// n <= kGroupMax bwd-weight GEMMs dW_i = X_i^T . dY_i (A and B MN-contiguous, f32 out, no accumulate), each with its
+// fused bias gradient (colsum) and either the BFP wire epilogue (all of them) or none; 256x128 tiles, one per
+// workgroup, no split-K: M_i % 256 == 0, N_i % 128 == 0, K_i % 64 == 0. a[i].workspace: f32 scratch of
+// gemm_wgrad_group_ws(a[i]) elements (the bias-gradient partials, one slab per 256-row tile row).
+constexpr int kGroupMax = 8;
+bool gemm_wgrad_group_supported(const GemmArgs* a, int n);
+int64_t gemm_wgrad_group_ws(const GemmArgs& a);
+void launch_gemm_wgrad_group(const GemmArgs* a, int n, hipStream_t stream);
 
 }  // namespace fan

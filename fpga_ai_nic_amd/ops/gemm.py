@@ -119,6 +119,40 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     return C
 
 
+def wgrad_group_supported(problems) -> bool:
+    """Shapes the grouped bwd-weight launch takes: X [K][M], dY [K][N] bf16 with M % 256, N % 128, K % 64 == 0,
+    at most 8 problems (see :func:`gemm_wgrad_group`)."""
+    if not 1 <= len(problems) <= 8:
+        return False
+    for p in problems:
+        X, dY = p[0], p[1]
+        K, M, N = X.shape[0], X.shape[1], dY.shape[1]
+        if M % 256 or N % 128 or K % 64 or dY.shape[0] != K or X.dtype != torch.bfloat16 or not X.is_cuda:
+            return False
+    return True
+
+
+def gemm_wgrad_group(problems, wire=None):
+    """Up to 8 bwd-weight GEMMs in ONE dispatch: for each ``(X, dY, C, colsum[, off])`` C = X^T . dY (f32, or with
+    ``wire=(buf, shard, own, codec[, period])`` BFP-encoded into the bucket's wire buffer at flat offset ``off``,
+    the bias segment right after C) and colsum = the column sums of dY (the fused bias gradient). 256x128 tiles, one
+    per workgroup, no split-K: a transformer layer's projections (each too small to fill the CUs alone) fill them
+    together (csrc/gemm/gemm_pair.hip launch_gemm_wgrad_group)."""
+    Cx = _ext.require()
+    Xs = [p[0] for p in problems]
+    dYs = [p[1] for p in problems]
+    Cs = [p[2] for p in problems]
+    css = [p[3] for p in problems]
+    offs = [int(p[4]) if len(p) > 4 else 0 for p in problems]
+    ws = _workspace(Cs[0].device, Cx.gemm_wgrad_group_ws([(x.shape[1], y.shape[1]) for x, y in zip(Xs, dYs)]))
+    if wire is None:
+        Cx.gemm_wgrad_group(Xs, dYs, Cs, css, offs, ws)
+    else:
+        buf, shard, own, codec = wire[:4]
+        period = wire[4] if len(wire) > 4 else 0
+        Cx.gemm_wgrad_group(Xs, dYs, Cs, css, offs, ws, buf, int(shard), int(own), int(codec), int(period))
+
+
 def _aligned16(C, bias, aux) -> bool:
     """A bf16 output's epilogue stores (and the bias / activation loads beside them) are 16 B per lane."""
     ok = C.data_ptr() % 16 == 0 and C.stride(0) % 8 == 0

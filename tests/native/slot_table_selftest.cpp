@@ -139,6 +139,7 @@ static void run_case(int mode, unsigned seed, bool wrap) {
   cfg.lazy_done = mode != 1 && mode != 5;
   cfg.side_epi = mode == 2;
   cfg.epi_on_producer = mode >= 4;
+  cfg.done_words = seed % 2 == 0;  // multi-rank completion by the done word or by the done event
   cfg.comm = COMM;
   cfg.side = SIDE;
   std::vector<int> evs;

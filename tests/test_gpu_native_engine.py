@@ -207,9 +207,11 @@ def test_mlp_mpi_cli_native_engine_gpu():
 
 
 @pytest.mark.parametrize("force", [False, True])
-def test_engine_perf_counters(force):
+def test_engine_perf_counters(force, monkeypatch):
     """Perf counters (the NIC's latency / host-stall registers): requests, logical / wire bytes, host wait time
-    and summed device time of timed requests."""
+    and summed device time of timed requests. The multi-rank engine with FAN_DONE_WORDS=1 (the NIC's done write
+    into host memory; off by default, completion is then the done event)."""
+    monkeypatch.setenv("FAN_DONE_WORDS", "1")
     eng = NativeAllReduce(_native_transport() if force else None, codec="bfp_rne", force_comm=force)
     eng.reset_counters()
     eng.timing = True
