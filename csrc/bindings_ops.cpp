@@ -69,7 +69,13 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     g.bias = bias->data_ptr();
   }
   if (aux) {
-    TORCH_CHECK(aux->scalar_type() == C.scalar_type(), "aux dtype must match C");
+    if (is_bits_epi((int)epilogue)) {  // the 1-bit ReLU mask plane: uint8 [M][ldaux bytes]
+      TORCH_CHECK(aux->is_cuda() && aux->scalar_type() == at::kByte && aux->dim() == 2 && aux->size(0) == g.M &&
+                      aux->size(1) * 8 >= g.N,
+                  "mask-bit epilogue: aux must be a uint8 [M][>= N/8] GPU plane");
+    } else {
+      TORCH_CHECK(aux->scalar_type() == C.scalar_type(), "aux dtype must match C");
+    }
     g.aux = aux->data_ptr();
     g.ldaux = ld_of(*aux);
   }

@@ -184,14 +184,20 @@ struct Out<bf16_t> {
 template <int EPI, typename TC, bool ACCUM>
 __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                      const TC* __restrict__ aux, int64_t ldaux, int row, int col) {
-  if (EPI == kEpiBias || EPI == kEpiBiasRelu) {
+  static_assert(EPI != kEpiBiasReluBits || sizeof(TC) == 2, "mask-bit epilogues: bf16 output");
+  if (EPI == kEpiBias || EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {
     const uint2 u = *reinterpret_cast<const uint2*>(bias + col);
     v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xFFFF0000u);
     v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xFFFF0000u);
   }
-  if (EPI == kEpiBiasRelu) {
+  if (EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {  // (4-column paths never write mask bits: split-K only)
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = fmaxf(v[u], 0.f);
+  }
+  if (EPI == kEpiReluBits) {
+    const uint32_t b = reinterpret_cast<const uint8_t*>(aux)[(int64_t)row * ldaux + col / 8] >> (col & 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (b >> u) & 1u ? v[u] : 0.f;
   }
   if (EPI == kEpiReluMask) {
     float m[4];
@@ -213,19 +219,26 @@ __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc
 // epilogue of a 256x256 bf16 tile is store-ISSUE-bound (MI355X_MICROARCH.md per-instruction table: a dwordx2 store
 // tail runs at about half the rate of dwordx4), so the bf16 outputs are written 8 columns per lane. Same
 // arithmetic, element for element, as epi4.
+// kEpiReluBits: `bits` holds the 8 mask bits of these columns; kEpiBiasReluBits: returns them (bit u: the stored bf16
+// output u is > 0, the test kEpiReluMask applies to the activation).
 template <int EPI, bool ACCUM>
-__device__ __forceinline__ void epi8_bf16(float v[8], bf16_t* __restrict__ C, int64_t ldc,
-                                          const bf16_t* __restrict__ bias, const uint4* mask, int row, int col) {
+__device__ __forceinline__ uint32_t epi8_bf16(float v[8], bf16_t* __restrict__ C, int64_t ldc,
+                                              const bf16_t* __restrict__ bias, const uint4* mask, uint32_t bits,
+                                              int row, int col) {
   auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
   auto hi = [](uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); };
-  if (EPI == kEpiBias || EPI == kEpiBiasRelu) {
+  if (EPI == kEpiBias || EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {
     const uint4 u = *reinterpret_cast<const uint4*>(bias + col);
     v[0] += lo(u.x); v[1] += hi(u.x); v[2] += lo(u.y); v[3] += hi(u.y);
     v[4] += lo(u.z); v[5] += hi(u.z); v[6] += lo(u.w); v[7] += hi(u.w);
   }
-  if (EPI == kEpiBiasRelu) {
+  if (EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
+  }
+  if (EPI == kEpiReluBits) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (bits >> u) & 1u ? v[u] : 0.f;
   }
   if (EPI == kEpiReluMask) {
     const uint4 m = *mask;
@@ -239,8 +252,19 @@ __device__ __forceinline__ void epi8_bf16(float v[8], bf16_t* __restrict__ C, in
     v[0] += lo(o.x); v[1] += hi(o.x); v[2] += lo(o.y); v[3] += hi(o.y);
     v[4] += lo(o.z); v[5] += hi(o.z); v[6] += lo(o.w); v[7] += hi(o.w);
   }
-  *reinterpret_cast<uint4*>(p) = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
-                                            pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+  const uint4 o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                             pack_bf16x2(v[6], v[7]));
+  *reinterpret_cast<uint4*>(p) = o;
+  uint32_t out = 0;
+  if (EPI == kEpiBiasReluBits) {  // positive finite or +inf: bf16 bits in [1, 0x7F80] (what "> 0" holds for)
+    const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t h = (u & 1) ? (w[u >> 1] >> 16) : (w[u >> 1] & 0xFFFFu);
+      out |= (h - 1u < 0x7F80u ? 1u : 0u) << u;
+    }
+  }
+  return out;
 }
 
 // kEpiWire target (GemmArgs::wire*): passed by value as one kernel argument.
@@ -524,8 +548,20 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
       constexpr int NP8 = 16 / RP8;
       static_assert(WTN % 8 == 0 && RP8 <= 16 && 16 % RP8 == 0, "8-column chunks of whole 16-row blocks");
       constexpr bool kPf8 = EPI == kEpiReluMask;
+      constexpr bool kBitsIn = EPI == kEpiReluBits, kBitsOut = EPI == kEpiBiasReluBits;
       constexpr int kPfd = 2;
       uint4 aq8[kPf8 ? MI : 1][kPf8 ? NP8 : 1];
+      uint32_t bq[kBitsIn ? MI : 1][kBitsIn ? NP8 : 1];
+      // mask bits: one byte per lane (its 8 columns) per pass, prefetched like the activation chunks
+      auto bits_load = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+        for (int pass = 0; pass < NP8; ++pass) {
+          const int row = row0 + i * 16 + pass * RP8 + lane / C8;
+          const int col = col0 + (lane % C8) * 8;
+          if (!mn_edge || (row < M && col < N))
+            bq[i][pass] = reinterpret_cast<const uint8_t*>(aux)[(int64_t)row * ldaux + col / 8];
+        }
+      };
       auto aux_load8 = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
         for (int pass = 0; pass < NP8; ++pass) {
@@ -539,10 +575,17 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
 #pragma unroll
         for (int i = 0; i < kPfd && i < MI; ++i) aux_load8(i);
       }
+      if constexpr (kBitsIn) {
+#pragma unroll
+        for (int i = 0; i < kPfd && i < MI; ++i) bits_load(i);
+      }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         if constexpr (kPf8) {
           if (i + kPfd < MI) aux_load8(i + kPfd);
+        }
+        if constexpr (kBitsIn) {
+          if (i + kPfd < MI) bits_load(i + kPfd);
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
@@ -561,7 +604,11 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
           if (mn_edge && (row >= M || col >= N)) continue;  // N % 8 == 0: an 8-column chunk is wholly in or out
           const uint4* mk = nullptr;
           if constexpr (kPf8) mk = &aq8[i][pass];
-          epi8_bf16<EPI, ACCUM>(v, reinterpret_cast<bf16_t*>(C), ldc, bias, mk, row, col);
+          uint32_t bits = 0;
+          if constexpr (kBitsIn) bits = bq[i][pass];
+          const uint32_t ob = epi8_bf16<EPI, ACCUM>(v, reinterpret_cast<bf16_t*>(C), ldc, bias, mk, bits, row, col);
+          if constexpr (kBitsOut)  // aux is the mask plane this forward writes
+            reinterpret_cast<uint8_t*>(const_cast<TC*>(aux))[(int64_t)row * ldaux + col / 8] = (uint8_t)ob;
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);
       }
@@ -1708,7 +1755,7 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
     // (and the in-kernel wire encode: since the 4-wave kernel became persistent, the 4096^2 bwd-weight with the wire
     // + bias-gradient epilogue runs faster in the step there, 1.036-1.038 vs 1.042-1.052 ms/step,
     // profiles/r2_pl3_wire_ab.txt; in isolation it measured +13 vs +7 us for the encode)
-    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192 || EPI == kEpiReluMask));
+    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192 || EPI == kEpiReluMask || is_bits_epi(EPI)));
     if (pl4 && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto launch = [&](auto k, bool persist) {  // persist: the kernel loops over tiles (not with colsum)
@@ -1858,6 +1905,11 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   };
   wo.off = (uint32_t)a.wire_off;
 
+  if constexpr (is_bits_epi(EPI)) {  // no split-K (the 4-column reduce path cannot write mask bytes)
+    FAN_CHECK(sk == 1, "mask-bit epilogues: no split-K");
+    launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>(a, sk, wo, s);
+    return;
+  }
   if (sk > 1) {
     // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + p*N]), then an ordered reduce that
     // applies the epilogue (deterministic: slabs summed in split order)
@@ -1902,6 +1954,14 @@ void launch_epi(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_EPI_CASE(kEpiBias)
     FAN_EPI_CASE(kEpiBiasRelu)
     FAN_EPI_CASE(kEpiReluMask)
+    case kEpiBiasReluBits:  // mask-bit epilogues: bf16 output only (the 8-column store path writes / reads the bits)
+      FAN_CHECK(a.c_bf16 && !a.accumulate, "mask-bit epilogues: bf16 output, no accumulate");
+      launch_typed<BM, BN, WM, WN, AK, BKC, kEpiBiasReluBits, bf16_t, false>(a, sk, s);
+      break;
+    case kEpiReluBits:
+      FAN_CHECK(a.c_bf16 && !a.accumulate, "mask-bit epilogues: bf16 output, no accumulate");
+      launch_typed<BM, BN, WM, WN, AK, BKC, kEpiReluBits, bf16_t, false>(a, sk, s);
+      break;
     case kEpiWire:  // only the bwd-weight layout (A and B MN-contiguous) produces wire-ready gradients
       if constexpr (!AK && !BKC) {
         FAN_CHECK(!a.c_bf16 && !a.accumulate, "wire epilogue: f32, no accumulate");

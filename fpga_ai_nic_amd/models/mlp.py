@@ -12,6 +12,8 @@ no gather/scatter copies, no separate optimizer pass.
 """
 from __future__ import annotations
 
+import os
+
 import math
 from dataclasses import dataclass
 
@@ -164,14 +166,35 @@ class MLP:
         self.act = [torch.empty(mb, c, dtype=adt, device=dev) for c in self.sizes[:-1]]
         self.logits = torch.empty(mb, self.sizes[-1], dtype=torch.float32, device=dev)
         self.dz = [None] + [torch.empty(mb, c, dtype=adt, device=dev) for c in self.sizes[1:]]
+        # 1-bit ReLU masks of the hidden activations (uint8 [mb][c/8]): written by the forward GEMM, read by the
+        # bwd-data GEMM instead of the bf16 activation (ops/gemm.py EPI_RELU_BITS)
+        self.mask = [None] * self.L
+        for i in range(1, self.L):
+            if self._relu_at(i - 1) and self._bits_ok(mb, i):
+                self.mask[i] = torch.empty(mb, self.sizes[i] // 8, dtype=torch.uint8, device=dev)
         self.loss_rows = torch.empty(mb, dtype=torch.float32, device=dev)
         self._act_mb = mb
+
+    def _bits_ok(self, mb: int, i: int) -> bool:
+        """Activation i (output of layer i - 1, input of layer i) through mask bits (opt-in, FAN_RELU_BITS=1): bf16
+        GPU model, and both GEMMs (layer i - 1's forward, layer i's bwd-data) on whole-wave unsplit static plans.
+        Measured slower on the flagship step (1.047-1.049 vs 1.023-1.035 ms/step, profiles/r5_relu_bits_ab.txt):
+        the bwd-data GEMMs gain 4-11 us, but the forward's extra byte stores cost 7-10 us per GEMM, and the
+        bwd-weight GEMM that follows each bwd-data GEMM loses the activation the mask read had just pulled into the
+        MALL (+5 / +21 us)."""
+        if not (self.device.type == "cuda" and self.dtype == torch.bfloat16 and self.bias):
+            return False
+        if os.environ.get("FAN_RELU_BITS", "0") != "1":
+            return False
+        c_in, c, c_out = self.sizes[i - 1], self.sizes[i], self.sizes[i + 1]
+        return G.mask_bits_supported(mb, c, c_in) and G.mask_bits_supported(mb, c, c_out)
 
     # ------------------------------------------------------------------ compute
     def forward_layer(self, i: int):
         l = self.layers[i]
         out = self.act[i + 1] if i + 1 < self.L else self.logits
-        G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i))
+        mask = self.mask[i + 1] if i + 1 < self.L else None
+        G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i), mask_out=mask)
 
     def loss_backward(self, labels, grad_scale: float):
         NN.softmax_xent(self.logits, labels, self.dz[self.L], self.loss_rows, grad_scale)
@@ -208,7 +231,11 @@ class MLP:
         if i == 0:
             return
         l = self.layers[i]
-        G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i], relu_input=self.act[i] if self._relu_at(i - 1) else None)
+        if self.mask[i] is not None:
+            G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i], relu_bits=self.mask[i])
+        else:
+            G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i],
+                              relu_input=self.act[i] if self._relu_at(i - 1) else None)
 
     def forward(self, x):
         """Inference forward (returns f32 logits)."""
