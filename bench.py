@@ -359,13 +359,15 @@ def main(argv=None):
         trainer, model, engine = setup.trainer, setup.model, setup.engine
         x, y = batch(mb, seed, model)
         wd.arm(f"warmup {tag} mb={mb}")
-        if tag in ("timed", "ref") and cuda and a.settle_ms > 0:
+        if tag in ("timed", "ref", "split") and cuda and a.settle_ms > 0:
             # The shader clock needs ~50 ms of sustained load to reach the level a training run holds: the driver's
             # 5 warmup + 20 steps read 1.038-1.047 ms/step where 50 + 20 read 0.989 and 5 + 100 0.996
             # (profiles/r4_warmup_settle.jsonl). Untimed steps of the same batch in chunks of 10 until settle_ms
             # passed (the chunk count agreed over ranks, so every rank runs the same steps); then W + K as ever.
             # Both timed cells (the headline and the reference batch, extra.mb<ref>) get it, so they are measured
-            # alike (extra.settle per cell).
+            # alike (extra.settle per cell), and so do the world-1 split cells (unfused update, forced multi-rank
+            # path): built after the headline, they start from an idle clock (forced_dist read 1.15-1.18 ms/step
+            # without it, 1.06-1.07 standalone with it).
             t_s, n_s = time.perf_counter(), 0
             while n_s < 5000:
                 for _ in range(10):
