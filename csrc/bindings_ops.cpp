@@ -304,6 +304,9 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1, pybind11::arg("wire_codec") = 1,
         pybind11::arg("wire_period") = 0);
   m.def("gemm_wgrad_group_ws", &gemm_wgrad_group_ws_floats, "f32 workspace elements for a group of (M, N) problems");
+  m.def("gemm_set_occ2", [](int on) { gemm_occ2_flag().store(on); },
+        "unsplit 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)");
+  m.def("gemm_occ2", []() { return gemm_occ2_flag().load(); });
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);
   m.def("gemm_set_main_loop", [](int mode) { gemm_main_loop_flag().store(mode); },

@@ -92,6 +92,9 @@ std::atomic<int>& gemm_persist_flag();
 // 256x256 persistent 4-wave loop on the ring of four 32-k half-stages (gemm_pl4h_kernel) instead of two 64-k stages
 // (FAN_GEMM_HALF, gemm_set_half_stage)
 std::atomic<int>& gemm_half_stage_flag();
+// unsplit, bias-gradient-free 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)
+// instead of the persistent one-workgroup-per-CU kernel (FAN_GEMM_OCC2, gemm_set_occ2)
+std::atomic<int>& gemm_occ2_flag();
 // split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
 // separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
 // gemm_set_fixup); bit-identical either way

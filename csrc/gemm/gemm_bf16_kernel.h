@@ -1582,6 +1582,116 @@ __global__ void __launch_bounds__(256, 1)
   }
 }
 
+// Two workgroups per CU (occupancy 2: two waves per SIMD from DIFFERENT workgroups). 256x128 tiles, 4 waves of
+// 128x64 (128 AGPR accumulators), a ring of THREE 32-k half-stages (24 KiB each: 72 KiB per workgroup, 144 per CU),
+// one barrier per half-stage. Why: in gemm_pl4_kernel (one wave per SIMD) the SIMD idles whenever its only wave
+// stalls — on the LDS-DMA issue (a build without it is 12-13 % faster), the barrier, the fragment reads, the
+// epilogue's stores — and every CU writes its tile's output at the same moment. Two independent workgroups per CU
+// stall at different times (their barriers are their own), so one's MFMAs fill the other's stalls, and their
+// epilogues fall at different times. The 8-wave gemm_pl_kernel also ran two waves per SIMD, but of ONE workgroup,
+// sharing its barriers and DMA phases. Fragments single-buffered (the other workgroup covers the read latency):
+//   half-stage h: wait own pieces of h (vmcnt(G): h + 1's may stay in flight), barrier (everyone's pieces of h
+//   landed, everyone's reads of h - 1 retired), DMA of h + 2 into stage (h + 2) % 3 = the stage of h - 1, the 12
+//   fragment reads of h, 32 MFMAs.
+// Same k order as gemm_pl4_kernel's 256x128 tiles: bit-identical results. Opt-in (FAN_GEMM_OCC2=1): it replaces the
+// persistent 256x256 kernel of unsplit, bias-gradient-free plans.
+template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
+__global__ void __launch_bounds__(256, 2)
+    gemm_pl2h_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
+                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
+                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
+                     float* __restrict__ colsum, WireOut wo) {
+  constexpr int BM = 256, BN = 128, NT = 256, HK = 32, IB = NT * 16;
+  constexpr int A_BYTES = BM * HK * 2, STAGE = A_BYTES + BN * HK * 2;  // 16 + 8 KiB
+  constexpr int GA = A_BYTES / IB, G = GA + BN * HK * 2 / IB;         // 4 + 2 pieces per wave and half-stage
+  constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NJ = WTN / 16;
+  constexpr int Q = MI * NJ, DSP = Q / G;  // 32 MFMAs, a DMA piece every 5
+  static_assert(G * DSP <= Q, "schedule");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  (void)split_k; (void)colsum;
+
+  const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / 2, wn = wave % 2;
+  const uint32_t lds0 = lds_addr_of(smem);
+  auto tile_body = [&](int v) __attribute__((always_inline)) {
+  const int tile = xcd_remap(v, tiles);
+  const int GM = tiles_m >= 4 ? 4 : tiles_m;
+  const int grp = tile / (GM * tiles_n);
+  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
+  const int in_grp = tile % (GM * tiles_n);
+  const int m0 = (grp * GM + in_grp % gm) * BM;
+  const int n0 = (in_grp / gm) * BN;
+  const int nh = K / HK;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint32_t off[G];
+#pragma unroll
+  for (int p = 0; p < GA; ++p) off[p] = piece_off_h<AK, BM, NT>(lda, m0, wave, lane, p);
+#pragma unroll
+  for (int p = GA; p < G; ++p) off[p] = piece_off_h<BKC, BN, NT>(ldb, n0, wave, lane, p - GA);
+  const int64_t a_step = AK ? (int64_t)HK * 2 : (int64_t)HK * lda * 2;
+  const int64_t b_step = BKC ? (int64_t)HK * 2 : (int64_t)HK * ldb * 2;
+  const char* a_k0 = reinterpret_cast<const char*>(A);
+  const char* b_k0 = reinterpret_cast<const char*>(B);
+
+  // glds piece p of half-stage `src` (clamped by the caller) into LDS stage `stg` (0..2)
+  auto piece = [&](int stg, int src, int p) __attribute__((always_inline)) {
+    const uint32_t st = lds0 + stg * STAGE + wave * 1024;
+    if (p < GA) glds16_s(a_k0 + src * a_step, off[p], st + p * IB);
+    else glds16_s(b_k0 + src * b_step, off[p], st + A_BYTES + (p - GA) * IB);
+  };
+
+  // prologue: half-stages 0 and 1 in flight
+#pragma unroll
+  for (int p = 0; p < G; ++p) piece(0, 0, p);
+#pragma unroll
+  for (int p = 0; p < G; ++p) piece(1, min(1, nh - 1), p);
+
+  int st = 0;  // stage of h
+  for (int h = 0; h < nh; ++h) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    asm volatile("s_barrier" ::: "memory");
+    const char* rd = smem + st * STAGE;
+    const int dst = st == 0 ? 2 : st - 1;  // (h + 2) % 3
+    const int src = min(h + 2, nh - 1);    // past the end: the last half-stage again (keeps vmcnt's count)
+    s16x8 fa[MI], fb[NJ];
+#pragma unroll
+    for (int r = 0; r < MI; ++r) fa[r] = read_frag_h<AK>(rd, wm * WTM + r * 16, lane);
+#pragma unroll
+    for (int r = 0; r < NJ; ++r) fb[r] = read_frag_h<BKC>(rd + A_BYTES, wn * WTN + r * 16, lane);
+    static_for<Q>([&](auto qc) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+#ifndef FAN_GEMM_NODMA
+      if constexpr (q % DSP == 0 && q / DSP < G) piece(dst, src, q / DSP);
+#endif
+      mfma_acc(acc[q / NJ][q % NJ], fa[q / NJ], fb[q % NJ]);
+    });
+    st = st == 2 ? 0 : st + 1;
+  }
+
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces write the LDS too
+  __syncthreads();
+  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, false>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
+                                                 aux, ldaux, M, N, 0, ws, wo);
+  };
+  for (int v = blockIdx.x; v < tiles; v += gridDim.x) {
+    tile_body(v);
+    __syncthreads();  // every wave's staging reads done before the next tile's DMA overwrites the LDS
+  }
+}
+
 // Ordered split-K reduction + epilogue (deterministic: slabs summed in split order). SK > 0: the split count as a
 // compile-time constant, so every slab's load is issued before the first add (SK = 0: runtime split_k, one slab
 // per loop trip).
@@ -1766,6 +1876,21 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
         if (fixed) *fixed = wf.fix != nullptr;
       };
       const bool half = gemm_half_stage_flag().load(std::memory_order_relaxed) != 0;
+      if constexpr (!SPLIT && !is_wire_epi(EPI)) {
+        // two workgroups per CU on 256x128 tiles (gemm_pl2h_kernel, opt-in)
+        if (gemm_occ2_flag().load(std::memory_order_relaxed) != 0 && !a.colsum && sk == 1 && a.K % 32 == 0) {
+          constexpr int lds2 = 3 * (256 + 128) * 32 * 2;
+          auto k = gemm_pl2h_kernel<AK, BKC, EPI, TC, ACCUM>;
+          FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds2));
+          const int tiles2 = (a.M / 256) * (a.N / 128);
+          const int cap = gemm_persist_flag().load(std::memory_order_relaxed);
+          const int g2 = cap > 0 && tiles2 > 2 * cap ? 2 * cap : tiles2;
+          hipLaunchKernelGGL(k, g2, 256, lds2, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
+                             a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1,
+                             (float*)a.workspace, a.colsum, wo);
+          return 0;
+        }
+      }
       if constexpr (!BKC) {
         if (a.colsum) {
           if (half) launch(gemm_pl4h_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);

@@ -31,6 +31,14 @@ extern template void launch_tile<true, false>(const GemmArgs&, int, int, int, in
 extern template void launch_tile<true, true>(const GemmArgs&, int, int, int, int, hipStream_t);
 }  // namespace gemm_detail
 
+std::atomic<int>& gemm_occ2_flag() {
+  static std::atomic<int> flag{[] {
+    const char* e = getenv("FAN_GEMM_OCC2");
+    return e && e[0] == '1' ? 1 : 0;
+  }()};
+  return flag;
+}
+
 std::atomic<int>& gemm_main_loop_flag() {
   // 256x256 main loop (aligned shapes): 2 software-pipelined, 4 or 8 waves by layout / K (default), 0 one-role
   // loop (FAN_GEMM_PL=0), 3 / 5 pipelined 4-wave / 8-wave only. Selectable for in-process A/B (gemm_set_main_loop).
