@@ -304,6 +304,9 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1, pybind11::arg("wire_codec") = 1,
         pybind11::arg("wire_period") = 0);
   m.def("gemm_wgrad_group_ws", &gemm_wgrad_group_ws_floats, "f32 workspace elements for a group of (M, N) problems");
+  m.def("gemm_set_prio", [](int on) { gemm_prio_flag().store(on); },
+        "4-wave pipelined GEMM waves at s_setprio 2 (another stream's kernels issue in their stalls)");
+  m.def("gemm_prio", []() { return gemm_prio_flag().load(); });
   m.def("gemm_set_occ2", [](int on) { gemm_occ2_flag().store(on); },
         "unsplit 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)");
   m.def("gemm_occ2", []() { return gemm_occ2_flag().load(); });

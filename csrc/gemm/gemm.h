@@ -95,6 +95,9 @@ std::atomic<int>& gemm_half_stage_flag();
 // unsplit, bias-gradient-free 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)
 // instead of the persistent one-workgroup-per-CU kernel (FAN_GEMM_OCC2, gemm_set_occ2)
 std::atomic<int>& gemm_occ2_flag();
+// the 4-wave pipelined GEMM waves at s_setprio 2, so another stream's kernels sharing their CUs (the all-reduce's)
+// issue in the GEMM waves' stalls only (default on; FAN_GEMM_PRIO=0, gemm_set_prio)
+std::atomic<int>& gemm_prio_flag();
 // split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
 // separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
 // gemm_set_fixup); bit-identical either way

@@ -294,6 +294,9 @@ struct WireOut {
   // flat bucket index of C(0, 0) (GemmArgs::wire_off): a weight matrix that is not the first tensor of its bucket
   // (a transformer layer's bucket holds several; bench/bert_overlap.py). bias_off is absolute (includes it).
   uint32_t off;
+  // > 0: the 4-wave persistent loops run their waves at this s_setprio level (gemm_prio_flag): a kernel of another
+  // stream sharing the CU (the all-reduce's copy / reduce / SGD kernels) then issues only in the GEMM wave's stalls
+  int prio;
 };
 
 // flat index -> (shard, position); f < 2^31, shard >= 256: the float estimate is off by at most one
@@ -1154,6 +1157,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / 2, wn = wave % 2;
   const uint32_t lds0 = lds_addr_of(smem);
+  if (wo.prio > 0) __builtin_amdgcn_s_setprio(2);
   // Persistent over its tiles when the grid is smaller than the tile count (one workgroup per CU, grid a multiple
   // of the XCD count, so virtual block v = blockIdx.x + i * gridDim.x stays on blockIdx.x's XCD): a workgroup's
   // next tile starts its operand DMA while the previous tile's epilogue stores drain, instead of a new workgroup
@@ -2029,6 +2033,7 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
 #endif
   };
   wo.off = (uint32_t)a.wire_off;
+  wo.prio = gemm_prio_flag().load(std::memory_order_relaxed);
 
   if constexpr (is_bits_epi(EPI)) {  // no split-K (the 4-column reduce path cannot write mask bytes)
     FAN_CHECK(sk == 1, "mask-bit epilogues: no split-K");

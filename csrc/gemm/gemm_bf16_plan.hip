@@ -31,6 +31,16 @@ extern template void launch_tile<true, false>(const GemmArgs&, int, int, int, in
 extern template void launch_tile<true, true>(const GemmArgs&, int, int, int, int, hipStream_t);
 }  // namespace gemm_detail
 
+std::atomic<int>& gemm_prio_flag() {
+  static std::atomic<int> flag{[] {
+    // default on: the multi-rank step 1.087-1.089 vs 1.093-1.101 ms/step (1-rank group, sharded update), config 5
+    // 2.562-2.571 vs 2.587-2.629 ms (profiles/r5_gemm_prio_ab.txt); no other waves share the CU at world 1
+    const char* e = getenv("FAN_GEMM_PRIO");
+    return e && e[0] == '0' ? 0 : 1;
+  }()};
+  return flag;
+}
+
 std::atomic<int>& gemm_occ2_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_OCC2");

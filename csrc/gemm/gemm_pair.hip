@@ -34,6 +34,7 @@ void launch_group(const GemmArgs& a0, const GemmArgs& a1, int grid0, int grid1, 
 // WireOut of one problem, as launch_typed builds it (the bias segment right after C in the flat bucket)
 WireOut wire_of(const GemmArgs& a) {
   WireOut wo{};
+  wo.prio = gemm_prio_flag().load(std::memory_order_relaxed);
   if (a.wire) {
     wo.p = a.wire;
     wo.shard = a.wire_shard;
