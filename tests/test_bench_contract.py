@@ -25,7 +25,7 @@ def _json_lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
 
 
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("world", [1, 2, 3, 4])  # 3: the reference's world size (sw/run.sh: mpirun -n 3)
 def test_bench_json_contract(world, tmp_path):
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
             "--mb-per-gpu", "16"]
