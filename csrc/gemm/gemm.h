@@ -98,6 +98,9 @@ std::atomic<int>& gemm_occ2_flag();
 // the 4-wave pipelined GEMM waves at s_setprio 2, so another stream's kernels sharing their CUs (the all-reduce's)
 // issue in the GEMM waves' stalls only (default on; FAN_GEMM_PRIO=0, gemm_set_prio)
 std::atomic<int>& gemm_prio_flag();
+// 256x256 bf16 plans on the persistent loop whose tile transitions overlap the epilogue with the next tile's first
+// K-tiles (pl4_run OVL; default on, FAN_GEMM_OVL=0, gemm_set_ovl)
+std::atomic<int>& gemm_ovl_flag();
 // split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
 // separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
 // gemm_set_fixup); bit-identical either way

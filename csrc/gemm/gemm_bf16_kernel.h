@@ -527,12 +527,16 @@ __device__ __forceinline__ void colsum_finish(float (&cs)[NJ], int lane, int col
 // region one 16-row block at a time and written as coalesced row segments (f32 16 B / bf16 8 B per lane), with
 // the fused epilogue; SPLIT writes the f32 partial slab of K-split ksplit; kEpiWire encodes whole 16-column
 // groups (one lane per group: 16-B mantissa store + exponent byte). Caller: all LDS operand reads retired.
-template <int MI, int NJ, int WTN, int EPI, typename TC, bool ACCUM, bool SPLIT>
+// SW (bf16 8-column path only): staged columns per pass over a 16-row block — WTN, or 64 (two halves: 17 KiB of
+// staging for 4 waves instead of 33, beside the operand stages of the overlapped persistent loop).
+template <int MI, int NJ, int WTN, int EPI, typename TC, bool ACCUM, bool SPLIT, int SW = WTN>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* smem, int wave, int lane, int row0,
                                            int col0, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                            const TC* __restrict__ aux, int64_t ldaux, int M, int N, int ksplit,
                                            float* __restrict__ ws, const WireOut& wo, bool mn_edge = false) {
-  constexpr int EW = WTN + 4;  // staged row stride in floats (16-B aligned, breaks bank aliasing)
+  static_assert(SW == WTN || (SW == 64 && WTN % 64 == 0 && sizeof(TC) == 2 && !SPLIT && !is_wire_epi(EPI)),
+                "64-column staging: bf16 8-column path only");
+  constexpr int EW = SW + 4;  // staged row stride in floats (16-B aligned, breaks bank aliasing)
   float* stg = reinterpret_cast<float*>(smem) + wave * (16 * EW);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   constexpr int C4 = WTN / 4;   // float4 chunks per staged row
@@ -546,33 +550,38 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
   // persistent kernels.
   if constexpr (sizeof(TC) == 2 && !SPLIT && !is_wire_epi(EPI)) {
     {
-      constexpr int C8 = WTN / 8;   // 16-B chunks per staged row
+      constexpr int C8 = SW / 8;    // 16-B chunks per staged row
       constexpr int RP8 = 64 / C8;  // rows per pass
       constexpr int NP8 = 16 / RP8;
+      constexpr int HV = WTN / SW;  // staged column halves
       static_assert(WTN % 8 == 0 && RP8 <= 16 && 16 % RP8 == 0, "8-column chunks of whole 16-row blocks");
       constexpr bool kPf8 = EPI == kEpiReluMask;
       constexpr bool kBitsIn = EPI == kEpiReluBits, kBitsOut = EPI == kEpiBiasReluBits;
       constexpr int kPfd = 2;
-      uint4 aq8[kPf8 ? MI : 1][kPf8 ? NP8 : 1];
-      uint32_t bq[kBitsIn ? MI : 1][kBitsIn ? NP8 : 1];
+      uint4 aq8[kPf8 ? MI : 1][kPf8 ? HV * NP8 : 1];
+      uint32_t bq[kBitsIn ? MI : 1][kBitsIn ? HV * NP8 : 1];
       // mask bits: one byte per lane (its 8 columns) per pass, prefetched like the activation chunks
       auto bits_load = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
-        for (int pass = 0; pass < NP8; ++pass) {
-          const int row = row0 + i * 16 + pass * RP8 + lane / C8;
-          const int col = col0 + (lane % C8) * 8;
-          if (!mn_edge || (row < M && col < N))
-            bq[i][pass] = reinterpret_cast<const uint8_t*>(aux)[(int64_t)row * ldaux + col / 8];
-        }
+        for (int hv = 0; hv < HV; ++hv)
+#pragma unroll
+          for (int pass = 0; pass < NP8; ++pass) {
+            const int row = row0 + i * 16 + pass * RP8 + lane / C8;
+            const int col = col0 + hv * SW + (lane % C8) * 8;
+            if (!mn_edge || (row < M && col < N))
+              bq[i][hv * NP8 + pass] = reinterpret_cast<const uint8_t*>(aux)[(int64_t)row * ldaux + col / 8];
+          }
       };
       auto aux_load8 = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
-        for (int pass = 0; pass < NP8; ++pass) {
-          const int row = row0 + i * 16 + pass * RP8 + lane / C8;
-          const int col = col0 + (lane % C8) * 8;
-          if (!mn_edge || (row < M && col < N))
-            aq8[i][pass] = *reinterpret_cast<const uint4*>(aux + (int64_t)row * ldaux + col);
-        }
+        for (int hv = 0; hv < HV; ++hv)
+#pragma unroll
+          for (int pass = 0; pass < NP8; ++pass) {
+            const int row = row0 + i * 16 + pass * RP8 + lane / C8;
+            const int col = col0 + hv * SW + (lane % C8) * 8;
+            if (!mn_edge || (row < M && col < N))
+              aq8[i][hv * NP8 + pass] = *reinterpret_cast<const uint4*>(aux + (int64_t)row * ldaux + col);
+          }
       };
       if constexpr (kPf8) {
 #pragma unroll
@@ -591,9 +600,11 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
           if (i + kPfd < MI) bits_load(i + kPfd);
         }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
+        for (int hv = 0; hv < HV; ++hv) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) stg[(row_l + r) * EW + j * 16 + col_l] = acc[i][j][r];
+        for (int j = 0; j < SW / 16; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) stg[(row_l + r) * EW + j * 16 + col_l] = acc[i][hv * (SW / 16) + j][r];
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own LDS writes landed (wave-private region)
 #pragma unroll
         for (int pass = 0; pass < NP8; ++pass) {
@@ -603,17 +614,18 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
           const float4 q1 = *reinterpret_cast<const float4*>(stg + rr * EW + cc + 4);
           float v[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
           const int row = row0 + i * 16 + rr;
-          const int col = col0 + cc;
+          const int col = col0 + hv * SW + cc;
           if (mn_edge && (row >= M || col >= N)) continue;  // N % 8 == 0: an 8-column chunk is wholly in or out
           const uint4* mk = nullptr;
-          if constexpr (kPf8) mk = &aq8[i][pass];
+          if constexpr (kPf8) mk = &aq8[i][hv * NP8 + pass];
           uint32_t bits = 0;
-          if constexpr (kBitsIn) bits = bq[i][pass];
+          if constexpr (kBitsIn) bits = bq[i][hv * NP8 + pass];
           const uint32_t ob = epi8_bf16<EPI, ACCUM>(v, reinterpret_cast<bf16_t*>(C), ldc, bias, mk, bits, row, col);
           if constexpr (kBitsOut)  // aux is the mask plane this forward writes
             reinterpret_cast<uint8_t*>(const_cast<TC*>(aux))[(int64_t)row * ldaux + col / 8] = (uint8_t)ob;
         }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // the staged rows are read before the next half / block rewrites them
+        }
       }
       return;
     }
@@ -1124,8 +1136,14 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
 // problem's tiles * split_k (COLSUM: the one tile v0). gemm_pl4_kernel passes (blockIdx.x, gridDim.x); the grouped
 // kernel (gemm_group2_kernel) gives each of its two problems its own range of workgroups. vstep must be a multiple
 // of the XCD count so a virtual block stays on its workgroup's XCD (xcd_remap).
+// OVL (256x256 bf16 outputs, persistent, no split-K / bias gradient; FAN_GEMM_OVL): the tile transitions overlap.
+// The epilogue stages through a region of its own beside the operand stages (64-column halves, 17 KiB), so the next
+// tile's K-tiles 0 and 1 are fetched under the last k-step of this tile (its MFMAs read no fragments, the stages are
+// free after its barrier), and the next tile waits only for its K-tile 0 (vmcnt(G + kS): the epilogue's kS stores
+// are the youngest) and then for K-tile 1 with those stores still allowed in flight — vmcnt counts loads, stores and
+// LDS-DMA together, in issue order (MI355X_MICROARCH.md). Same arithmetic: bit-identical to OVL off.
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256>
+          int BM_ = 256, bool OVL = false>
 __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
                                         int64_t ldb, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                         const TC* __restrict__ aux, int64_t ldaux, int M, int N, int K, int split_k,
@@ -1150,6 +1168,13 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   // classifier forward reads a 64 MB activation straight from HBM inside the step: 76 vs 63 us from the MALL).
   constexpr int STAGES = BN == 128 ? 3 : 2;
   static_assert(RSP >= 1 && DSP >= 1 && G * DSP <= Q, "schedule");
+  static_assert(!OVL || (BM == 256 && BN == 256 && !COLSUM && !SPLIT && !ACCUM && sizeof(TC) == 2 &&
+                         !is_wire_epi(EPI) && !is_bits_epi(EPI)),
+                "overlapped transitions: 256x256 bf16 tiles without split-K or bias gradient");
+  constexpr int kSW = OVL ? 64 : WTN;                             // epilogue staging width
+  constexpr int kS = MI * (WTN / kSW) * (16 / (64 / (kSW / 8)));  // the epilogue's stores per wave and tile
+  constexpr int DSP2 = Q / (2 * G);                               // OVL: the next tile's two K-tiles in one k-step
+  static_assert(!OVL || (G + kS <= 63 && DSP2 >= 1), "vmcnt range / schedule");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
@@ -1163,7 +1188,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   // next tile starts its operand DMA while the previous tile's epilogue stores drain, instead of a new workgroup
   // waiting for the old one to retire (the 2-round grids: 8192x4096 forward and bwd-data). Not with the fused
   // bias gradient: its extra live registers would spill in the loop (the launcher gives it one tile per workgroup).
-  auto tile_body = [&](int v) __attribute__((always_inline)) {
+  auto tile_body = [&](int v, bool first, int vn) __attribute__((always_inline)) {
   const int wg = xcd_remap(v, tiles * split_k);
   const int tile = wg % tiles, ksplit = wg / tiles;
   const int GM = tiles_m >= 4 ? 4 : tiles_m;
@@ -1218,9 +1243,9 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   // MFMAs from the start (all issued by 3/4 of the block: the barrier's lgkmcnt(0) after k-step 0 then waits on
   // nothing young); DMA: the G pieces of K-tile dma_kt, one per DSP MFMAs.
   auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int rd_ks, int dma_kt,
-                   bool csk) __attribute__((always_inline)) {
+                   bool csk, auto next_c, bool next_on = false) __attribute__((always_inline)) {
     constexpr int cur = decltype(cur_c)::value;
-    constexpr bool READ = decltype(read_c)::value, DMA = decltype(dma_c)::value;
+    constexpr bool READ = decltype(read_c)::value, DMA = decltype(dma_c)::value, NEXT = decltype(next_c)::value;
     if (COLSUM && csk)
       static_for<NJ>([&](auto jc) __attribute__((always_inline)) { cs[jc.value] += frag_sum(fb[cur][jc.value]); });
     static_for<MI * NJ>([&](auto qc) __attribute__((always_inline)) {
@@ -1228,6 +1253,10 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
       if constexpr (READ && q % RSP == 0 && q / RSP < R) read_next(rd_st, rd_ks, cur ^ 1, q / RSP);
 #ifndef FAN_GEMM_NODMA  // diagnostic builds only: the main loop without its operand DMA (wrong results, timing)
       if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_kt, q / DSP);
+      // OVL: the next tile's K-tiles 0 and 1 (off[] already holds that tile's offsets)
+      if constexpr (NEXT && q % DSP2 == 0 && q / DSP2 < 2 * G) {
+        if (next_on) piece(q / DSP2 / G, q / DSP2 % G);
+      }
 #endif
       mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
     });
@@ -1238,12 +1267,19 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   using F_ = std::false_type;
 
   // prologue: K-tiles 0 and 1 in flight; retire 0 (this wave), barrier (every wave), read k-step (0, 0)
+  // (OVL after a transition: both were fetched by the previous tile's last k-step, before its epilogue's stores)
+  if (!OVL || first) {
 #pragma unroll
-  for (int p = 0; p < G; ++p) piece(0, p);
+    for (int p = 0; p < G; ++p) piece(0, p);
+  }
   if (nk > 1) {
+    if (!OVL || first) {
 #pragma unroll
-    for (int p = 0; p < G; ++p) piece(1, p);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      for (int p = 0; p < G; ++p) piece(1, p);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + kS) : "memory");
+    }
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -1256,24 +1292,48 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     const bool csk = do_colsum && kt >= cs0 && kt < cs1;
     FAN_STAMP(0);
     if constexpr (STAGES == 2) {
-      block(I0{}, T_{}, F_{}, st, 1, 0, csk);
+      constexpr bool kLast = OVL && !decltype(more_c)::value && !decltype(more2_c)::value;
+      if constexpr (kLast) {
+        // the last K-tile: this tile's offsets are dead (its last DMA went out two K-tiles ago); the next tile's
+        // (if any) take their place, for the DMA of its K-tiles 0 and 1 in k-step 1 below
+        if (vn >= 0) {
+          const int t1 = xcd_remap(vn, tiles);
+          const int g1 = t1 / (GM * tiles_n);
+          const int gm1 = (tiles_m - g1 * GM) < GM ? (tiles_m - g1 * GM) : GM;
+          const int i1 = t1 % (GM * tiles_n);
+          const int m1 = (g1 * GM + i1 % gm1) * BM, n1 = (i1 / gm1) * BN;
+#pragma unroll
+          for (int p = 0; p < GA; ++p) off[p] = piece_off<AK, BM, NT>(lda, m1, wave, lane, p);
+#pragma unroll
+          for (int p = GA; p < G; ++p) off[p] = piece_off<BKC, BN, NT>(ldb, n1, wave, lane, p - GA);
+        }
+      }
+      block(I0{}, T_{}, F_{}, st, 1, 0, csk, F_{});
       FAN_STAMP(1);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      // (OVL, first K-tile after a transition: K-tile 1 landed, the previous epilogue's stores may stay in flight)
+      if (OVL && kt == 0 && !first) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       FAN_STAMP(2);
       __builtin_amdgcn_s_barrier();
       FAN_STAMP(3);
-      block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk);
+      if constexpr (kLast) {
+        // fetch the next tile's first two K-tiles under this k-step's MFMAs (no fragment reads here: both stages
+        // are free once every wave passed the barrier above)
+        block(I1{}, F_{}, F_{}, smem, 0, 0, csk, T_{}, vn >= 0);
+      } else {
+        block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk, F_{});
+      }
     } else {
       // DMA of K-tile kt + 2 under k-step 0; the barrier then needs only K-tile kt + 1 (the G younger pieces of
       // kt + 2 may stay in flight)
-      block(I0{}, T_{}, more2_c, st, 1, kt + 2, csk);
+      block(I0{}, T_{}, more2_c, st, 1, kt + 2, csk, F_{});
       FAN_STAMP(1);
       if constexpr (decltype(more2_c)::value) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       FAN_STAMP(2);
       __builtin_amdgcn_s_barrier();
       FAN_STAMP(3);
-      block(I1{}, more_c, F_{}, smem + ((kt + 1) % 3) * STAGE, 0, 0, csk);
+      block(I1{}, more_c, F_{}, smem + ((kt + 1) % 3) * STAGE, 0, 0, csk, F_{});
     }
     FAN_STAMP(4);
   };
@@ -1292,33 +1352,43 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     colsum_finish<NJ, WTN, kEpiNone, true>(
         cs, lane, n0 + wn * WTN, ws + (SPLIT ? (int64_t)split_k * M * N + (int64_t)ksplit * N : (int64_t)im * N), wo,
         N);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every operand read retired before the epilogue reuses the LDS
-  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
-                                                 aux, ldaux, M, N, ksplit, ws, wo);
+  if constexpr (OVL) {
+    // staging rows of its own (wave-private) beside the operand stages: nothing to wait for (the operand reads
+    // retired before the last barrier; the next tile's DMA into the stages must stay in flight)
+    store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT, kSW>(acc, smem + 2 * STAGE, wave, lane, m0 + wm * WTM,
+                                                        n0 + wn * WTN, C, ldc, bias, aux, ldaux, M, N, ksplit, ws, wo);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every operand read retired before the epilogue reuses the LDS
+    store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
+                                                   aux, ldaux, M, N, ksplit, ws, wo);
+  }
   if constexpr (SPLIT && is_wire_epi(EPI)) {
     if (wo.fix) split_fixup<BM, BN>(tile, m0, n0, ws, split_k, reinterpret_cast<float*>(C), ldc, M, N, colsum, wo, smem);
   }
   };
   if constexpr (COLSUM) {
-    if (v0 < tiles * split_k) tile_body(v0);
+    if (v0 < tiles * split_k) tile_body(v0, true, -1);
   } else {
     for (int v = v0; v < tiles * split_k; v += vstep) {
-      tile_body(v);
-      __syncthreads();  // every wave's staging reads done before the next tile's DMA overwrites the LDS
+      tile_body(v, v == v0, v + vstep < tiles * split_k ? v + vstep : -1);
+      // every wave's staging reads done before the next tile's DMA overwrites the LDS (OVL: its own staging rows,
+      // and a barrier here would drain the next tile's DMA and this tile's stores)
+      if constexpr (!OVL) __syncthreads();
     }
   }
 }
 
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256>
+          int BM_ = 256, bool OVL = false>
 __global__ void __launch_bounds__(256, 1)
     gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
                     float* __restrict__ colsum, WireOut wo) {
-  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M, N, K, split_k,
-                                                           ws, colsum, wo, (int)blockIdx.x, (int)gridDim.x);
+  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_, OVL>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M, N, K,
+                                                                split_k, ws, colsum, wo, (int)blockIdx.x,
+                                                                (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1880,6 +1950,19 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
         if (fixed) *fixed = wf.fix != nullptr;
       };
       const bool half = gemm_half_stage_flag().load(std::memory_order_relaxed) != 0;
+      if constexpr (!SPLIT && !ACCUM && sizeof(TC) == 2 && !is_wire_epi(EPI) && !is_bits_epi(EPI)) {
+        // overlapped tile transitions (pl4_run OVL, opt-in)
+        if (gemm_ovl_flag().load(std::memory_order_relaxed) != 0 && !a.colsum && sk == 1 && !half &&
+            a.K >= 2 * BK) {  // (the last k-step fetches the next tile's K-tiles 0 AND 1)
+          constexpr int lds_o = 2 * (BM + BN) * BK * 2 + 4 * 16 * (64 + 4) * 4;
+          auto k = gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true>;
+          FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_o));
+          hipLaunchKernelGGL(k, persist_grid(grid), 256, lds_o, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B,
+                             a.ldb, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K,
+                             1, (float*)a.workspace, a.colsum, wo);
+          return 0;
+        }
+      }
       if constexpr (!SPLIT && !is_wire_epi(EPI)) {
         // two workgroups per CU on 256x128 tiles (gemm_pl2h_kernel, opt-in)
         if (gemm_occ2_flag().load(std::memory_order_relaxed) != 0 && !a.colsum && sk == 1 && a.K % 32 == 0) {

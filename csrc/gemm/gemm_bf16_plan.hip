@@ -41,6 +41,16 @@ std::atomic<int>& gemm_prio_flag() {
   return flag;
 }
 
+std::atomic<int>& gemm_ovl_flag() {
+  static std::atomic<int> flag{[] {
+    // default on: the flagship step 0.9868 / 0.9903 / 0.9921 vs 0.9946-1.0034 ms/step off, interleaved on one box
+    // (profiles/r5_gemm_ovl_ab.txt); bit-identical (tests/test_gpu_gemm_ovl.py)
+    const char* e = getenv("FAN_GEMM_OVL");
+    return e && e[0] == '0' ? 0 : 1;
+  }()};
+  return flag;
+}
+
 std::atomic<int>& gemm_occ2_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_OCC2");
