@@ -101,6 +101,9 @@ std::atomic<int>& gemm_prio_flag();
 // 256x256 bf16 plans on the persistent loop whose tile transitions overlap the epilogue with the next tile's first
 // K-tiles (pl4_run OVL; default on, FAN_GEMM_OVL=0, gemm_set_ovl)
 std::atomic<int>& gemm_ovl_flag();
+// with it: the accumulators transposed (MFMA operands swapped) and the bf16 epilogue stored straight from registers,
+// no LDS round trip (pl4_run TRN; FAN_GEMM_TRN, gemm_set_trn)
+std::atomic<int>& gemm_trn_flag();
 // split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
 // separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
 // gemm_set_fixup); bit-identical either way

@@ -1136,14 +1136,91 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
 // problem's tiles * split_k (COLSUM: the one tile v0). gemm_pl4_kernel passes (blockIdx.x, gridDim.x); the grouped
 // kernel (gemm_group2_kernel) gives each of its two problems its own range of workgroups. vstep must be a multiple
 // of the XCD count so a virtual block stays on its workgroup's XCD (xcd_remap).
+// Epilogue of a TRANSPOSED accumulator tile (pl4_run TRN: the MFMAs take B as their first operand, so each 16x16
+// block lands as C^T: lane l holds row l % 16, columns 4 (l / 16) .. +3), for bf16 outputs without an LDS round trip.
+// Per pair of 16-column blocks (j, j + 1) and 16-row block i: bias + ReLU in f32 (epi8_bf16's operations, in its
+// order), packed to bf16, then one v_permlane16_swap per dword exchanges rows 1 / 3 of block j's registers with rows
+// 0 / 2 of block j + 1's, after which every lane holds 8 consecutive columns of its row: one 16-B store (lanes of
+// row group g: columns (g & 1) * 16 + (g >> 1) * 8 of the pair). The ReLU mask zeroes bf16 halves (x * 0 rounds to
+// +0 either way). No staging, no LDS traffic, no waits: the wave's stores go out back to back.
+template <int MI, int NJ, int WTN, int EPI>
+__device__ __forceinline__ void store_tile_trn(const f32x4 (&acc)[MI][NJ], int lane, int row0, int col0,
+                                               bf16_t* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
+                                               const bf16_t* __restrict__ aux, int64_t ldaux) {
+  static_assert(NJ % 2 == 0, "pairs of 16-column blocks");
+  constexpr bool kBias = EPI == kEpiBias || EPI == kEpiBiasRelu;
+  constexpr bool kMask = EPI == kEpiReluMask;
+  const int g = lane >> 4, rl = lane & 15;
+  const int ocol = (g & 1) * 16 + (g >> 1) * 8;
+  auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
+  auto hi = [](uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); };
+  uint2 bq[kBias ? NJ : 1];
+  if constexpr (kBias) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bq[j] = *reinterpret_cast<const uint2*>(bias + col0 + j * 16 + 4 * g);
+  }
+  constexpr int kPfd = 2;
+  uint4 aq[kMask ? MI : 1][kMask ? NJ / 2 : 1];
+  auto aux_load = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+    for (int jp = 0; jp < NJ / 2; ++jp)
+      aq[i][jp] = *reinterpret_cast<const uint4*>(aux + (int64_t)(row0 + i * 16 + rl) * ldaux + col0 + jp * 32 + ocol);
+  };
+  if constexpr (kMask) {
+#pragma unroll
+    for (int i = 0; i < kPfd && i < MI; ++i) aux_load(i);
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    if constexpr (kMask) {
+      if (i + kPfd < MI) aux_load(i + kPfd);
+    }
+#pragma unroll
+    for (int jp = 0; jp < NJ / 2; ++jp) {
+      float x[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[h][r] = acc[i][2 * jp + h][r];
+        if constexpr (kBias) {
+          const uint2 u = bq[2 * jp + h];
+          x[h][0] += lo(u.x); x[h][1] += hi(u.x); x[h][2] += lo(u.y); x[h][3] += hi(u.y);
+        }
+        if constexpr (EPI == kEpiBiasRelu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[h][r] = fmaxf(x[h][r], 0.f);
+        }
+      }
+      uint32_t a0 = pack_bf16x2(x[0][0], x[0][1]), a1 = pack_bf16x2(x[0][2], x[0][3]);
+      uint32_t b0 = pack_bf16x2(x[1][0], x[1][1]), b1 = pack_bf16x2(x[1][2], x[1][3]);
+      const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      uint32_t w[4] = {s0[0], s1[0], s0[1], s1[1]};
+      if constexpr (kMask) {
+        const uint4 m = aq[i][jp];
+        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t keep_lo = lo(mw[k]) > 0.f ? 0x0000FFFFu : 0u, keep_hi = hi(mw[k]) > 0.f ? 0xFFFF0000u : 0u;
+          w[k] &= keep_lo | keep_hi;
+        }
+      }
+      *reinterpret_cast<uint4*>(C + (int64_t)(row0 + i * 16 + rl) * ldc + col0 + jp * 32 + ocol) =
+          make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
 // OVL (256x256 bf16 outputs, persistent, no split-K / bias gradient; FAN_GEMM_OVL): the tile transitions overlap.
 // The epilogue stages through a region of its own beside the operand stages (64-column halves, 17 KiB), so the next
 // tile's K-tiles 0 and 1 are fetched under the last k-step of this tile (its MFMAs read no fragments, the stages are
 // free after its barrier), and the next tile waits only for its K-tile 0 (vmcnt(G + kS): the epilogue's kS stores
 // are the youngest) and then for K-tile 1 with those stores still allowed in flight — vmcnt counts loads, stores and
 // LDS-DMA together, in issue order (MI355X_MICROARCH.md). Same arithmetic: bit-identical to OVL off.
+// TRN (with OVL): the MFMAs take B first, so the accumulators hold C^T blocks and the epilogue stores straight from
+// registers (store_tile_trn). The products and their k order are the same: bit-identical (tests/test_gpu_gemm_ovl.py).
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false>
+          int BM_ = 256, bool OVL = false, bool TRN = false>
 __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
                                         int64_t ldb, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                         const TC* __restrict__ aux, int64_t ldaux, int M, int N, int K, int split_k,
@@ -1175,6 +1252,9 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   constexpr int kS = MI * (WTN / kSW) * (16 / (64 / (kSW / 8)));  // the epilogue's stores per wave and tile
   constexpr int DSP2 = Q / (2 * G);                               // OVL: the next tile's two K-tiles in one k-step
   static_assert(!OVL || (G + kS <= 63 && DSP2 >= 1), "vmcnt range / schedule");
+  static_assert(!TRN || (OVL && (EPI == kEpiNone || EPI == kEpiBias || EPI == kEpiBiasRelu || EPI == kEpiReluMask)),
+                "transposed accumulators: the overlapped bf16 loop's plain / bias / ReLU / ReLU-mask epilogues");
+  static_assert(!TRN || kS == MI * NJ / 2, "one 16-B store per pair of 16-column blocks per 16-row block");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
@@ -1258,7 +1338,8 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
         if (next_on) piece(q / DSP2 / G, q / DSP2 % G);
       }
 #endif
-      mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
+      if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[cur][q % NJ], fa[cur][q / NJ]);
+      else mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
     });
   };
   using I0 = std::integral_constant<int, 0>;
@@ -1352,7 +1433,10 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     colsum_finish<NJ, WTN, kEpiNone, true>(
         cs, lane, n0 + wn * WTN, ws + (SPLIT ? (int64_t)split_k * M * N + (int64_t)ksplit * N : (int64_t)im * N), wo,
         N);
-  if constexpr (OVL) {
+  if constexpr (TRN) {
+    store_tile_trn<MI, NJ, WTN, EPI>(acc, lane, m0 + wm * WTM, n0 + wn * WTN, reinterpret_cast<bf16_t*>(C), ldc, bias,
+                                     reinterpret_cast<const bf16_t*>(aux), ldaux);
+  } else if constexpr (OVL) {
     // staging rows of its own (wave-private) beside the operand stages: nothing to wait for (the operand reads
     // retired before the last barrier; the next tile's DMA into the stages must stay in flight)
     store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT, kSW>(acc, smem + 2 * STAGE, wave, lane, m0 + wm * WTM,
@@ -1380,15 +1464,15 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 }
 
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false>
+          int BM_ = 256, bool OVL = false, bool TRN = false>
 __global__ void __launch_bounds__(256, 1)
     gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
                     float* __restrict__ colsum, WireOut wo) {
-  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_, OVL>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M, N, K,
-                                                                split_k, ws, colsum, wo, (int)blockIdx.x,
-                                                                (int)gridDim.x);
+  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_, OVL, TRN>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M, N,
+                                                                     K, split_k, ws, colsum, wo, (int)blockIdx.x,
+                                                                     (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1955,7 +2039,11 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
         if (gemm_ovl_flag().load(std::memory_order_relaxed) != 0 && !a.colsum && sk == 1 && !half &&
             a.K >= 2 * BK) {  // (the last k-step fetches the next tile's K-tiles 0 AND 1)
           constexpr int lds_o = 2 * (BM + BN) * BK * 2 + 4 * 16 * (64 + 4) * 4;
-          auto k = gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true>;
+          // (not with the ReLU-mask epilogue: its activation loads, 16 rows x 64 B per instruction in the
+          // transposed layout, measured slower than the staged 4 rows x 256 B: profiles/r5_gemm_trn_ab.txt)
+          const bool trn = gemm_trn_flag().load(std::memory_order_relaxed) != 0 && EPI != kEpiReluMask;
+          auto k = trn ? gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, true>
+                       : gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, false>;
           FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_o));
           hipLaunchKernelGGL(k, persist_grid(grid), 256, lds_o, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B,
                              a.ldb, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K,

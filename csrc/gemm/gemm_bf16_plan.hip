@@ -51,6 +51,14 @@ std::atomic<int>& gemm_ovl_flag() {
   return flag;
 }
 
+std::atomic<int>& gemm_trn_flag() {
+  static std::atomic<int> flag{[] {
+    const char* e = getenv("FAN_GEMM_TRN");
+    return e && e[0] == '1' ? 1 : 0;
+  }()};
+  return flag;
+}
+
 std::atomic<int>& gemm_occ2_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_OCC2");
