@@ -174,6 +174,10 @@ def run(argv=None, out=sys.stdout):
     sink.write(kind="mlp_mpi", sizes=sizes, global_mb=cfg.global_mb, world=world, iters=cfg.iters,
                s_per_iter=total / max(cfg.iters, 1), samples_per_s=cfg.global_mb * cfg.iters / total, loss=loss,
                config=cfg.to_dict())
+    if cfg.checkpoint:
+        # a sharded-update engine leaves each rank's master / momentum current only on the shards it owns: gather them
+        # first (collective, every rank; a no-op for the other engines)
+        trainer.gather_state()
     if cfg.checkpoint and rank == 0:
         checkpoint.save(cfg.checkpoint, model, iteration=start_iter + cfg.warmup + cfg.iters, dtype=cfg.dtype,
                         meta={"bn": a.bn, "bk": a.bk, "bc": a.bc, "world": world})
