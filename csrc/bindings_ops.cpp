@@ -313,6 +313,9 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_set_trn", [](int on) { gemm_trn_flag().store(on); },
         "overlapped 256x256 bf16 loop with transposed accumulators and the LDS-free epilogue (pl4_run TRN)");
   m.def("gemm_trn", []() { return gemm_trn_flag().load(); });
+  m.def("gemm_set_edma", [](int on) { gemm_edma_flag().store(on); },
+        "overlapped 256x256 loop with two barriers per K-tile and the operand DMA over both k-steps (pl4_run EDMA)");
+  m.def("gemm_edma", []() { return gemm_edma_flag().load(); });
   m.def("gemm_set_occ2", [](int on) { gemm_occ2_flag().store(on); },
         "unsplit 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)");
   m.def("gemm_occ2", []() { return gemm_occ2_flag().load(); });

@@ -104,6 +104,9 @@ std::atomic<int>& gemm_ovl_flag();
 // with it: the accumulators transposed (MFMA operands swapped) and the bf16 epilogue stored straight from registers,
 // no LDS round trip (pl4_run TRN; FAN_GEMM_TRN, gemm_set_trn)
 std::atomic<int>& gemm_trn_flag();
+// with it: two barriers per K-tile, the operand DMA spread over both k-steps (pl4_run EDMA; FAN_GEMM_EDMA,
+// gemm_set_edma)
+std::atomic<int>& gemm_edma_flag();
 // split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
 // separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
 // gemm_set_fixup); bit-identical either way

@@ -1219,8 +1219,31 @@ __device__ __forceinline__ void store_tile_trn(const f32x4 (&acc)[MI][NJ], int l
 // LDS-DMA together, in issue order (MI355X_MICROARCH.md). Same arithmetic: bit-identical to OVL off.
 // TRN (with OVL): the MFMAs take B first, so the accumulators hold C^T blocks and the epilogue stores straight from
 // registers (store_tile_trn). The products and their k order are the same: bit-identical (tests/test_gpu_gemm_ovl.py).
+// EDMA (with OVL, FAN_GEMM_EDMA): two barriers per K-tile instead of one, so the LDS-DMA of K-tile kt + 2 spreads over
+// most of both k-steps and each K-tile gets about twice the latency window. Barrier A, in k-step 0 once this wave's
+// reads of K-tile kt's k-step-1 fragments retired (lgkmcnt(0)), frees stage kt & 1 for that DMA; barrier B, in k-step
+// 1, waits (counted vmcnt: K-tile kt + 2's pieces issued so far may stay in flight) for K-tile kt + 1 and only then are
+// its k-step-0 fragments read, at a denser spacing. Without it the DMA waits for the single barrier between the
+// k-steps and all 16 pieces go out in k-step 1, the last ones 66 MFMAs before the next barrier needs them (the
+// library's hand-written gfx950 NT kernel splits its K-tile the same way, three barriers per K-tile). Same products,
+// same k order: bit-identical.
+#ifndef FAN_EDMA_RSP0
+#define FAN_EDMA_RSP0 2  // k-step 0: fragment-read spacing (MFMAs)
+#endif
+#ifndef FAN_EDMA_QA
+#define FAN_EDMA_QA 36  // k-step 0: barrier A before this MFMA
+#endif
+#ifndef FAN_EDMA_DSP
+#define FAN_EDMA_DSP 3  // DMA-piece spacing (MFMAs), from barrier A on
+#endif
+#ifndef FAN_EDMA_QB
+#define FAN_EDMA_QB 26  // k-step 1: barrier B before this MFMA
+#endif
+#ifndef FAN_EDMA_RSP1
+#define FAN_EDMA_RSP1 2  // k-step 1: fragment-read spacing after barrier B
+#endif
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false, bool TRN = false>
+          int BM_ = 256, bool OVL = false, bool TRN = false, bool EDMA = false>
 __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
                                         int64_t ldb, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                         const TC* __restrict__ aux, int64_t ldaux, int M, int N, int K, int split_k,
@@ -1255,6 +1278,20 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   static_assert(!TRN || (OVL && (EPI == kEpiNone || EPI == kEpiBias || EPI == kEpiBiasRelu || EPI == kEpiReluMask)),
                 "transposed accumulators: the overlapped bf16 loop's plain / bias / ReLU / ReLU-mask epilogues");
   static_assert(!TRN || kS == MI * NJ / 2, "one 16-B store per pair of 16-column blocks per 16-row block");
+  // EDMA: pieces 0 .. kE_P0 - 1 of K-tile kt + 2 go out in k-step 0 after barrier A, the rest in k-step 1 from MFMA 1;
+  // barrier B waits for all but the kE_NB pieces of kt + 2 issued before it
+  constexpr int kE_QA = FAN_EDMA_QA, kE_QB = FAN_EDMA_QB, kE_DSP = FAN_EDMA_DSP;
+  constexpr int kE_RSP0 = FAN_EDMA_RSP0, kE_RSP1 = FAN_EDMA_RSP1;
+  constexpr int kE_P0r = (Q - 2 - kE_QA) / kE_DSP + 1, kE_P0 = kE_P0r < G ? kE_P0r : G;
+  constexpr int kE_N1r = (kE_QB - 1 + kE_DSP - 1) / kE_DSP, kE_N1 = kE_N1r < G - kE_P0 ? kE_N1r : G - kE_P0;
+  constexpr int kE_NB = kE_P0 + kE_N1;
+  static_assert(!EDMA || (OVL && STAGES == 2), "EDMA: the overlapped 256x256 loop");
+  static_assert(!EDMA || (kE_QA + 1 + kE_DSP * (kE_P0 - 1) <= Q - 1 && (kE_P0 == G || kE_QA + 1 + kE_DSP * kE_P0 > Q - 1) &&
+                          (kE_P0 + kE_N1 == G || 1 + kE_DSP * kE_N1 >= kE_QB) && 1 + kE_DSP * (G - kE_P0 - 1) <= Q - 1),
+                "EDMA: every piece of K-tile kt + 2 is issued once, in one of the two k-steps");
+  static_assert(!EDMA || (kE_RSP0 * (R - 1) < kE_QA && kE_QA < Q && kE_QB >= 1 && kE_QB + kE_RSP1 * (R - 1) < Q &&
+                          kE_NB <= 63),
+                "EDMA schedule");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
@@ -1374,6 +1411,43 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     FAN_STAMP(0);
     if constexpr (STAGES == 2) {
       constexpr bool kLast = OVL && !decltype(more_c)::value && !decltype(more2_c)::value;
+      if constexpr (EDMA && !kLast) {
+        constexpr bool MORE = decltype(more_c)::value, MORE2 = decltype(more2_c)::value;
+        const char* st1 = smem + ((kt + 1) & 1) * STAGE;
+        // k-step 0 (set 0): K-tile kt's k-step-1 fragments into set 1; barrier A; K-tile kt + 2's first pieces
+        static_for<Q>([&](auto qc) __attribute__((always_inline)) {
+          constexpr int q = decltype(qc)::value;
+          if constexpr (q % kE_RSP0 == 0 && q / kE_RSP0 < R) read_next(st, 1, 1, q / kE_RSP0);
+          if constexpr (MORE2 && q == kE_QA) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+          }
+#ifndef FAN_GEMM_NODMA
+          if constexpr (MORE2 && q > kE_QA && (q - kE_QA - 1) % kE_DSP == 0 && (q - kE_QA - 1) / kE_DSP < kE_P0)
+            piece(kt + 2, (q - kE_QA - 1) / kE_DSP);
+#endif
+          if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[0][q % NJ], fa[0][q / NJ]);
+          else mfma_acc(acc[q / NJ][q % NJ], fa[0][q / NJ], fb[0][q % NJ]);
+        });
+        // k-step 1 (set 1): the rest of K-tile kt + 2; barrier B (K-tile kt + 1 landed in every wave); its k-step-0
+        // fragments into set 0
+        static_for<Q>([&](auto qc) __attribute__((always_inline)) {
+          constexpr int q = decltype(qc)::value;
+#ifndef FAN_GEMM_NODMA
+          if constexpr (MORE2 && q >= 1 && (q - 1) % kE_DSP == 0 && kE_P0 + (q - 1) / kE_DSP < G)
+            piece(kt + 2, kE_P0 + (q - 1) / kE_DSP);
+#endif
+          if constexpr (MORE && q == kE_QB) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MORE2 ? kE_NB : 0) : "memory");
+            __builtin_amdgcn_s_barrier();
+          }
+          if constexpr (MORE && q >= kE_QB && (q - kE_QB) % kE_RSP1 == 0 && (q - kE_QB) / kE_RSP1 < R)
+            read_next(st1, 0, 0, (q - kE_QB) / kE_RSP1);
+          if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[1][q % NJ], fa[1][q / NJ]);
+          else mfma_acc(acc[q / NJ][q % NJ], fa[1][q / NJ], fb[1][q % NJ]);
+        });
+        return;
+      }
       if constexpr (kLast) {
         // the last K-tile: this tile's offsets are dead (its last DMA went out two K-tiles ago); the next tile's
         // (if any) take their place, for the DMA of its K-tiles 0 and 1 in k-step 1 below
@@ -1464,15 +1538,15 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 }
 
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false, bool TRN = false>
+          int BM_ = 256, bool OVL = false, bool TRN = false, bool EDMA = false>
 __global__ void __launch_bounds__(256, 1)
     gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
                     float* __restrict__ colsum, WireOut wo) {
-  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_, OVL, TRN>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M, N,
-                                                                     K, split_k, ws, colsum, wo, (int)blockIdx.x,
-                                                                     (int)gridDim.x);
+  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_, OVL, TRN, EDMA>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M,
+                                                                           N, K, split_k, ws, colsum, wo,
+                                                                           (int)blockIdx.x, (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -2042,8 +2116,10 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
           // (not with the ReLU-mask epilogue: its activation loads, 16 rows x 64 B per instruction in the
           // transposed layout, measured slower than the staged 4 rows x 256 B: profiles/r5_gemm_trn_ab.txt)
           const bool trn = gemm_trn_flag().load(std::memory_order_relaxed) != 0 && EPI != kEpiReluMask;
+          const bool edma = gemm_edma_flag().load(std::memory_order_relaxed) != 0;
           auto k = trn ? gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, true>
-                       : gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, false>;
+                       : edma ? gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, false, true>
+                              : gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, false>;
           FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_o));
           hipLaunchKernelGGL(k, persist_grid(grid), 256, lds_o, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B,
                              a.ldb, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K,

@@ -59,6 +59,14 @@ std::atomic<int>& gemm_trn_flag() {
   return flag;
 }
 
+std::atomic<int>& gemm_edma_flag() {
+  static std::atomic<int> flag{[] {
+    const char* e = getenv("FAN_GEMM_EDMA");
+    return e && e[0] == '1' ? 1 : 0;
+  }()};
+  return flag;
+}
+
 std::atomic<int>& gemm_occ2_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_OCC2");
