@@ -29,3 +29,14 @@ def C():
     from fpga_ai_nic_amd import _ext
 
     return _ext.require()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _release_process_group():
+    """A test that initialised torch.distributed in this process (a 1-rank group) leaves it up for the others; tear
+    it down once at the end of the session instead of leaving that to interpreter exit."""
+    yield
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
