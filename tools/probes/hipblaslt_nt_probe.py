@@ -30,7 +30,9 @@ def main():
     Bt = ((torch.rand(N, K, device="cuda") * 2 - 1)).to(torch.bfloat16)
     B = Bt.t().contiguous()
     Cb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    aux = (torch.rand(M, N, device="cuda") - 0.5).to(torch.bfloat16)
     arms = {"pl4_nt": lambda: G.gemm(A, False, Bt, True, Cb, G.EPI_NONE),
+            "pl4_nt_mask": lambda: G.gemm(A, False, Bt, True, Cb, G.EPI_RELU_MASK, aux=aux),
             "pl4_nn": lambda: G.gemm(A, False, B, False, Cb, G.EPI_NONE),
             "lib_nt": lambda: torch.matmul(A, Bt.t()),
             "lib_nn": lambda: torch.matmul(A, B)}
