@@ -913,17 +913,14 @@ __global__ void __launch_bounds__(WM * WN * 64, WM * WN / 4)
 //     retired its reads of it before the barrier), one piece per 4 MFMAs.
 // The DMA of a K-tile thus has two k-steps of MFMAs to land. LDS: 2 stages x 64 KiB. Glds with SGPR bases + 32-bit
 // lane offsets computed once. Aligned shapes only (M, N % 256, K % (64 * split_k)); every layout and epilogue.
+// M0 is written in the statement that reads it and not restored (cdna_hip_programming.md §5.7's clobbering form): the
+// compiler emits no M0 access of its own in any kernel of this library (every M0 read or write in the built code
+// objects is one of these statements' s_mov_b32 m0 / global_load_lds), and saving / restoring it cost 2 of the 3 SALU
+// instructions per 1 KiB piece — the flagship step measured 1.0 % faster without them, 3 of 3 interleaved pairs
+// (profiles/r5_glds_m0_ab.txt).
 __device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds_addr)
-      : "memory");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_addr)
+               : "memory");
 }
 
 // Byte offset (from the operand's K-tile origin) of this lane's chunk of glds instruction i: stage_one's address

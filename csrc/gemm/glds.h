@@ -8,18 +8,10 @@ namespace fan {
 // Issued from inline asm so hipcc does not track it: otherwise its waitcnt pass conservatively inserts
 // s_waitcnt vmcnt(0) in front of LDS fragment reads (observed in front of ds_read_b64_tr_b16), draining the
 // prefetch every K-tile. Completion is counted by hand with s_waitcnt vmcnt(N) + a raw s_barrier.
-// M0 is set and restored inside the same statement (cdna_hip_programming.md §5.7).
+// M0 is set inside the same statement and not restored (cdna_hip_programming.md §5.7's clobbering form; the compiler
+// emits no M0 access of its own in these kernels: see glds16_s in gemm_bf16_kernel.h).
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_addr)
-      : "memory");
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds_addr) : "memory");
 }
 
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {

@@ -9,6 +9,8 @@ import sys
 so, script = sys.argv[1], sys.argv[2]
 sys.argv = [script] + sys.argv[3:]
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402,F401  (first, as fpga_ai_nic_amd/_ext.py does: the extension must bind torch's HIP runtime)
+
 spec = importlib.util.spec_from_file_location("fpga_ai_nic_amd._C", so)
 mod = importlib.util.module_from_spec(spec)
 sys.modules["fpga_ai_nic_amd._C"] = mod
