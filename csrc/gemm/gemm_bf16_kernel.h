@@ -923,6 +923,15 @@ __device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint3
                : "memory");
 }
 
+// The same with the LDS destination as a wave-uniform base + a compile-time byte offset, added into M0 by the
+// statement itself (1 SALU per piece instead of the compiler's add + the move).
+template <uint32_t OFF>
+__device__ __forceinline__ void glds16_si(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase),
+               "s"(lds_base), "i"(OFF)
+               : "memory", "scc");
+}
+
 // Byte offset (from the operand's K-tile origin) of this lane's chunk of glds instruction i: stage_one's address
 // math without the base pointer.
 template <bool KCONTIG, int OUTER, int NT>
@@ -1343,10 +1352,11 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 
   // glds piece p (0..G-1) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
   // the accumulator array in scratch memory)
-  auto piece = [&](int kt, int p) __attribute__((always_inline)) {
+  auto piece = [&](int kt, auto pc) __attribute__((always_inline)) {
+    constexpr int p = decltype(pc)::value;
     const uint32_t st = lds0 + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE + wave * 1024;
-    if (p < GA) glds16_s(a_k0 + kt * a_step, off[p], st + p * OpTile<BM, NT>::IB);
-    else glds16_s(b_k0 + kt * b_step, off[p], st + A_BYTES + (p - GA) * OpTile<BN, NT>::IB);
+    if constexpr (p < GA) glds16_si<p * OpTile<BM, NT>::IB>(a_k0 + kt * a_step, off[p], st);
+    else glds16_si<A_BYTES + (p - GA) * OpTile<BN, NT>::IB>(b_k0 + kt * b_step, off[p], st);
   };
   // next k-step's fragment r (0..R-1: A rows 0..7, then B columns 0..NJ-1) into set `set`
   auto read_next = [&](const char* st, int ks, int set, int r) __attribute__((always_inline)) {
@@ -1366,10 +1376,10 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
       constexpr int q = decltype(qc)::value;
       if constexpr (READ && q % RSP == 0 && q / RSP < R) read_next(rd_st, rd_ks, cur ^ 1, q / RSP);
 #ifndef FAN_GEMM_NODMA  // diagnostic builds only: the main loop without its operand DMA (wrong results, timing)
-      if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_kt, q / DSP);
+      if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_kt, std::integral_constant<int, q / DSP>{});
       // OVL: the next tile's K-tiles 0 and 1 (off[] already holds that tile's offsets)
       if constexpr (NEXT && q % DSP2 == 0 && q / DSP2 < 2 * G) {
-        if (next_on) piece(q / DSP2 / G, q / DSP2 % G);
+        if (next_on) piece(q / DSP2 / G, std::integral_constant<int, q / DSP2 % G>{});
       }
 #endif
       if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[cur][q % NJ], fa[cur][q / NJ]);
@@ -1383,14 +1393,10 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 
   // prologue: K-tiles 0 and 1 in flight; retire 0 (this wave), barrier (every wave), read k-step (0, 0)
   // (OVL after a transition: both were fetched by the previous tile's last k-step, before its epilogue's stores)
-  if (!OVL || first) {
-#pragma unroll
-    for (int p = 0; p < G; ++p) piece(0, p);
-  }
+  if (!OVL || first) static_for<G>([&](auto pc) __attribute__((always_inline)) { piece(0, pc); });
   if (nk > 1) {
     if (!OVL || first) {
-#pragma unroll
-      for (int p = 0; p < G; ++p) piece(1, p);
+      static_for<G>([&](auto pc) __attribute__((always_inline)) { piece(1, pc); });
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + kS) : "memory");
@@ -1421,7 +1427,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
           }
 #ifndef FAN_GEMM_NODMA
           if constexpr (MORE2 && q > kE_QA && (q - kE_QA - 1) % kE_DSP == 0 && (q - kE_QA - 1) / kE_DSP < kE_P0)
-            piece(kt + 2, (q - kE_QA - 1) / kE_DSP);
+            piece(kt + 2, std::integral_constant<int, (q - kE_QA - 1) / kE_DSP>{});
 #endif
           if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[0][q % NJ], fa[0][q / NJ]);
           else mfma_acc(acc[q / NJ][q % NJ], fa[0][q / NJ], fb[0][q % NJ]);
@@ -1432,7 +1438,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
           constexpr int q = decltype(qc)::value;
 #ifndef FAN_GEMM_NODMA
           if constexpr (MORE2 && q >= 1 && (q - 1) % kE_DSP == 0 && kE_P0 + (q - 1) / kE_DSP < G)
-            piece(kt + 2, kE_P0 + (q - 1) / kE_DSP);
+            piece(kt + 2, std::integral_constant<int, kE_P0 + (q - 1) / kE_DSP>{});
 #endif
           if constexpr (MORE && q == kE_QB) {
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MORE2 ? kE_NB : 0) : "memory");
