@@ -932,6 +932,22 @@ __device__ __forceinline__ void glds16_si(const void* sbase, uint32_t voff, uint
                : "memory", "scc");
 }
 
+// s_waitcnt vmcnt(VM) lgkmcnt(LGKM) through the compiler's builtin, so that its own wait insertion knows what the wait
+// leaves outstanding: after an asm wait (opaque to it) it re-waits, lgkmcnt(N) by lgkmcnt(N), in front of the first use
+// of every fragment read already complete — ~16 extra s_waitcnt per K-tile of the 4-wave loop. The empty asm keeps
+// the LDS reads after it from being hoisted above it (the asm form's "memory" clobber). FAN_GEMM_ASM_WAITS (diagnostic
+// builds): the asm form.
+template <int VM, int LGKM>
+__device__ __forceinline__ void waitcnt_known() {
+  static_assert(VM >= 0 && VM <= 63 && LGKM >= 0 && LGKM <= 15, "s_waitcnt field ranges");
+#ifdef FAN_GEMM_ASM_WAITS
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(%1)" ::"n"(VM), "n"(LGKM) : "memory");
+#else
+  __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (LGKM << 8) | ((VM >> 4) << 14));
+  asm volatile("" ::: "memory");
+#endif
+}
+
 // Byte offset (from the operand's K-tile origin) of this lane's chunk of glds instruction i: stage_one's address
 // math without the base pointer.
 template <bool KCONTIG, int OUTER, int NT>
@@ -1469,8 +1485,8 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
       block(I0{}, T_{}, F_{}, st, 1, 0, csk, F_{});
       FAN_STAMP(1);
       // (OVL, first K-tile after a transition: K-tile 1 landed, the previous epilogue's stores may stay in flight)
-      if (OVL && kt == 0 && !first) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (OVL && kt == 0 && !first) waitcnt_known<kS, 0>();
+      else waitcnt_known<0, 0>();
       FAN_STAMP(2);
       __builtin_amdgcn_s_barrier();
       FAN_STAMP(3);
@@ -1480,18 +1496,22 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
         block(I1{}, F_{}, F_{}, smem, 0, 0, csk, T_{}, vn >= 0);
       } else {
         block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk, F_{});
+        // the next K-tile's k-step-0 fragments (read above, long complete): one wait here instead of the compiler's
+        // per-fragment ones in front of the next k-step's MFMAs
+        if constexpr (decltype(more_c)::value) waitcnt_known<63, 0>();
       }
     } else {
       // DMA of K-tile kt + 2 under k-step 0; the barrier then needs only K-tile kt + 1 (the G younger pieces of
       // kt + 2 may stay in flight)
       block(I0{}, T_{}, more2_c, st, 1, kt + 2, csk, F_{});
       FAN_STAMP(1);
-      if constexpr (decltype(more2_c)::value) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if constexpr (decltype(more2_c)::value) waitcnt_known<G, 0>();
+      else waitcnt_known<0, 0>();
       FAN_STAMP(2);
       __builtin_amdgcn_s_barrier();
       FAN_STAMP(3);
       block(I1{}, more_c, F_{}, smem + ((kt + 1) % 3) * STAGE, 0, 0, csk, F_{});
+      if constexpr (decltype(more_c)::value) waitcnt_known<63, 0>();
     }
     FAN_STAMP(4);
   };
