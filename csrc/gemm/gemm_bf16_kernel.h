@@ -1277,7 +1277,10 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   constexpr int GA = OpTile<BM, NT>::GLDS, G = GA + OpTile<BN, NT>::GLDS;  // 8 + 8 (BN 128: 8 + 4; BM 224: 7 + 4)
   constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NJ = WTN / 16;
   constexpr int Q = MI * NJ, R = MI + NJ;  // MFMAs and fragment reads per k-step and wave
-  constexpr int RSP = (Q * 3 / 4) / R, DSP = Q / G;  // read / DMA spacing in MFMAs (64 MFMAs: 3 / 4; 32: 2 / 2)
+#ifndef FAN_GEMM_RSP_Q4
+#define FAN_GEMM_RSP_Q4 3  // diagnostic builds: the fragment reads span this many quarters of a k-step
+#endif
+  constexpr int RSP = (Q * FAN_GEMM_RSP_Q4 / 4) / R, DSP = Q / G;  // read / DMA spacing in MFMAs (64 MFMAs: 3 / 4)
   static_assert(BN == 256 || BN == 128, "256x256 or 256x128 tiles");
   // 224x128 tiles: 1792 rows (the reference's per-rank batch, sw/run.sh:16) are 8 row tiles, so a 1792 x 4096 output
   // is 8 x 32 = 256 workgroups, one per CU (256-row tiles give 7 x 32 = 224 and leave 32 CUs idle). The A image is
