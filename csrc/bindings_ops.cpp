@@ -316,6 +316,9 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_set_edma", [](int on) { gemm_edma_flag().store(on); },
         "overlapped 256x256 loop with two barriers per K-tile and the operand DMA over both k-steps (pl4_run EDMA)");
   m.def("gemm_edma", []() { return gemm_edma_flag().load(); });
+  m.def("gemm_set_reduce4", [](int on) { gemm_reduce4_flag().store(on); },
+        "split-K wire / fused-update reduce: 4 values per lane (1) or one 16-value group per lane (0)");
+  m.def("gemm_reduce4", []() { return gemm_reduce4_flag().load(); });
   m.def("gemm_set_occ2", [](int on) { gemm_occ2_flag().store(on); },
         "unsplit 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)");
   m.def("gemm_occ2", []() { return gemm_occ2_flag().load(); });

@@ -107,6 +107,9 @@ std::atomic<int>& gemm_trn_flag();
 // with it: two barriers per K-tile, the operand DMA spread over both k-steps (pl4_run EDMA; FAN_GEMM_EDMA,
 // gemm_set_edma)
 std::atomic<int>& gemm_edma_flag();
+// split-K wire / fused-update reduce: lane-contiguous form, 4 values per lane (1, default) or one 16-value group per
+// lane (0) (FAN_GEMM_REDUCE4, gemm_set_reduce4); bit-identical either way
+std::atomic<int>& gemm_reduce4_flag();
 // split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
 // separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
 // gemm_set_fixup); bit-identical either way

@@ -2016,6 +2016,94 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// The fused update of 4 values of a group (flat index f, f % 4 == 0; shared exponent E): local_update16's operations
+// on a quarter of the group.
+__device__ __forceinline__ void local_update4(float v[4], uint32_t E, uint32_t f, const WireOut& wo) {
+  float4 a = *reinterpret_cast<const float4*>(wo.um + f);
+  float w[4] = {a.x, a.y, a.z, a.w}, m[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool hm = wo.umom != nullptr;
+  if (hm) {
+    const float4 b = *reinterpret_cast<const float4*>(wo.umom + f);
+    m[0] = b.x; m[1] = b.y; m[2] = b.z; m[3] = b.w;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) sgd_apply(wire_roundtrip_rne(v[u], E), w[u], m[u], hm, wo.up);
+  *reinterpret_cast<float4*>(wo.um + f) = make_float4(w[0], w[1], w[2], w[3]);
+  if (hm) *reinterpret_cast<float4*>(wo.umom + f) = make_float4(m[0], m[1], m[2], m[3]);
+  if (wo.ulp) *reinterpret_cast<uint2*>(wo.ulp + f) = make_uint2(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]));
+}
+
+// splitk_reduce_wire_kernel, lane-contiguous: each lane sums and finishes 4 consecutive values (one float4 per slab),
+// 4 lanes a 16-column group, so every load and store of a wave covers 1 KiB contiguous (one lane per group strides
+// 64 B per lane). The group's shared exponent is the max over its 4 lanes (quad xor shuffles: exact), and every
+// value is summed in split order, encoded, rounded and updated as there: bit-identical. The bias partials (colsum)
+// are reduced per 16-column group after the loop, as there. (M * N / 4 is a multiple of 4 — N % 16 == 0 — and the
+// grid's thread count too, so a quad's lanes are always all in or all out of range.)
+template <bool UPD, int SK = 0>
+__global__ void __launch_bounds__(256)
+    splitk_reduce_wire4_kernel(const float* __restrict__ ws, int split_k, float* __restrict__ C, int64_t ldc, int M,
+                               int N, float* __restrict__ colsum, WireOut wo) {
+  if constexpr (SK > 0) split_k = SK;
+  const int64_t slab = (int64_t)M * N, quads = slab / 4;
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q = t0; q < quads; q += step) {
+    const int64_t e = q * 4;
+    const int row = (int)(e / N), col = (int)(e % N);
+    float4 a = *reinterpret_cast<const float4*>(ws + e);
+#pragma unroll
+    for (int k = 1; k < (SK > 0 ? SK : split_k); ++k) {
+      const float4 b = *reinterpret_cast<const float4*>(ws + k * slab + e);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+    uint32_t mx = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) mx = max(mx, __float_as_uint(v[u]) & 0x7FFFFFFFu);
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, 1));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, 2));
+    const uint32_t E = mx >> 23;
+    const uint32_t loc = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
+    if constexpr (UPD) {
+      local_update4(v, E, wo.off + loc, wo);
+    } else {
+      const int sub = (col & 15) >> 2;
+      const uint32_t fg = wo.off + loc - 4u * (uint32_t)sub;  // the group's flat index
+      const int sh = wire_shard_of(fg, wo);
+      const uint32_t pos = fg - (uint32_t)sh * (uint32_t)wo.shard;
+      uint32_t w = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w |= ((uint32_t)wire_encode(v[u], E, wo.codec) & 0xFFu) << (8 * u);
+      uint8_t* base = wire_shard_base(sh, wo);
+      *reinterpret_cast<uint32_t*>(base + pos + 4 * sub) = w;
+      if (sub == 0) base[wo.shard + pos / 16] = (uint8_t)E;
+      if (wo.own == kWireOwnAll || (wo.period > 0 ? sh % wo.period : sh) == wo.own)
+        *reinterpret_cast<float4*>(C + loc) = a;
+    }
+  }
+  if (colsum) {
+    for (int64_t g = t0; g < N / 16; g += step) {
+      const int col = (int)g * 16;
+      const float* p = ws + (int64_t)split_k * slab + col;
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; u += 4) {
+        const float4 b = *reinterpret_cast<const float4*>(p + u);
+        v[u] = b.x; v[u + 1] = b.y; v[u + 2] = b.z; v[u + 3] = b.w;
+      }
+      for (int k = 1; k < split_k; ++k) {
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+          const float4 b = *reinterpret_cast<const float4*>(p + (int64_t)k * N + u);
+          v[u] += b.x; v[u + 1] += b.y; v[u + 2] += b.z; v[u + 3] += b.w;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) colsum[col + u] = v[u];
+      if (wo.bias_off > 0) wire_store16<UPD>(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
+    }
+  }
+}
+
 // Ordered reduce of bias-gradient partial slabs part[p * N + n], p < parts, into colsum[n]; WIRE: also encodes the
 // bias segment of the [W | b] bucket (flat wo.bias_off + n). One block per 64 columns: 16 lanes x float4 columns by
 // 16 part classes (p % 16), each summed in p order, then the classes summed in class order (deterministic).
@@ -2323,9 +2411,16 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     if constexpr (is_wire_epi(EPI)) {
       if (fixed) return;
       const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
+      const bool lane4 = gemm_reduce4_flag().load(std::memory_order_relaxed) != 0;
       with_split_count(sk, [&](auto skc) {
-        hipLaunchKernelGGL((splitk_reduce_wire_kernel<EPI == kEpiWireUpd, decltype(skc)::value>), stream_grid(items),
-                           256, 0, s, (const float*)a.workspace, sk, (float*)a.C, a.ldc, a.M, a.N, a.colsum, wo);
+        if (lane4)
+          hipLaunchKernelGGL((splitk_reduce_wire4_kernel<EPI == kEpiWireUpd, decltype(skc)::value>),
+                             stream_grid((size_t)a.M * a.N / 4), 256, 0, s, (const float*)a.workspace, sk, (float*)a.C,
+                             a.ldc, a.M, a.N, a.colsum, wo);
+        else
+          hipLaunchKernelGGL((splitk_reduce_wire_kernel<EPI == kEpiWireUpd, decltype(skc)::value>),
+                             stream_grid(items), 256, 0, s, (const float*)a.workspace, sk, (float*)a.C, a.ldc, a.M,
+                             a.N, a.colsum, wo);
       });
     } else {
       with_split_count(sk, [&](auto skc) {

@@ -67,6 +67,14 @@ std::atomic<int>& gemm_edma_flag() {
   return flag;
 }
 
+std::atomic<int>& gemm_reduce4_flag() {
+  static std::atomic<int> flag{[] {
+    const char* e = getenv("FAN_GEMM_REDUCE4");
+    return e && e[0] == '0' ? 0 : 1;
+  }()};
+  return flag;
+}
+
 std::atomic<int>& gemm_occ2_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_OCC2");

@@ -125,3 +125,41 @@ def test_fixup_training_bit_identical(C):
         gemm_tune.reset()
     for a, b in zip(*weights):
         assert torch.equal(a, b)
+
+
+@pytest.fixture
+def R4():
+    from fpga_ai_nic_amd import _ext
+
+    C = _ext.require()
+    saved, fix = C.gemm_reduce4(), C.gemm_fixup()
+    C.gemm_set_fixup(0)
+    yield C
+    C.gemm_set_reduce4(saved)
+    C.gemm_set_fixup(fix)
+
+
+@pytest.mark.parametrize("sk,tile", [(2, (256, 256)), (4, (256, 256)), (3, (256, 256)), (4, (256, 128))])
+@pytest.mark.parametrize("bias", [True, False])
+@pytest.mark.parametrize("codec,own", [("bfp_rne", 1), ("bfp_trunc", 0), ("bfp_rne", -2)])
+def test_reduce4_wire_bit_identical(R4, sk, tile, bias, codec, own):
+    """The lane-contiguous split-K reduce (4 values per lane, the group exponent from quad shuffles;
+    FAN_GEMM_REDUCE4 / gemm_set_reduce4) against the one-group-per-lane kernel: the same bits in every output
+    (own -2: every shard's f32 copy)."""
+    run = _wire_call(1024, 1024, 1536, sk, tile, codec, nsh=3, own=own, bias=bias, seed=sk * 5 + bias)
+    R4.gemm_set_reduce4(0)
+    ref = run()
+    R4.gemm_set_reduce4(1)
+    _same(ref, run())
+
+
+@pytest.mark.parametrize("opt", [dict(lr=0.05), dict(lr=0.02, momentum=0.9, weight_decay=1e-3),
+                                 dict(lr=0.02, momentum=0.9, nesterov=True)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_reduce4_fused_update_bit_identical(R4, opt, bias):
+    """The flagship's 1024x4096 bwd-weight with the update fused into the reduce."""
+    run = _wire_call(1024, 4096, 8192, 4, (256, 256), "bfp_rne", nsh=1, own=-1, bias=bias, seed=13, upd_opt=opt)
+    R4.gemm_set_reduce4(0)
+    ref = run()
+    R4.gemm_set_reduce4(1)
+    _same(ref, run())
