@@ -320,5 +320,9 @@ void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t
 void launch_wire_reduce_sgd(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots,
                             int self_pos, const void* local, float* master, float* mom, SgdParams p, size_t n_valid,
                             const WirePtrs& dst, int n_dst, size_t n_s, bool peers, hipStream_t stream);
+// BFP codecs: the lane-contiguous form of that kernel, 4 values per lane (1, default) or one 16-value group per lane
+// (0) (FAN_WIRE_REDUCE4); bit-identical either way
+void set_wire_reduce4(int on);
+int wire_reduce4();
 
 }  // namespace fan

@@ -265,6 +265,87 @@ __global__ void __launch_bounds__(kBlock)
   if (rel >= 0) p2p_release(rel);
 }
 
+// wire_reduce_sgd_kernel for the BFP codecs, lane-contiguous: 4 consecutive values per lane, 4 lanes a 16-value group
+// (the group's exponent for the codec round trip from quad xor shuffles: exact), so every load and store of a wave
+// covers contiguous bytes instead of striding a group per lane — the same sums in slot order, the same round trip and
+// SGD per value: bit-identical (FAN_WIRE_REDUCE4, default on). n_s is a multiple of 16 and the grid's thread count a
+// multiple of 4, so a quad's lanes are always all in or all out of range.
+template <typename TL, int C, bool HAS_MOM>
+__global__ void __launch_bounds__(kBlock)
+    wire_reduce_sgd4_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
+                            const TL* __restrict__ local, float* __restrict__ master, float* __restrict__ mom,
+                            SgdParams p, size_t n_valid, WirePtrs dst, int n_dst, size_t n_s, int rel) {
+  static_assert(C == kBfpTrunc || C == kBfpRne, "BFP codecs");
+  const size_t tasks = n_s >> 2;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+    const size_t le = t << 2;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < n_slots; ++r) {
+      float v[4];
+      if (r == self_pos) {
+        if constexpr (sizeof(TL) == 4) {
+          const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(local) + le);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        } else {
+          const uint2 a = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(local) + le);
+          v[0] = __uint_as_float(a.x << 16); v[1] = __uint_as_float(a.x & 0xFFFF0000u);
+          v[2] = __uint_as_float(a.y << 16); v[3] = __uint_as_float(a.y & 0xFFFF0000u);
+        }
+      } else {
+        const uint8_t* sh = slots + (size_t)r * slot_stride;
+        const uint32_t m = *reinterpret_cast<const uint32_t*>(sh + le);
+        const uint32_t E = sh[n_s + (le >> 4)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int32_t q = (int32_t)(int8_t)(uint8_t)(m >> (8 * j));
+          v[j] = (C == kBfpTrunc) ? bfp_decode_trunc(q, E) : bfp_decode_rne(q, E);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += v[j];
+    }
+    // codec_roundtrip16 on the quad's group
+    uint32_t mx = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mx = max(mx, __float_as_uint(acc[j]) & 0x7FFFFFFFu);
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, 1));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, 2));
+    const uint32_t E = mx >> 23;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t q = (C == kBfpTrunc) ? bfp_encode_trunc(__float_as_uint(acc[j]), E) : bfp_encode_rne(acc[j], E);
+      const int32_t q8 = (int32_t)(int8_t)(uint8_t)((uint32_t)q & 0xFFu);
+      acc[j] = (C == kBfpTrunc) ? bfp_decode_trunc(q8, E) : bfp_decode_rne(q8, E);
+    }
+    float4 wv = *reinterpret_cast<const float4*>(master + le);
+    float w[4] = {wv.x, wv.y, wv.z, wv.w}, m[4] = {0.f, 0.f, 0.f, 0.f};
+    if (HAS_MOM) {
+      const float4 mv = *reinterpret_cast<const float4*>(mom + le);
+      m[0] = mv.x; m[1] = mv.y; m[2] = mv.z; m[3] = mv.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // wire_sgd_kernel's operations, in its order
+      if (le + j >= n_valid) continue;
+      float gj = acc[j] * p.grad_scale;
+      if (p.weight_decay != 0.0f) gj = fmaf(p.weight_decay, w[j], gj);
+      if (HAS_MOM) {
+        m[j] = fmaf(p.momentum, m[j], gj);
+        gj = p.nesterov ? fmaf(p.momentum, m[j], gj) : m[j];
+      }
+      w[j] = fmaf(-p.lr, gj, w[j]);
+    }
+    if (le < n_valid) {
+      *reinterpret_cast<float4*>(master + le) = make_float4(w[0], w[1], w[2], w[3]);
+      if (HAS_MOM) *reinterpret_cast<float4*>(mom + le) = make_float4(m[0], m[1], m[2], m[3]);
+    }
+    const uint2 lp = make_uint2(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]));
+    for (int i = 0; i < n_dst; ++i)
+      if (dst.p[i] != nullptr) *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(dst.p[i]) + le) = lp;
+  }
+  if (rel >= 0) p2p_release(rel);
+}
+
 template <typename TOUT, int C>
 __global__ void __launch_bounds__(kBlock) wire_unpack_strided_kernel(const uint8_t* __restrict__ in,
                                                                     size_t shard_stride, TOUT* __restrict__ out,
@@ -507,12 +588,42 @@ void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t
   FAN_HIP_CHECK(hipGetLastError());
 }
 
+static std::atomic<int>& reduce4_flag() {
+  static std::atomic<int> f{[] {
+    const char* e = getenv("FAN_WIRE_REDUCE4");
+    return e && e[0] == '0' ? 0 : 1;
+  }()};
+  return f;
+}
+void set_wire_reduce4(int on) { reduce4_flag().store(on); }
+int wire_reduce4() { return reduce4_flag().load(std::memory_order_relaxed); }
+
 template <int C>
 static void reduce_sgd_dispatch(int local_dtype, int grid, const void* slots, size_t slot_stride, int n_slots,
                                 int self_pos, const void* local, float* master, float* mom, SgdParams p,
                                 size_t n_valid, const WirePtrs& dst, int n_dst, size_t n_s, int rel,
-                                hipStream_t stream) {
+                                hipStream_t stream, int grid4) {
   const uint8_t* sl = (const uint8_t*)slots;
+  if constexpr (C == kBfpTrunc || C == kBfpRne) {
+    if (grid4 > 0) {
+      if (local_dtype == kF32) {
+        if (mom)
+          hipLaunchKernelGGL((wire_reduce_sgd4_kernel<float, C, true>), grid4, kBlock, 0, stream, sl, slot_stride,
+                             n_slots, self_pos, (const float*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+        else
+          hipLaunchKernelGGL((wire_reduce_sgd4_kernel<float, C, false>), grid4, kBlock, 0, stream, sl, slot_stride,
+                             n_slots, self_pos, (const float*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+      } else {
+        if (mom)
+          hipLaunchKernelGGL((wire_reduce_sgd4_kernel<bf16_t, C, true>), grid4, kBlock, 0, stream, sl, slot_stride,
+                             n_slots, self_pos, (const bf16_t*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+        else
+          hipLaunchKernelGGL((wire_reduce_sgd4_kernel<bf16_t, C, false>), grid4, kBlock, 0, stream, sl, slot_stride,
+                             n_slots, self_pos, (const bf16_t*)local, master, mom, p, n_valid, dst, n_dst, n_s, rel);
+      }
+      return;
+    }
+  }
   if (local_dtype == kF32) {
     if (mom)
       hipLaunchKernelGGL((wire_reduce_sgd_kernel<float, C, true>), grid, kBlock, 0, stream, sl, slot_stride, n_slots,
@@ -539,9 +650,10 @@ void launch_wire_reduce_sgd(int codec, int local_dtype, const void* slots, size_
   if (n_s == 0) return;
   const int cap = peers ? std::min(wire_max_blocks(), p2p_grid_cap()) : wire_max_blocks();
   const int grid = stream_grid(n_s / 16, kBlock, cap);
+  const int grid4 = wire_reduce4() ? stream_grid(n_s / 4, kBlock, cap) : 0;
   const int rel = peers ? p2p_release_mode() : -1;
   FAN_CODEC_SWITCH(codec, reduce_sgd_dispatch<C>(local_dtype, grid, slots, slot_stride, n_slots, self_pos, local,
-                                                 master, mom, p, n_valid, dst, n_dst, n_s, rel, stream));
+                                                 master, mom, p, n_valid, dst, n_dst, n_s, rel, stream, grid4));
   FAN_HIP_CHECK(hipGetLastError());
 }
 

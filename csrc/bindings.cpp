@@ -153,6 +153,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_p2p_release_mode", &fan::set_p2p_release_mode);
   m.def("p2p_grid_cap", &fan::p2p_grid_cap, "workgroup cap of the peer-storing kernels");
   m.def("set_p2p_grid_cap", &fan::set_p2p_grid_cap);
+  m.def("wire_reduce4", &fan::wire_reduce4, "owner reduce + SGD kernel: 4 values per lane (1) or 16 (0)");
+  m.def("set_wire_reduce4", &fan::set_wire_reduce4);
   m.def("wire_reduce", &wire_reduce, "sum wire slots (+ dense local) -> wire and/or f32", pybind11::arg("slots"),
         pybind11::arg("n_slots"), pybind11::arg("self_pos"), pybind11::arg("local"), pybind11::arg("out_wire"),
         pybind11::arg("out_f32"), pybind11::arg("shard_elems"), pybind11::arg("codec"));

@@ -105,8 +105,8 @@ def _case(world, fabric, n=50000 - 48, momentum=0.9, steps=2):
     return {"ok": not why, "why": why}
 
 
-def _child(world, fabric):
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="32")
+def _child(world, fabric, **extra_env):
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="32", **extra_env)
     try:
         r = subprocess.run([sys.executable, os.path.abspath(__file__), str(world), fabric], env=env,
                            capture_output=True, text=True, timeout=150)
@@ -120,6 +120,12 @@ def _child(world, fabric):
 @pytest.mark.parametrize("world,fabric", [(2, "p2p"), (3, "p2p"), (8, "p2p"), (3, "loopback")])
 def test_shard_update_bit_identical_to_unsharded(world, fabric):
     _child(world, fabric)
+
+
+def test_shard_update_group_per_lane_reduce():
+    """The owner reduce + SGD kernel in its one-group-per-lane form (FAN_WIRE_REDUCE4=0; the default runs 4 values
+    per lane): the same bits as the unsharded schedule too."""
+    _child(3, "p2p", FAN_WIRE_REDUCE4="0")
 
 
 def test_shard_update_forced_one_rank_matches_inline():
