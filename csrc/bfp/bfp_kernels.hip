@@ -197,6 +197,66 @@ __global__ void __launch_bounds__(kBlock)
   p2p_release(rel);
 }
 
+// wire_reduce_to_kernel for the BFP codecs, lane-contiguous (as wire_reduce_sgd4_kernel below): 4 values per lane, 4
+// lanes a group, the group exponent from quad xor shuffles; each destination gets the lane's 4 mantissa bytes as one
+// dword and the group's exponent byte from its first lane. The same sums in slot order and the same encoding:
+// bit-identical (FAN_WIRE_REDUCE4).
+template <typename TL, int C>
+__global__ void __launch_bounds__(kBlock)
+    wire_reduce_to4_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
+                           const TL* __restrict__ local, WirePtrs dst, int n_dst, size_t n_s, int rel) {
+  static_assert(C == kBfpTrunc || C == kBfpRne, "BFP codecs");
+  const size_t tasks = n_s >> 2;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+    const size_t le = t << 2;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < n_slots; ++r) {
+      float v[4];
+      if (r == self_pos) {
+        if constexpr (sizeof(TL) == 4) {
+          const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(local) + le);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        } else {
+          const uint2 a = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(local) + le);
+          v[0] = __uint_as_float(a.x << 16); v[1] = __uint_as_float(a.x & 0xFFFF0000u);
+          v[2] = __uint_as_float(a.y << 16); v[3] = __uint_as_float(a.y & 0xFFFF0000u);
+        }
+      } else {
+        const uint8_t* sh = slots + (size_t)r * slot_stride;
+        const uint32_t m = *reinterpret_cast<const uint32_t*>(sh + le);
+        const uint32_t E = sh[n_s + (le >> 4)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int32_t q = (int32_t)(int8_t)(uint8_t)(m >> (8 * j));
+          v[j] = (C == kBfpTrunc) ? bfp_decode_trunc(q, E) : bfp_decode_rne(q, E);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += v[j];
+    }
+    uint32_t mx = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mx = max(mx, __float_as_uint(acc[j]) & 0x7FFFFFFFu);
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, 1));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, 2));
+    const uint32_t E = mx >> 23;
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t q = (C == kBfpTrunc) ? bfp_encode_trunc(__float_as_uint(acc[j]), E) : bfp_encode_rne(acc[j], E);
+      w |= ((uint32_t)q & 0xFFu) << (8 * j);
+    }
+    for (int i = 0; i < n_dst; ++i) {  // wave-uniform condition
+      uint8_t* d = dst.p[i];
+      if (d == nullptr) continue;
+      *reinterpret_cast<uint32_t*>(d + le) = w;
+      if ((le & 15) == 0) d[n_s + (le >> 4)] = (uint8_t)E;
+    }
+  }
+  p2p_release(rel);
+}
+
 // The value a rank decodes after the owner re-encodes `v` (one 16-value group) with codec C.
 template <int C>
 __device__ __forceinline__ void codec_roundtrip16(float v[16]) {
@@ -571,13 +631,38 @@ void launch_wire_pack_to(int codec, int in_dtype, const void* in, const WirePtrs
   FAN_HIP_CHECK(hipGetLastError());
 }
 
+// the lane-contiguous reduce-to-peers kernel for the BFP codecs (false: not launched — another codec, or the flag off)
+template <int C>
+static bool reduce_to4_dispatch(int grid4, int local_dtype, const void* slots, size_t slot_stride, int n_slots,
+                                int self_pos, const void* local, const WirePtrs& dst, int n_dst, size_t n_s,
+                                hipStream_t stream) {
+  if constexpr (C == kBfpTrunc || C == kBfpRne) {
+    if (grid4 <= 0) return false;
+    if (local_dtype == kF32)
+      hipLaunchKernelGGL((wire_reduce_to4_kernel<float, C>), grid4, kBlock, 0, stream, (const uint8_t*)slots,
+                         slot_stride, n_slots, self_pos, (const float*)local, dst, n_dst, n_s, p2p_release_mode());
+    else
+      hipLaunchKernelGGL((wire_reduce_to4_kernel<bf16_t, C>), grid4, kBlock, 0, stream, (const uint8_t*)slots,
+                         slot_stride, n_slots, self_pos, (const bf16_t*)local, dst, n_dst, n_s, p2p_release_mode());
+    return true;
+  } else {
+    return false;
+  }
+}
+
 void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t slot_stride, int n_slots, int self_pos,
                            const void* local, const WirePtrs& dst, int n_dst, size_t n_s, hipStream_t stream) {
   check_ns(n_s);
   FAN_CHECK(n_dst <= kMaxPeers && local != nullptr, "reduce_to: local operand and at most 16 destinations");
   if (n_s == 0) return;
   const int grid = stream_grid(n_s / 16, kBlock, std::min(wire_max_blocks(), p2p_grid_cap()));
+  const int grid4 = wire_reduce4() ? stream_grid(n_s / 4, kBlock, std::min(wire_max_blocks(), p2p_grid_cap())) : 0;
   FAN_CODEC_SWITCH(codec, {
+    if (reduce_to4_dispatch<C>(grid4, local_dtype, slots, slot_stride, n_slots, self_pos, local, dst, n_dst, n_s,
+                               stream)) {
+      FAN_HIP_CHECK(hipGetLastError());
+      return;
+    }
     if (local_dtype == kF32)
       hipLaunchKernelGGL((wire_reduce_to_kernel<float, C>), grid, kBlock, 0, stream, (const uint8_t*)slots,
                          slot_stride, n_slots, self_pos, (const float*)local, dst, n_dst, n_s, p2p_release_mode());
