@@ -22,6 +22,13 @@ namespace fan {
 
 static int wire_max_blocks();
 
+// The lane-contiguous (4 values per lane) BFP reduce kernels pay off where the dense f32 operands dominate the bytes
+// (the local gradient, the master / momentum planes) and cost where the 1-byte wire slots do — one group per lane
+// already reads a slot's mantissas 1 KiB per wave instruction, 4 values per lane 256 B: C.wire_reduce of 8 slots
+// measured 38.1 vs 33.6 us, of 2 slots 17.0 vs 17.1 (tools/probes/wire_reduce4_probe.py). So they run for at most two
+// slots (world 1 through the multi-rank path, 2 ranks); FAN_WIRE_REDUCE4=0 turns them off.
+static bool wire_reduce4_for(int n_slots) { return n_slots <= 2 && wire_reduce4() != 0; }
+
 static std::atomic<int>& release_mode_flag() {
   static std::atomic<int> m{[] {
     const char* e = getenv("FAN_P2P_RELEASE");
@@ -150,6 +157,64 @@ __global__ void __launch_bounds__(kBlock)
     }
     if (OUT_F32) DenseLane16<float>::store16(out_f32, le, acc);
     if (OUT_WIRE) WireLane16<C>::store16(out_wire, n_s, le, acc);
+  }
+}
+
+// wire_reduce_kernel for the BFP codecs, lane-contiguous (as wire_reduce_to4_kernel): 4 values per lane, the group
+// exponent from quad xor shuffles; bit-identical (FAN_WIRE_REDUCE4).
+template <typename TL, int C, bool HAS_LOCAL, bool OUT_WIRE, bool OUT_F32>
+__global__ void __launch_bounds__(kBlock)
+    wire_reduce4_kernel(const uint8_t* __restrict__ slots, size_t slot_stride, int n_slots, int self_pos,
+                        const TL* __restrict__ local, uint8_t* __restrict__ out_wire, float* __restrict__ out_f32,
+                        size_t n_s) {
+  static_assert(C == kBfpTrunc || C == kBfpRne, "BFP codecs");
+  const size_t tasks = n_s >> 2;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < tasks; t += stride) {
+    const size_t le = t << 2;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < n_slots; ++r) {
+      float v[4];
+      if (HAS_LOCAL && r == self_pos) {
+        if constexpr (sizeof(TL) == 4) {
+          const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(local) + le);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        } else {
+          const uint2 a = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(local) + le);
+          v[0] = __uint_as_float(a.x << 16); v[1] = __uint_as_float(a.x & 0xFFFF0000u);
+          v[2] = __uint_as_float(a.y << 16); v[3] = __uint_as_float(a.y & 0xFFFF0000u);
+        }
+      } else {
+        const uint8_t* sh = slots + (size_t)r * slot_stride;
+        const uint32_t m = *reinterpret_cast<const uint32_t*>(sh + le);
+        const uint32_t E = sh[n_s + (le >> 4)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int32_t q = (int32_t)(int8_t)(uint8_t)(m >> (8 * j));
+          v[j] = (C == kBfpTrunc) ? bfp_decode_trunc(q, E) : bfp_decode_rne(q, E);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += v[j];
+    }
+    if (OUT_F32) *reinterpret_cast<float4*>(out_f32 + le) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    if (OUT_WIRE) {
+      uint32_t mx = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mx = max(mx, __float_as_uint(acc[j]) & 0x7FFFFFFFu);
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, 1));
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, 2));
+      const uint32_t E = mx >> 23;
+      uint32_t w = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t q =
+            (C == kBfpTrunc) ? bfp_encode_trunc(__float_as_uint(acc[j]), E) : bfp_encode_rne(acc[j], E);
+        w |= ((uint32_t)q & 0xFFu) << (8 * j);
+      }
+      *reinterpret_cast<uint32_t*>(out_wire + le) = w;
+      if ((le & 15) == 0) out_wire[n_s + (le >> 4)] = (uint8_t)E;
+    }
   }
 }
 
@@ -537,13 +602,23 @@ void launch_wire_unpack(int codec, int out_dtype, const void* in, void* out, siz
 template <typename TL, int C>
 static void reduce_dispatch(const void* slots, size_t slot_stride, int n_slots, int self_pos, const void* local,
                             void* out_wire, float* out_f32, size_t n_s, hipStream_t stream) {
-  const int grid = stream_grid(n_s / 16, kBlock, wire_max_blocks());
+  const bool q4 = (C == kBfpTrunc || C == kBfpRne) && wire_reduce4_for(n_slots);
+  const int grid = stream_grid(q4 ? n_s / 4 : n_s / 16, kBlock, wire_max_blocks());
   const uint8_t* sl = (const uint8_t*)slots;
   const TL* lo = (const TL*)local;
   uint8_t* ow = (uint8_t*)out_wire;
-#define FAN_RED(HL, OW, OF)                                                                              \
-  hipLaunchKernelGGL((wire_reduce_kernel<TL, C, HL, OW, OF>), grid, kBlock, 0, stream, sl, slot_stride, \
-                     n_slots, self_pos, lo, ow, out_f32, n_s)
+#define FAN_RED(HL, OW, OF)                                                                                    \
+  do {                                                                                                         \
+    if constexpr (C == kBfpTrunc || C == kBfpRne) {                                                            \
+      if (q4) {                                                                                                \
+        hipLaunchKernelGGL((wire_reduce4_kernel<TL, C, HL, OW, OF>), grid, kBlock, 0, stream, sl, slot_stride, \
+                           n_slots, self_pos, lo, ow, out_f32, n_s);                                           \
+        break;                                                                                                 \
+      }                                                                                                        \
+    }                                                                                                          \
+    hipLaunchKernelGGL((wire_reduce_kernel<TL, C, HL, OW, OF>), grid, kBlock, 0, stream, sl, slot_stride,      \
+                       n_slots, self_pos, lo, ow, out_f32, n_s);                                               \
+  } while (0)
   const bool hl = local != nullptr, w = out_wire != nullptr, f = out_f32 != nullptr;
   FAN_CHECK(w || f, "wire_reduce needs an output");
   if (hl) {
@@ -656,7 +731,8 @@ void launch_wire_reduce_to(int codec, int local_dtype, const void* slots, size_t
   FAN_CHECK(n_dst <= kMaxPeers && local != nullptr, "reduce_to: local operand and at most 16 destinations");
   if (n_s == 0) return;
   const int grid = stream_grid(n_s / 16, kBlock, std::min(wire_max_blocks(), p2p_grid_cap()));
-  const int grid4 = wire_reduce4() ? stream_grid(n_s / 4, kBlock, std::min(wire_max_blocks(), p2p_grid_cap())) : 0;
+  const int grid4 =
+      wire_reduce4_for(n_slots) ? stream_grid(n_s / 4, kBlock, std::min(wire_max_blocks(), p2p_grid_cap())) : 0;
   FAN_CODEC_SWITCH(codec, {
     if (reduce_to4_dispatch<C>(grid4, local_dtype, slots, slot_stride, n_slots, self_pos, local, dst, n_dst, n_s,
                                stream)) {
@@ -735,7 +811,7 @@ void launch_wire_reduce_sgd(int codec, int local_dtype, const void* slots, size_
   if (n_s == 0) return;
   const int cap = peers ? std::min(wire_max_blocks(), p2p_grid_cap()) : wire_max_blocks();
   const int grid = stream_grid(n_s / 16, kBlock, cap);
-  const int grid4 = wire_reduce4() ? stream_grid(n_s / 4, kBlock, cap) : 0;
+  const int grid4 = wire_reduce4_for(n_slots) ? stream_grid(n_s / 4, kBlock, cap) : 0;
   const int rel = peers ? p2p_release_mode() : -1;
   FAN_CODEC_SWITCH(codec, reduce_sgd_dispatch<C>(local_dtype, grid, slots, slot_stride, n_slots, self_pos, local,
                                                  master, mom, p, n_valid, dst, n_dst, n_s, rel, stream, grid4));
