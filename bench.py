@@ -261,7 +261,7 @@ def main(argv=None):
         return ctx["p2p"]
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
-              force=False, panels=None, ring_sub=0, epi=None, engine=None, sizes=None, mdtype=None, bias=True,
+              force=False, ring_sub=0, epi=None, engine=None, sizes=None, mdtype=None, bias=True,
               relu="hidden", shard=None):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default); engine: python | native (default: the run's)."""
@@ -290,11 +290,10 @@ def main(argv=None):
             for l in model.layers:
                 ctrl.broadcast_(l.master, 0)
             model.sync_lp()
-        tr = DataParallelTrainer(model, eng, lr=a.lr, gemm_inflight=gemm, fused_update=fused, panels=panels)
+        tr = DataParallelTrainer(model, eng, lr=a.lr, gemm_inflight=gemm, fused_update=fused)
         info = {"compress": kind, "algo": algo, "rings": getattr(eng, "rings", 0) if eng is not None else 0,
                 "transport": (getattr(t, "name", transport) if comm is None else "p2p") if multi or force else "none",
                 "gemm_inflight": tr.gemm_inflight, "copy": ("sdma" if sdma else "kernel") if comm is not None else None,
-                "panels": tr.panel_plans[0]["chunks"] if tr.panel_plans else 0,
                 "ring_sub": int(getattr(eng, "ring_sub", 1)) if algo == "ring" else None,
                 "epilogue_stream": ("compute" if getattr(eng, "epilogue_on_producer", False) else "comm")
                 if eng is not None and not getattr(eng, "inline", True) else "inline",
@@ -460,10 +459,6 @@ def main(argv=None):
                 arms.append(dict(name="p2p_ring_sdma", kind="bfp", algo="ring", rings=R, transport="p2p", sdma=True))
             # each ring hop streamed in 3 sub-slices (a ready flag each; engine.cpp run_ring_direct)
             arms.append(dict(name="p2p_ring_stream3", kind="bfp", algo="ring", rings=R, transport="p2p", ring_sub=3))
-            # layer 0's bucket as 4 row panels, each submitted right after its GEMM (the exchange of the last bucket,
-            # which no backward is left to hide, starts a panel earlier; dp.py panels)
-            arms.append(dict(name="rccl_mesh_panels4", kind="bfp", algo="mesh", transport="native", panels=4))
-            arms.append(dict(name="p2p_mesh_panels4", kind="bfp", algo="mesh", transport="p2p", panels=4))
             # sharded update (ZeRO-1 style): each owner reduces + applies SGD to its shard, the ranks all-gather the new
             # bf16 weights into the layer's next weight buffer (no deferred epilogue, 1/N of the update pass per rank)
             arms.append(dict(name="rccl_mesh_shard", kind="bfp", algo="mesh", transport="native", shard=True))
@@ -493,7 +488,7 @@ def main(argv=None):
             try:
                 setup = build(spec["name"], spec["kind"], algo=spec.get("algo", "mesh"), rings=spec.get("rings", 1),
                               transport=spec["transport"], gemm=spec.get("gemm", "persistent"),
-                              sdma=spec.get("sdma", False), panels=spec.get("panels", 0),
+                              sdma=spec.get("sdma", False),
                               ring_sub=spec.get("ring_sub", 1), epi=spec.get("epi"), engine=spec.get("engine"),
                               shard=spec.get("shard", False))
                 rec.update(setup.info)
@@ -986,13 +981,14 @@ def _tuning_report():
 
 
 def replica_digest(tensors):
-    """Per tensor: (exact bit hash, fp64 sum). The hash is integer arithmetic on the f32 bit patterns (position-
+    """Per tensor: (exact bit hash, fp64 sum). The hash is integer arithmetic on the f32 / bf16 bit patterns (position-
     weighted, wrapping mod 2^64), so it is order-independent and equal across ranks iff the bits are."""
     import torch
 
     out = []
     for t in tensors:
-        b = t.detach().reshape(-1).contiguous().view(torch.int32).to(torch.int64)
+        bits = torch.int32 if t.element_size() == 4 else torch.int16
+        b = t.detach().reshape(-1).contiguous().view(bits).to(torch.int64)
         w = torch.arange(b.numel(), device=b.device, dtype=torch.int64).mul_(2).add_(1)
         h = int((b * w).sum().item()) & 0xFFFFFFFFFFFFFFFF
         out.append([f"{h:016x}", float(t.detach().double().sum().item())])
@@ -1003,21 +999,33 @@ def _dist_report(setup, world, rank, device, D, gate_rec):
     """extra.dist: what the run actually ran on — torch's and the engine communicator's rank counts (RCCL:
     ncclCommCount), the transport, the ring orders and link matrix the planner used, the devices (PCI bus ids) of
     the ranks — whether the production all-reduce path passed the bit-exact gate, and whether the replicas' weights
-    are bit-identical after the run (all-gathered digests)."""
+    are bit-identical after the run (all-gathered digests). Sharded-update arms: every rank's master is the
+    concatenation of the owners' shards after ``gather_state()``, identical by construction, so the check there is on
+    the bf16 weights each rank actually trains with (``lp``, written by the weight all-gather), hashed BEFORE the
+    gather, plus each rank's own check that its ``lp`` equals bf16(gathered master)."""
+    import torch
+
     from fpga_ai_nic_amd.utils import topology
 
     engine, model = setup.engine, setup.model
     C = getattr(engine, "C", None)
-    if getattr(setup.trainer, "shard", False):  # owner-sharded master / momentum: gather them before comparing
+    shard = bool(getattr(setup.trainer, "shard", False))
+    lp_digest, lp_match = None, None
+    if shard:  # owner-sharded master / momentum: gather them before comparing
+        setup.trainer.finish()
+        lp_digest = replica_digest([l.lp for l in model.layers if l.lp is not None])
         setup.trainer.gather_state()
+        lp_match = all(torch.equal(l.lp[:l.n], l.master[:l.n].to(torch.bfloat16))
+                       for l in model.layers if l.lp is not None)
     mine = {
-        "digest": replica_digest([l.master for l in model.layers]),
+        "digest": replica_digest([l.master for l in model.layers]) + (lp_digest or []),
+        "lp_matches_master": lp_match,
         "comm_ranks": int(C.comm_ranks) if C is not None else (world if engine is not None else 1),
         "bus_id": topology.device_bus_id(device.index) if device.type == "cuda" else None,
     }
     every = D.all_gather_object(mine)
     digests = [e["digest"] for e in every]
-    ident = all(d == digests[0] for d in digests)
+    ident = all(d == digests[0] for d in digests) and all(e["lp_matches_master"] is not False for e in every)
     return {
         "world": world,
         "torch_backend": D.backend(),
@@ -1031,7 +1039,8 @@ def _dist_report(setup, world, rank, device, D, gate_rec):
         "allreduce_exact": gate_rec["exact"] if gate_rec is not None else None,
         "allreduce_gate": gate_rec,
         "replicas_identical": ident,
-        "master_gathered_from_owners": bool(getattr(setup.trainer, "shard", False)),
+        "master_gathered_from_owners": shard,
+        "lp_matches_master": [e["lp_matches_master"] for e in every] if shard else None,
         "replica_digests": digests if not ident else digests[0],
     }
 

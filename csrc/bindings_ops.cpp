@@ -3,7 +3,7 @@
 #include "bfp/bfp_format.h"
 #include "comm/planner.h"
 #include "gemm/gemm.h"
-#include "gemm/gemm_pair.h"
+#include "gemm/gemm_group.h"
 #include "nn/nn.h"
 
 namespace fan {
@@ -69,13 +69,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     g.bias = bias->data_ptr();
   }
   if (aux) {
-    if (is_bits_epi((int)epilogue)) {  // the 1-bit ReLU mask plane: uint8 [M][ldaux bytes]
-      TORCH_CHECK(aux->is_cuda() && aux->scalar_type() == at::kByte && aux->dim() == 2 && aux->size(0) == g.M &&
-                      aux->size(1) * 8 >= g.N,
-                  "mask-bit epilogue: aux must be a uint8 [M][>= N/8] GPU plane");
-    } else {
-      TORCH_CHECK(aux->scalar_type() == C.scalar_type(), "aux dtype must match C");
-    }
+    TORCH_CHECK(aux->scalar_type() == C.scalar_type(), "aux dtype must match C");
     g.aux = aux->data_ptr();
     g.ldaux = ld_of(*aux);
   }
@@ -144,36 +138,6 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
     TORCH_CHECK(gemm_f32_supported(g), "gemm_f32: unsupported shape M=", g.M, " N=", g.N, " K=", g.K);
     launch_gemm_f32(g, fan_stream());
   }
-}
-
-// One layer's backward pair in one dispatch: dX = (dZ . W^T) * (X > 0) (bf16) and dW = X^T . dZ (f32).
-// X [M][cin], dZ [M][cout], W [cin][cout] (bf16); dX [M][cin] bf16; dW [cin][cout] f32.
-void gemm_bwd_pair(const at::Tensor& dZ, const at::Tensor& W, const at::Tensor& X, at::Tensor& dX, at::Tensor& dW,
-                   int64_t bw_bn, int64_t grid0, int64_t grid1) {
-  for (const at::Tensor* t : {&dZ, &W, &X, static_cast<const at::Tensor*>(&dX)})
-    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->stride(1) == 1,
-                "gemm_bwd_pair: bf16 2-D GPU tensors");
-  TORCH_CHECK(dW.is_cuda() && dW.scalar_type() == at::kFloat && dW.dim() == 2 && dW.stride(1) == 1, "dW: f32 2-D");
-  const int64_t M = X.size(0), cin = X.size(1), cout = dZ.size(1);
-  TORCH_CHECK(dZ.size(0) == M && W.size(0) == cin && W.size(1) == cout && dX.size(0) == M && dX.size(1) == cin &&
-                  dW.size(0) == cin && dW.size(1) == cout,
-              "gemm_bwd_pair: shapes");
-  GemmArgs bd{};
-  bd.A = dZ.data_ptr(); bd.lda = ld_of(dZ);
-  bd.B = W.data_ptr(); bd.ldb = ld_of(W);
-  bd.C = dX.data_ptr(); bd.ldc = ld_of(dX);
-  bd.aux = X.data_ptr(); bd.ldaux = ld_of(X);
-  bd.M = (int)M; bd.N = (int)cin; bd.K = (int)cout;
-  bd.a_kcontig = true; bd.b_kcontig = true; bd.epilogue = kEpiReluMask; bd.c_bf16 = true;
-  GemmArgs bw{};
-  bw.A = X.data_ptr(); bw.lda = ld_of(X);
-  bw.B = dZ.data_ptr(); bw.ldb = ld_of(dZ);
-  bw.C = dW.data_ptr(); bw.ldc = ld_of(dW);
-  bw.M = (int)cin; bw.N = (int)cout; bw.K = (int)M;
-  bw.a_kcontig = false; bw.b_kcontig = false; bw.epilogue = kEpiNone; bw.c_bf16 = false;
-  bw.tile_bm = 256; bw.tile_bn = (int)bw_bn;
-  TORCH_CHECK(gemm_bwd_pair_supported(bd, bw, (int)grid0, (int)grid1), "gemm_bwd_pair: unsupported configuration");
-  launch_gemm_bwd_pair(bd, bw, (int)grid0, (int)grid1, fan_stream());
 }
 
 // Up to kGroupMax bwd-weight GEMMs C_i = X_i^T . dY_i (+ colsum_i = sum of dY_i's rows) in one dispatch, f32 out or
@@ -294,9 +258,6 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("upd_grad_scale") = 1.0, pybind11::arg("upd_weight_decay") = 0.0,
         pybind11::arg("upd_momentum") = 0.0, pybind11::arg("upd_nesterov") = false);
   m.def("gemm_supported", &gemm_supported);
-  m.def("gemm_bwd_pair", &gemm_bwd_pair, "one layer's bwd-data (ReLU mask, bf16) + bwd-weight (f32) in one dispatch",
-        pybind11::arg("dZ"), pybind11::arg("W"), pybind11::arg("X"), pybind11::arg("dX"), pybind11::arg("dW"),
-        pybind11::arg("bw_bn") = 256, pybind11::arg("grid0") = 128, pybind11::arg("grid1") = 128);
   m.def("gemm_wgrad_group", &gemm_wgrad_group,
         "up to 8 bwd-weight GEMMs (+ fused bias gradients, f32 or BFP wire epilogue) in one dispatch",
         pybind11::arg("Xs"), pybind11::arg("dYs"), pybind11::arg("Cs"), pybind11::arg("colsums"),
@@ -310,18 +271,9 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_set_ovl", [](int on) { gemm_ovl_flag().store(on); },
         "256x256 bf16 plans on the persistent loop with overlapped tile transitions (pl4_run OVL)");
   m.def("gemm_ovl", []() { return gemm_ovl_flag().load(); });
-  m.def("gemm_set_trn", [](int on) { gemm_trn_flag().store(on); },
-        "overlapped 256x256 bf16 loop with transposed accumulators and the LDS-free epilogue (pl4_run TRN)");
-  m.def("gemm_trn", []() { return gemm_trn_flag().load(); });
-  m.def("gemm_set_edma", [](int on) { gemm_edma_flag().store(on); },
-        "overlapped 256x256 loop with two barriers per K-tile and the operand DMA over both k-steps (pl4_run EDMA)");
-  m.def("gemm_edma", []() { return gemm_edma_flag().load(); });
   m.def("gemm_set_reduce4", [](int on) { gemm_reduce4_flag().store(on); },
         "split-K wire / fused-update reduce: 4 values per lane (1) or one 16-value group per lane (0)");
   m.def("gemm_reduce4", []() { return gemm_reduce4_flag().load(); });
-  m.def("gemm_set_occ2", [](int on) { gemm_occ2_flag().store(on); },
-        "unsplit 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)");
-  m.def("gemm_occ2", []() { return gemm_occ2_flag().load(); });
   m.def("gemm_f32_split", &gemm_f32_split, "f32 GEMM split-K factor (split_k <= 0: automatic)", pybind11::arg("M"),
         pybind11::arg("N"), pybind11::arg("K"), pybind11::arg("split_k") = 0);
   m.def("gemm_set_main_loop", [](int mode) { gemm_main_loop_flag().store(mode); },
@@ -331,12 +283,6 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_set_persist", [](int cap) { gemm_persist_flag().store(cap); },
         "grid cap of the persistent 4-wave GEMM kernel (<= 0: one workgroup per tile)");
   m.def("gemm_persist", []() { return gemm_persist_flag().load(); });
-  m.def("gemm_set_half_stage", [](int on) { gemm_half_stage_flag().store(on); },
-        "256x256 persistent 4-wave loop: ring of four 32-k half-stages (1) or two 64-k stages (0)");
-  m.def("gemm_half_stage", []() { return gemm_half_stage_flag().load(); });
-  m.def("gemm_set_fixup", [](int on) { gemm_fixup_flag().store(on); },
-        "split-K wire epilogues: in-GEMM last-workgroup fixup (1) or the separate slab reduce kernel (0)");
-  m.def("gemm_fixup", []() { return gemm_fixup_flag().load(); });
   m.def("gemm_set_stamp_buffer", [](const c10::optional<at::Tensor>& t) {
           gemm_set_stamp_buffer(t ? t->data_ptr() : nullptr);
         },

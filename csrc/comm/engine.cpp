@@ -325,8 +325,17 @@ std::vector<EpiThunk> AllReduceEngine::run_mesh(const EngineLayout& L, const voi
     mark(kTpReduced);
     if (!ident) {
       RoctxRange rr("fan/mesh/all_gather_weights");
-      comm_->all_gather(lp + (size_t)r * s, lp, (size_t)s * 2, st);
-      count_peers((size_t)s * 2);
+      // the weight shard goes through the same verify tags and fault hook as the unsharded path's gathered gradient
+      uint8_t* W = reinterpret_cast<uint8_t*>(lp);
+      const size_t wb = (size_t)s * 2;
+      if (verify_) launch_msg_tags(W + (size_t)r * wb, wb, wb, 1, req_seq_, tag_region(3), st);
+      fault_.maybe_corrupt("mesh_reduce", W + (size_t)r * wb, wb, st);
+      comm_->all_gather(lp + (size_t)r * s, lp, wb, st);
+      count_peers(wb);
+      if (verify_) {
+        comm_->all_gather(tag_region(3), tag_region(4), 16, st);
+        verify_rows(W, wb, N, tag_region(4), kSiteMeshWeightGather, 0, st);
+      }
     }
     counters_.sharded_updates++;
     return {};
@@ -947,10 +956,17 @@ void AllReduceEngine::gather_owned(float* plane, int64_t n) {
   const int N = world_, r = rank_;
   const int64_t s = L.shard;
   hipStream_t st = stream_;
-  // every request that updated the plane has finished (its SGD ran on this engine's streams; not a device-wide sync:
-  // virtual ranks in one process would wait on each other's streams parked on this rank's coming flags)
+  // every request that updated the plane has finished. Its owner SGD ran on this engine's comm / aux stream, or — the
+  // backward's last request (on_producer) — on the caller's compute stream: the engine streams are synchronized and
+  // every used slot's done event (recorded on whichever stream ran the request's epilogue) is waited for before the
+  // all-gather reads the shard. Not a device-wide sync: virtual ranks in one process would wait on each other's
+  // streams parked on this rank's coming flags.
   FAN_HIP_CHECK(hipStreamSynchronize(stream_));
   FAN_HIP_CHECK(hipStreamSynchronize(aux_stream_));
+  table_->for_each_used([](int, const SlotTable<HipSlotDevice>::Slot& sl) {
+    FAN_CHECK(!sl.pending, "gather_owned: a request is still deferred (commit or synchronize every request first)");
+    FAN_HIP_CHECK(hipEventSynchronize(sl.done));
+  });
   size_t max_bytes = (size_t)s * 4;
   if (P2PComm* d = comm_->direct()) max_bytes = std::min(max_bytes, d->payload_bytes() / 256 * 256);
   const int64_t piece = std::max<int64_t>(64, (int64_t)(max_bytes / 4) / 64 * 64);
@@ -1137,7 +1153,12 @@ std::string AllReduceEngine::debug_status() {
   for (int i = 0; i < kSlots; ++i) {
     const auto& sl = table_->slot(i);
     os << (i ? ", " : "") << "{\"slot\": " << i << ", \"seq\": " << sl.seq << ", \"pending\": "
-       << (sl.pending ? "true" : "false") << ", \"done_word\": " << flags_host_[i * 16]
+       << (sl.pending ? "true" : "false") << ", \"done_word\": ";
+    // host-mapped done words are written only with FAN_DONE_WORDS=1: otherwise report the done event's state
+    if (table_->done_words()) os << flags_host_[i * 16];
+    else os << "null";
+    const int dn = table_->peek_done(i);
+    os << ", \"done\": " << (dn < 0 ? "null" : dn ? "true" : "false")
        << ", \"epilogue_stream\": \""
        << (!sl.used || sl.pending ? "none"
            : sl.epi_stream == stream_ ? "comm"
@@ -1179,7 +1200,9 @@ std::string AllReduceEngine::diagnostics(int slot) const {
   const auto& sl = table_->slot(slot);
   std::ostringstream os;
   os << "rank=" << rank_ << " world=" << world_ << " algo=" << (cfg_.algo ? "ring" : "mesh") << " codec=" << cfg_.codec
-     << " slot=" << slot << " seq=" << sl.seq << " done_word=" << flags_host_[slot * 16]
+     << " slot=" << slot << " seq=" << sl.seq
+     << (table_->done_words() ? " done_word=" + std::to_string(flags_host_[slot * 16])
+                              : std::string(" done_word=unwritten(FAN_DONE_WORDS=0)"))
      << " elapsed=" << (now_s() - extra_.at(slot).t_issue) << "s";
   if (comm_) os << " rccl_async_error='" << comm_->async_error() << "'";
   return os.str();
@@ -1228,7 +1251,7 @@ void AllReduceEngine::verify_rows(const uint8_t* rows, size_t row_bytes, int nro
 void AllReduceEngine::check_verify() {
   if (!verify_ || verr_host_->flag == 0) return;
   static const char* sites[] = {"?", "mesh all_to_all", "mesh all_gather", "ring round", "mesh direct send",
-                                "mesh direct gather", "ring direct hop"};
+                                "mesh direct gather", "ring direct hop", "mesh weight all_gather"};
   const VerifyError e = *verr_host_;
   std::ostringstream os;
   os << "verify: message " << (e.kind == 1 ? "corrupted" : "out of sequence (dropped or reordered)") << " in "

@@ -125,6 +125,7 @@ enum VerifySite : uint32_t {
   kSiteMeshDirectSend = 4,
   kSiteMeshDirectGather = 5,
   kSiteRingDirect = 6,
+  kSiteMeshWeightGather = 7,  // the sharded update's bf16 weight all-gather (run_mesh)
 };
 
 // Deferred epilogue of a request (decode + SGD), launched on the given stream at commit().
@@ -199,7 +200,9 @@ class AllReduceEngine {
   void commit(int slot, bool after_producer, hipStream_t producer, uint32_t seq = 0);
   void wait_stream(int slot, hipStream_t s, uint32_t seq = 0);  // GPU-side wait
   bool query(int slot, uint32_t seq = 0);                       // host: request done?
-  uint32_t done_word(int slot) const { return flags_host_[slot * 16]; }  // last completed sequence number
+  // the slot's host-mapped done word: the last completed sequence number, written only when done words are on
+  // (FAN_DONE_WORDS=1; off by default, then it stays 0 and debug_status reports the done event instead)
+  uint32_t done_word(int slot) const { return flags_host_[slot * 16]; }
   uint32_t slot_seq(int slot) const { return table_->slot(slot).seq; }
   void synchronize(int slot, double timeout_s = -1.0, uint32_t seq = 0);  // host: bounded wait (throws)
   float latency_ms(int slot);

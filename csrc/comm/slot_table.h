@@ -206,6 +206,15 @@ class SlotTable {
   }
   void ensure_done(int s) { ensure_done(slots_.at(s)); }
   void set_keep_done(int s, bool on) { slots_.at(s).keep_done = on; }
+  bool done_words() const { return cfg_.done_words && !cfg_.inline_mode; }
+  // completion of a slot's request for diagnostics, without recording anything: -1 unknown (pending, or its done
+  // event still lazy), else the done event's query
+  int peek_done(int s) {
+    Slot& sl = slots_.at(s);
+    if (!sl.used) return 1;
+    if (sl.pending || sl.done_lazy) return -1;
+    return dev_.query(sl.done) ? 1 : 0;
+  }
 
   // destructor helper: every slot's epilogue that may still run
   template <class F>

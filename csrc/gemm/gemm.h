@@ -20,14 +20,8 @@ enum GemmEpilogue : int {
   kEpiReluMask = 3,   // x * (aux[m][n] > 0)   (ReLU backward fused into the bwd-data GEMM)
   kEpiWire = 4,       // BFP-encode the f32 result straight into all-reduce wire shards (see GemmArgs::wire)
   kEpiWireUpd = 5,    // kernel-internal: kEpiWire with the fused local update (GemmArgs::upd_master set)
-  // ReLU through a 1-bit mask instead of the bf16 activation (bf16 output, no split-K): aux is a uint8 plane
-  // [M][ldaux bytes], bit n % 8 of byte n / 8 = (output(m, n) > 0). The forward writes it beside its activation, the
-  // bwd-data GEMM reads 1/16 of the bytes kEpiReluMask reads (64 MB -> 4 MB per 8192 x 4096 layer).
-  kEpiBiasReluBits = 6,  // relu(x + bias[n]) and its mask bits into aux
-  kEpiReluBits = 7,      // x * bit(aux, m, n)
 };
 constexpr bool is_wire_epi(int e) { return e == kEpiWire || e == kEpiWireUpd; }
-constexpr bool is_bits_epi(int e) { return e == kEpiBiasReluBits || e == kEpiReluBits; }
 
 // GemmArgs::wire_own value: every shard is also written to C in f32 (the ring needs every local slice in f32:
 // each reduce hop adds the local f32 contribution, hw/all_reduce.sv:1168-1183)
@@ -89,35 +83,15 @@ std::atomic<int>& gemm_main_loop_flag();
 // grid cap of the persistent 4-wave pipelined kernel (FAN_GEMM_PERSIST, default 256 = one workgroup per CU; 0: one
 // workgroup per tile); settable for in-process A/B and for tests that force several tiles per workgroup
 std::atomic<int>& gemm_persist_flag();
-// 256x256 persistent 4-wave loop on the ring of four 32-k half-stages (gemm_pl4h_kernel) instead of two 64-k stages
-// (FAN_GEMM_HALF, gemm_set_half_stage)
-std::atomic<int>& gemm_half_stage_flag();
-// unsplit, bias-gradient-free 256x256 plans on two workgroups per CU with 256x128 tiles (gemm_pl2h_kernel)
-// instead of the persistent one-workgroup-per-CU kernel (FAN_GEMM_OCC2, gemm_set_occ2)
-std::atomic<int>& gemm_occ2_flag();
 // the 4-wave pipelined GEMM waves at s_setprio 2, so another stream's kernels sharing their CUs (the all-reduce's)
 // issue in the GEMM waves' stalls only (default on; FAN_GEMM_PRIO=0, gemm_set_prio)
 std::atomic<int>& gemm_prio_flag();
 // 256x256 bf16 plans on the persistent loop whose tile transitions overlap the epilogue with the next tile's first
 // K-tiles (pl4_run OVL; default on, FAN_GEMM_OVL=0, gemm_set_ovl)
 std::atomic<int>& gemm_ovl_flag();
-// with it: the accumulators transposed (MFMA operands swapped) and the bf16 epilogue stored straight from registers,
-// no LDS round trip (pl4_run TRN; FAN_GEMM_TRN, gemm_set_trn)
-std::atomic<int>& gemm_trn_flag();
-// with it: two barriers per K-tile, the operand DMA spread over both k-steps (pl4_run EDMA; FAN_GEMM_EDMA,
-// gemm_set_edma)
-std::atomic<int>& gemm_edma_flag();
 // split-K wire / fused-update reduce: lane-contiguous form, 4 values per lane (1, default) or one 16-value group per
 // lane (0) (FAN_GEMM_REDUCE4, gemm_set_reduce4); bit-identical either way
 std::atomic<int>& gemm_reduce4_flag();
-// split-K wire epilogues: the last workgroup of each tile sums the slabs and runs the epilogue in the GEMM (1) or a
-// separate reduce kernel does (0, default: the fixup measured 14 % slower on the flagship step) (FAN_GEMM_FIXUP,
-// gemm_set_fixup); bit-identical either way
-std::atomic<int>& gemm_fixup_flag();
-// per-(device, stream) tile counters of that in-GEMM split-K fixup (kFixTiles entries, zero between launches: the
-// last workgroup of a tile resets its counter); nullptr while the stream is capturing and none exists yet
-unsigned* gemm_fix_counters(hipStream_t s);
-constexpr int kFixTiles = 4096;
 // diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
 void gemm_set_stamp_buffer(void* p);
 void* gemm_stamp_buffer();

@@ -184,20 +184,14 @@ struct Out<bf16_t> {
 template <int EPI, typename TC, bool ACCUM>
 __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                      const TC* __restrict__ aux, int64_t ldaux, int row, int col) {
-  static_assert(EPI != kEpiBiasReluBits || sizeof(TC) == 2, "mask-bit epilogues: bf16 output");
-  if (EPI == kEpiBias || EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {
+  if (EPI == kEpiBias || EPI == kEpiBiasRelu) {
     const uint2 u = *reinterpret_cast<const uint2*>(bias + col);
     v[0] += __uint_as_float(u.x << 16); v[1] += __uint_as_float(u.x & 0xFFFF0000u);
     v[2] += __uint_as_float(u.y << 16); v[3] += __uint_as_float(u.y & 0xFFFF0000u);
   }
-  if (EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {  // (4-column paths never write mask bits: split-K only)
+  if (EPI == kEpiBiasRelu) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = fmaxf(v[u], 0.f);
-  }
-  if (EPI == kEpiReluBits) {
-    const uint32_t b = reinterpret_cast<const uint8_t*>(aux)[(int64_t)row * ldaux + col / 8] >> (col & 4);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = (b >> u) & 1u ? v[u] : 0.f;
   }
   if (EPI == kEpiReluMask) {
     float m[4];
@@ -219,26 +213,19 @@ __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc
 // epilogue of a 256x256 bf16 tile is store-ISSUE-bound (MI355X_MICROARCH.md per-instruction table: a dwordx2 store
 // tail runs at about half the rate of dwordx4), so the bf16 outputs are written 8 columns per lane. Same
 // arithmetic, element for element, as epi4.
-// kEpiReluBits: `bits` holds the 8 mask bits of these columns; kEpiBiasReluBits: returns them (bit u: the stored bf16
-// output u is > 0, the test kEpiReluMask applies to the activation).
 template <int EPI, bool ACCUM>
-__device__ __forceinline__ uint32_t epi8_bf16(float v[8], bf16_t* __restrict__ C, int64_t ldc,
-                                              const bf16_t* __restrict__ bias, const uint4* mask, uint32_t bits,
-                                              int row, int col) {
+__device__ __forceinline__ void epi8_bf16(float v[8], bf16_t* __restrict__ C, int64_t ldc,
+                                          const bf16_t* __restrict__ bias, const uint4* mask, int row, int col) {
   auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
   auto hi = [](uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); };
-  if (EPI == kEpiBias || EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {
+  if (EPI == kEpiBias || EPI == kEpiBiasRelu) {
     const uint4 u = *reinterpret_cast<const uint4*>(bias + col);
     v[0] += lo(u.x); v[1] += hi(u.x); v[2] += lo(u.y); v[3] += hi(u.y);
     v[4] += lo(u.z); v[5] += hi(u.z); v[6] += lo(u.w); v[7] += hi(u.w);
   }
-  if (EPI == kEpiBiasRelu || EPI == kEpiBiasReluBits) {
+  if (EPI == kEpiBiasRelu) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) v[u] = fmaxf(v[u], 0.f);
-  }
-  if (EPI == kEpiReluBits) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (bits >> u) & 1u ? v[u] : 0.f;
   }
   if (EPI == kEpiReluMask) {
     const uint4 m = *mask;
@@ -255,16 +242,6 @@ __device__ __forceinline__ uint32_t epi8_bf16(float v[8], bf16_t* __restrict__ C
   const uint4 o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                              pack_bf16x2(v[6], v[7]));
   *reinterpret_cast<uint4*>(p) = o;
-  uint32_t out = 0;
-  if (EPI == kEpiBiasReluBits) {  // positive finite or +inf: bf16 bits in [1, 0x7F80] (what "> 0" holds for)
-    const uint32_t w[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint32_t h = (u & 1) ? (w[u >> 1] >> 16) : (w[u >> 1] & 0xFFFFu);
-      out |= (h - 1u < 0x7F80u ? 1u : 0u) << u;
-    }
-  }
-  return out;
 }
 
 // kEpiWire target (GemmArgs::wire*): passed by value as one kernel argument.
@@ -285,9 +262,6 @@ struct WireOut {
   bf16_t* ulp;
   float* umom;
   SgdParams up;
-  // split-K with a wire epilogue: per-tile arrival counters of the in-GEMM fixup (split_fixup; nullptr: the slabs
-  // are reduced by splitk_reduce_wire_kernel)
-  unsigned* fix;
 #ifdef FAN_GEMM_STAMPS
   unsigned long long* stamps;  // diagnostic builds: s_memtime stamp buffer (see FAN_STAMP)
 #endif
@@ -406,83 +380,6 @@ __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict_
   }
 }
 
-// In-GEMM split-K fixup of the wire epilogues (gemm_pl4_kernel, wo.fix set): every workgroup of a tile has stored
-// its slab (and, in tile row 0, its bias partial sums); the LAST of the tile's split_k workgroups to get here — an
-// agent-scope arrival counter per tile, reset to 0 by that workgroup for the next launch — sums the tile's slabs in
-// split order and runs the epilogue of splitk_reduce_wire_kernel on them: the same sums in the same order, so the
-// result is bit-identical, without a second launch that re-reads every slab from memory after the GEMM drained.
-// No workgroup waits for another (the last one to arrive does the work), so co-residency is never assumed.
-// MEASURED SLOWER, so opt-in (FAN_GEMM_FIXUP=1): the flagship step 1.166-1.169 vs 1.020-1.027 ms/step
-// (profiles/r4_gemm_splitk_fixup_ab.jsonl). The 1024x4096 bwd-weight has 64 tiles, so 64 workgroups each stream
-// ~1.7 MB (four 256 KB slabs + the update planes) where the reduce kernel spreads the same bytes over every CU; and
-// every workgroup's agent-scope release writes back its XCD's L2. Bit-identical (tests/test_gpu_gemm_fixup.py).
-// The fences: each thread's slab stores are released at agent scope (written back past its XCD's L2) before the
-// counter increment; the last workgroup acquires at agent scope (its L2 invalidated) before reading the slabs that
-// workgroups on other XCDs wrote.
-template <int BMT, int BNT>
-__device__ __forceinline__ void split_fixup(int tile, int m0, int n0, const float* __restrict__ ws, int split_k,
-                                            float* __restrict__ C, int64_t ldc, int M, int N,
-                                            float* __restrict__ colsum, const WireOut& wo, char* smem) {
-  __threadfence();
-  __syncthreads();
-  int* last_flag = reinterpret_cast<int*>(smem);
-  if (threadIdx.x == 0) {
-    const unsigned old = atomicAdd(wo.fix + tile, 1u);
-    const int last = old == (unsigned)(split_k - 1);
-    if (last) atomicExch(wo.fix + tile, 0u);
-    *last_flag = last;
-  }
-  __syncthreads();
-  if (!*last_flag) return;
-  __threadfence();
-  const int64_t slab = (int64_t)M * N;
-  constexpr int GPR = BNT / 16;  // 16-column groups per tile row
-  for (int g = threadIdx.x; g < BMT * GPR; g += blockDim.x) {
-    const int row = m0 + g / GPR, col = n0 + (g % GPR) * 16;
-    const float* p = ws + (int64_t)row * N + col;
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; u += 4) {
-      const float4 q = *reinterpret_cast<const float4*>(p + u);
-      v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
-    }
-    for (int k = 1; k < split_k; ++k) {
-#pragma unroll
-      for (int u = 0; u < 16; u += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(p + k * slab + u);
-        v[u] += q.x; v[u + 1] += q.y; v[u + 2] += q.z; v[u + 3] += q.w;
-      }
-    }
-    if (wo.um) wire_epi16<true>(v, C, ldc, wo, row, col);
-    else wire_epi16<false>(v, C, ldc, wo, row, col);
-  }
-  if (colsum && m0 == 0) {  // the bias partials of this tile's columns (written by tile row 0's workgroups)
-    for (int c = threadIdx.x; c < GPR; c += blockDim.x) {
-      const int col = n0 + c * 16;
-      const float* p = ws + (int64_t)split_k * slab + col;
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; u += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(p + u);
-        v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
-      }
-      for (int k = 1; k < split_k; ++k) {
-#pragma unroll
-        for (int u = 0; u < 16; u += 4) {
-          const float4 q = *reinterpret_cast<const float4*>(p + (int64_t)k * N + u);
-          v[u] += q.x; v[u + 1] += q.y; v[u + 2] += q.z; v[u + 3] += q.w;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) colsum[col + u] = v[u];
-      if (wo.bias_off > 0) {
-        if (wo.um) wire_store16<true>(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
-        else wire_store16<false>(v, (uint32_t)wo.bias_off + (uint32_t)col, wo);
-      }
-    }
-  }
-}
-
 // Fused bias gradient tail: lanes l, l^16, l^32, l^48 hold the same column over different k rows. Writes
 // out[col0 + j*16 + lane] (the column sums, or this K-split's partial sums); with kEpiWire and no split-K also
 // encodes the bias segment of the [W | b] bucket (its 16-column group is lanes 0..15).
@@ -556,22 +453,8 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
       constexpr int HV = WTN / SW;  // staged column halves
       static_assert(WTN % 8 == 0 && RP8 <= 16 && 16 % RP8 == 0, "8-column chunks of whole 16-row blocks");
       constexpr bool kPf8 = EPI == kEpiReluMask;
-      constexpr bool kBitsIn = EPI == kEpiReluBits, kBitsOut = EPI == kEpiBiasReluBits;
       constexpr int kPfd = 2;
       uint4 aq8[kPf8 ? MI : 1][kPf8 ? HV * NP8 : 1];
-      uint32_t bq[kBitsIn ? MI : 1][kBitsIn ? HV * NP8 : 1];
-      // mask bits: one byte per lane (its 8 columns) per pass, prefetched like the activation chunks
-      auto bits_load = [&](int i) __attribute__((always_inline)) {
-#pragma unroll
-        for (int hv = 0; hv < HV; ++hv)
-#pragma unroll
-          for (int pass = 0; pass < NP8; ++pass) {
-            const int row = row0 + i * 16 + pass * RP8 + lane / C8;
-            const int col = col0 + hv * SW + (lane % C8) * 8;
-            if (!mn_edge || (row < M && col < N))
-              bq[i][hv * NP8 + pass] = reinterpret_cast<const uint8_t*>(aux)[(int64_t)row * ldaux + col / 8];
-          }
-      };
       auto aux_load8 = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
         for (int hv = 0; hv < HV; ++hv)
@@ -587,17 +470,10 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
 #pragma unroll
         for (int i = 0; i < kPfd && i < MI; ++i) aux_load8(i);
       }
-      if constexpr (kBitsIn) {
-#pragma unroll
-        for (int i = 0; i < kPfd && i < MI; ++i) bits_load(i);
-      }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         if constexpr (kPf8) {
           if (i + kPfd < MI) aux_load8(i + kPfd);
-        }
-        if constexpr (kBitsIn) {
-          if (i + kPfd < MI) bits_load(i + kPfd);
         }
 #pragma unroll
         for (int hv = 0; hv < HV; ++hv) {
@@ -618,11 +494,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
           if (mn_edge && (row >= M || col >= N)) continue;  // N % 8 == 0: an 8-column chunk is wholly in or out
           const uint4* mk = nullptr;
           if constexpr (kPf8) mk = &aq8[i][hv * NP8 + pass];
-          uint32_t bits = 0;
-          if constexpr (kBitsIn) bits = bq[i][hv * NP8 + pass];
-          const uint32_t ob = epi8_bf16<EPI, ACCUM>(v, reinterpret_cast<bf16_t*>(C), ldc, bias, mk, bits, row, col);
-          if constexpr (kBitsOut)  // aux is the mask plane this forward writes
-            reinterpret_cast<uint8_t*>(const_cast<TC*>(aux))[(int64_t)row * ldaux + col / 8] = (uint8_t)ob;
+          epi8_bf16<EPI, ACCUM>(v, reinterpret_cast<bf16_t*>(C), ldc, bias, mk, row, col);
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // the staged rows are read before the next half / block rewrites them
         }
@@ -1156,116 +1028,16 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
 
 // The body of gemm_pl4_kernel as a device function: this workgroup runs virtual blocks v0, v0 + vstep, ... of the
 // problem's tiles * split_k (COLSUM: the one tile v0). gemm_pl4_kernel passes (blockIdx.x, gridDim.x); the grouped
-// kernel (gemm_group2_kernel) gives each of its two problems its own range of workgroups. vstep must be a multiple
+// kernel (gemm_groupn_kernel) gives each of its problems its own range of workgroups. vstep must be a multiple
 // of the XCD count so a virtual block stays on its workgroup's XCD (xcd_remap).
-// Epilogue of a TRANSPOSED accumulator tile (pl4_run TRN: the MFMAs take B as their first operand, so each 16x16
-// block lands as C^T: lane l holds row l % 16, columns 4 (l / 16) .. +3), for bf16 outputs without an LDS round trip.
-// Per pair of 16-column blocks (j, j + 1) and 16-row block i: bias + ReLU in f32 (epi8_bf16's operations, in its
-// order), packed to bf16, then one v_permlane16_swap per dword exchanges rows 1 / 3 of block j's registers with rows
-// 0 / 2 of block j + 1's, after which every lane holds 8 consecutive columns of its row: one 16-B store (lanes of
-// row group g: columns (g & 1) * 16 + (g >> 1) * 8 of the pair). The ReLU mask zeroes bf16 halves (x * 0 rounds to
-// +0 either way). No staging, no LDS traffic, no waits: the wave's stores go out back to back.
-template <int MI, int NJ, int WTN, int EPI>
-__device__ __forceinline__ void store_tile_trn(const f32x4 (&acc)[MI][NJ], int lane, int row0, int col0,
-                                               bf16_t* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
-                                               const bf16_t* __restrict__ aux, int64_t ldaux) {
-  static_assert(NJ % 2 == 0, "pairs of 16-column blocks");
-  constexpr bool kBias = EPI == kEpiBias || EPI == kEpiBiasRelu;
-  constexpr bool kMask = EPI == kEpiReluMask;
-  const int g = lane >> 4, rl = lane & 15;
-  const int ocol = (g & 1) * 16 + (g >> 1) * 8;
-  auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
-  auto hi = [](uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); };
-  uint2 bq[kBias ? NJ : 1];
-  if constexpr (kBias) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) bq[j] = *reinterpret_cast<const uint2*>(bias + col0 + j * 16 + 4 * g);
-  }
-  constexpr int kPfd = 2;
-  uint4 aq[kMask ? MI : 1][kMask ? NJ / 2 : 1];
-  auto aux_load = [&](int i) __attribute__((always_inline)) {
-#pragma unroll
-    for (int jp = 0; jp < NJ / 2; ++jp)
-      aq[i][jp] = *reinterpret_cast<const uint4*>(aux + (int64_t)(row0 + i * 16 + rl) * ldaux + col0 + jp * 32 + ocol);
-  };
-  if constexpr (kMask) {
-#pragma unroll
-    for (int i = 0; i < kPfd && i < MI; ++i) aux_load(i);
-  }
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    if constexpr (kMask) {
-      if (i + kPfd < MI) aux_load(i + kPfd);
-    }
-#pragma unroll
-    for (int jp = 0; jp < NJ / 2; ++jp) {
-      float x[2][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[h][r] = acc[i][2 * jp + h][r];
-        if constexpr (kBias) {
-          const uint2 u = bq[2 * jp + h];
-          x[h][0] += lo(u.x); x[h][1] += hi(u.x); x[h][2] += lo(u.y); x[h][3] += hi(u.y);
-        }
-        if constexpr (EPI == kEpiBiasRelu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x[h][r] = fmaxf(x[h][r], 0.f);
-        }
-      }
-      uint32_t a0 = pack_bf16x2(x[0][0], x[0][1]), a1 = pack_bf16x2(x[0][2], x[0][3]);
-      uint32_t b0 = pack_bf16x2(x[1][0], x[1][1]), b1 = pack_bf16x2(x[1][2], x[1][3]);
-      const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
-      const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
-      uint32_t w[4] = {s0[0], s1[0], s0[1], s1[1]};
-      if constexpr (kMask) {
-        const uint4 m = aq[i][jp];
-        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t keep_lo = lo(mw[k]) > 0.f ? 0x0000FFFFu : 0u, keep_hi = hi(mw[k]) > 0.f ? 0xFFFF0000u : 0u;
-          w[k] &= keep_lo | keep_hi;
-        }
-      }
-      *reinterpret_cast<uint4*>(C + (int64_t)(row0 + i * 16 + rl) * ldc + col0 + jp * 32 + ocol) =
-          make_uint4(w[0], w[1], w[2], w[3]);
-    }
-  }
-}
-
 // OVL (256x256 bf16 outputs, persistent, no split-K / bias gradient; FAN_GEMM_OVL): the tile transitions overlap.
 // The epilogue stages through a region of its own beside the operand stages (64-column halves, 17 KiB), so the next
 // tile's K-tiles 0 and 1 are fetched under the last k-step of this tile (its MFMAs read no fragments, the stages are
 // free after its barrier), and the next tile waits only for its K-tile 0 (vmcnt(G + kS): the epilogue's kS stores
 // are the youngest) and then for K-tile 1 with those stores still allowed in flight — vmcnt counts loads, stores and
 // LDS-DMA together, in issue order (MI355X_MICROARCH.md). Same arithmetic: bit-identical to OVL off.
-// TRN (with OVL): the MFMAs take B first, so the accumulators hold C^T blocks and the epilogue stores straight from
-// registers (store_tile_trn). The products and their k order are the same: bit-identical (tests/test_gpu_gemm_ovl.py).
-// EDMA (with OVL, FAN_GEMM_EDMA): two barriers per K-tile instead of one, so the LDS-DMA of K-tile kt + 2 spreads over
-// most of both k-steps and each K-tile gets about twice the latency window. Barrier A, in k-step 0 once this wave's
-// reads of K-tile kt's k-step-1 fragments retired (lgkmcnt(0)), frees stage kt & 1 for that DMA; barrier B, in k-step
-// 1, waits (counted vmcnt: K-tile kt + 2's pieces issued so far may stay in flight) for K-tile kt + 1 and only then are
-// its k-step-0 fragments read, at a denser spacing. Without it the DMA waits for the single barrier between the
-// k-steps and all 16 pieces go out in k-step 1, the last ones 66 MFMAs before the next barrier needs them (the
-// library's hand-written gfx950 NT kernel splits its K-tile the same way, three barriers per K-tile). Same products,
-// same k order: bit-identical.
-#ifndef FAN_EDMA_RSP0
-#define FAN_EDMA_RSP0 2  // k-step 0: fragment-read spacing (MFMAs)
-#endif
-#ifndef FAN_EDMA_QA
-#define FAN_EDMA_QA 36  // k-step 0: barrier A before this MFMA
-#endif
-#ifndef FAN_EDMA_DSP
-#define FAN_EDMA_DSP 3  // DMA-piece spacing (MFMAs), from barrier A on
-#endif
-#ifndef FAN_EDMA_QB
-#define FAN_EDMA_QB 26  // k-step 1: barrier B before this MFMA
-#endif
-#ifndef FAN_EDMA_RSP1
-#define FAN_EDMA_RSP1 2  // k-step 1: fragment-read spacing after barrier B
-#endif
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false, bool TRN = false, bool EDMA = false>
+          int BM_ = 256, bool OVL = false>
 __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
                                         int64_t ldb, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                         const TC* __restrict__ aux, int64_t ldaux, int M, int N, int K, int split_k,
@@ -1294,29 +1066,12 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   constexpr int STAGES = BN == 128 ? 3 : 2;
   static_assert(RSP >= 1 && DSP >= 1 && G * DSP <= Q, "schedule");
   static_assert(!OVL || (BM == 256 && BN == 256 && !COLSUM && !SPLIT && !ACCUM && sizeof(TC) == 2 &&
-                         !is_wire_epi(EPI) && !is_bits_epi(EPI)),
+                         !is_wire_epi(EPI)),
                 "overlapped transitions: 256x256 bf16 tiles without split-K or bias gradient");
   constexpr int kSW = OVL ? 64 : WTN;                             // epilogue staging width
   constexpr int kS = MI * (WTN / kSW) * (16 / (64 / (kSW / 8)));  // the epilogue's stores per wave and tile
   constexpr int DSP2 = Q / (2 * G);                               // OVL: the next tile's two K-tiles in one k-step
   static_assert(!OVL || (G + kS <= 63 && DSP2 >= 1), "vmcnt range / schedule");
-  static_assert(!TRN || (OVL && (EPI == kEpiNone || EPI == kEpiBias || EPI == kEpiBiasRelu || EPI == kEpiReluMask)),
-                "transposed accumulators: the overlapped bf16 loop's plain / bias / ReLU / ReLU-mask epilogues");
-  static_assert(!TRN || kS == MI * NJ / 2, "one 16-B store per pair of 16-column blocks per 16-row block");
-  // EDMA: pieces 0 .. kE_P0 - 1 of K-tile kt + 2 go out in k-step 0 after barrier A, the rest in k-step 1 from MFMA 1;
-  // barrier B waits for all but the kE_NB pieces of kt + 2 issued before it
-  constexpr int kE_QA = FAN_EDMA_QA, kE_QB = FAN_EDMA_QB, kE_DSP = FAN_EDMA_DSP;
-  constexpr int kE_RSP0 = FAN_EDMA_RSP0, kE_RSP1 = FAN_EDMA_RSP1;
-  constexpr int kE_P0r = (Q - 2 - kE_QA) / kE_DSP + 1, kE_P0 = kE_P0r < G ? kE_P0r : G;
-  constexpr int kE_N1r = (kE_QB - 1 + kE_DSP - 1) / kE_DSP, kE_N1 = kE_N1r < G - kE_P0 ? kE_N1r : G - kE_P0;
-  constexpr int kE_NB = kE_P0 + kE_N1;
-  static_assert(!EDMA || (OVL && STAGES == 2), "EDMA: the overlapped 256x256 loop");
-  static_assert(!EDMA || (kE_QA + 1 + kE_DSP * (kE_P0 - 1) <= Q - 1 && (kE_P0 == G || kE_QA + 1 + kE_DSP * kE_P0 > Q - 1) &&
-                          (kE_P0 + kE_N1 == G || 1 + kE_DSP * kE_N1 >= kE_QB) && 1 + kE_DSP * (G - kE_P0 - 1) <= Q - 1),
-                "EDMA: every piece of K-tile kt + 2 is issued once, in one of the two k-steps");
-  static_assert(!EDMA || (kE_RSP0 * (R - 1) < kE_QA && kE_QA < Q && kE_QB >= 1 && kE_QB + kE_RSP1 * (R - 1) < Q &&
-                          kE_NB <= 63),
-                "EDMA schedule");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
@@ -1401,8 +1156,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
         if (next_on) piece(q / DSP2 / G, std::integral_constant<int, q / DSP2 % G>{});
       }
 #endif
-      if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[cur][q % NJ], fa[cur][q / NJ]);
-      else mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
+      mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
     });
   };
   using I0 = std::integral_constant<int, 0>;
@@ -1433,43 +1187,6 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     FAN_STAMP(0);
     if constexpr (STAGES == 2) {
       constexpr bool kLast = OVL && !decltype(more_c)::value && !decltype(more2_c)::value;
-      if constexpr (EDMA && !kLast) {
-        constexpr bool MORE = decltype(more_c)::value, MORE2 = decltype(more2_c)::value;
-        const char* st1 = smem + ((kt + 1) & 1) * STAGE;
-        // k-step 0 (set 0): K-tile kt's k-step-1 fragments into set 1; barrier A; K-tile kt + 2's first pieces
-        static_for<Q>([&](auto qc) __attribute__((always_inline)) {
-          constexpr int q = decltype(qc)::value;
-          if constexpr (q % kE_RSP0 == 0 && q / kE_RSP0 < R) read_next(st, 1, 1, q / kE_RSP0);
-          if constexpr (MORE2 && q == kE_QA) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-          }
-#ifndef FAN_GEMM_NODMA
-          if constexpr (MORE2 && q > kE_QA && (q - kE_QA - 1) % kE_DSP == 0 && (q - kE_QA - 1) / kE_DSP < kE_P0)
-            piece(kt + 2, std::integral_constant<int, (q - kE_QA - 1) / kE_DSP>{});
-#endif
-          if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[0][q % NJ], fa[0][q / NJ]);
-          else mfma_acc(acc[q / NJ][q % NJ], fa[0][q / NJ], fb[0][q % NJ]);
-        });
-        // k-step 1 (set 1): the rest of K-tile kt + 2; barrier B (K-tile kt + 1 landed in every wave); its k-step-0
-        // fragments into set 0
-        static_for<Q>([&](auto qc) __attribute__((always_inline)) {
-          constexpr int q = decltype(qc)::value;
-#ifndef FAN_GEMM_NODMA
-          if constexpr (MORE2 && q >= 1 && (q - 1) % kE_DSP == 0 && kE_P0 + (q - 1) / kE_DSP < G)
-            piece(kt + 2, std::integral_constant<int, kE_P0 + (q - 1) / kE_DSP>{});
-#endif
-          if constexpr (MORE && q == kE_QB) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MORE2 ? kE_NB : 0) : "memory");
-            __builtin_amdgcn_s_barrier();
-          }
-          if constexpr (MORE && q >= kE_QB && (q - kE_QB) % kE_RSP1 == 0 && (q - kE_QB) / kE_RSP1 < R)
-            read_next(st1, 0, 0, (q - kE_QB) / kE_RSP1);
-          if constexpr (TRN) mfma_acc(acc[q / NJ][q % NJ], fb[1][q % NJ], fa[1][q / NJ]);
-          else mfma_acc(acc[q / NJ][q % NJ], fa[1][q / NJ], fb[1][q % NJ]);
-        });
-        return;
-      }
       if constexpr (kLast) {
         // the last K-tile: this tile's offsets are dead (its last DMA went out two K-tiles ago); the next tile's
         // (if any) take their place, for the DMA of its K-tiles 0 and 1 in k-step 1 below
@@ -1533,10 +1250,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     colsum_finish<NJ, WTN, kEpiNone, true>(
         cs, lane, n0 + wn * WTN, ws + (SPLIT ? (int64_t)split_k * M * N + (int64_t)ksplit * N : (int64_t)im * N), wo,
         N);
-  if constexpr (TRN) {
-    store_tile_trn<MI, NJ, WTN, EPI>(acc, lane, m0 + wm * WTM, n0 + wn * WTN, reinterpret_cast<bf16_t*>(C), ldc, bias,
-                                     reinterpret_cast<const bf16_t*>(aux), ldaux);
-  } else if constexpr (OVL) {
+  if constexpr (OVL) {
     // staging rows of its own (wave-private) beside the operand stages: nothing to wait for (the operand reads
     // retired before the last barrier; the next tile's DMA into the stages must stay in flight)
     store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT, kSW>(acc, smem + 2 * STAGE, wave, lane, m0 + wm * WTM,
@@ -1546,9 +1260,6 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     __syncthreads();  // every operand read retired before the epilogue reuses the LDS
     store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
                                                    aux, ldaux, M, N, ksplit, ws, wo);
-  }
-  if constexpr (SPLIT && is_wire_epi(EPI)) {
-    if (wo.fix) split_fixup<BM, BN>(tile, m0, n0, ws, split_k, reinterpret_cast<float*>(C), ldc, M, N, colsum, wo, smem);
   }
   };
   if constexpr (COLSUM) {
@@ -1564,22 +1275,21 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 }
 
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false, bool TRN = false, bool EDMA = false>
+          int BM_ = 256, bool OVL = false>
 __global__ void __launch_bounds__(256, 1)
     gemm_pl4_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
                     float* __restrict__ colsum, WireOut wo) {
-  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_, OVL, TRN, EDMA>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M,
+  pl4_run<AK, BKC, EPI, TC, ACCUM, SPLIT, COLSUM, BN_, BM_, OVL>(A, lda, B, ldb, C, ldc, bias, aux, ldaux, M,
                                                                            N, K, split_k, ws, colsum, wo,
                                                                            (int)blockIdx.x, (int)gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Grouped launch of two independent GEMMs (e.g. a layer's bwd-data and bwd-weight, which the reference runs as one
-// libxsmm PASS_BWD call, sw/mlp_mpi_example_f32.cpp:741-742): workgroups [0, grid0) run problem 0's tiles, the rest
-// problem 1's, each persistent over its own tile list. One dispatch instead of two, and the two problems' epilogues
-// (HBM-write phases) fall at different times on different CUs instead of every CU writing at once.
+// One GEMM problem of a grouped launch (gemm_groupn_kernel) and its compile-time configuration. (A grouped launch of a
+// layer's bwd-data + bwd-weight, the libxsmm PASS_BWD shape, measured no faster than two launches in round 5 and was
+// removed: profiles/r5_gemm_bwd_pair_ab.jsonl.)
 template <typename TC>
 struct PlProblem {
   const bf16_t* A;
@@ -1609,13 +1319,6 @@ struct PlCfg {
   }
 };
 
-template <class P0, class P1>
-__global__ void __launch_bounds__(256, 1)
-    gemm_group2_kernel(PlProblem<typename P0::TC> p0, PlProblem<typename P1::TC> p1, int grid0) {
-  if ((int)blockIdx.x < grid0) P0::run(p0, (int)blockIdx.x, grid0);
-  else P1::run(p1, (int)blockIdx.x - grid0, (int)gridDim.x - grid0);
-}
-
 // Grouped launch of up to kMaxGroup GEMMs of ONE configuration P, one tile per workgroup (P with the fused bias
 // gradient): problem i owns workgroups [first[i], first[i + 1]), a range padded to a multiple of the XCD count so
 // its local tile index keeps blockIdx.x's XCD (xcd_remap); the padding workgroups find no tile and exit. For a
@@ -1635,319 +1338,6 @@ __global__ void __launch_bounds__(256, 1) gemm_groupn_kernel(PlGroup<typename P:
   int i = 0;
   while (i + 1 < g.n && b >= g.first[i + 1]) ++i;  // workgroup-uniform
   P::run(g.p[i], b - g.first[i], g.first[i + 1] - g.first[i]);
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// The same 256x256 4-wave AGPR loop on a ring of FOUR half-stages (32 k each, 32 KiB: the LDS of the two 64-k
-// stages above) with one barrier per k-step instead of per K-tile. Why: the LDS-DMA issue is the loop's limiter
-// (a diagnostic build without the in-loop DMA, -DFAN_GEMM_NODMA, runs the big GEMMs 12-13 % faster:
-// profiles/r4_gemm_nodma_ab.jsonl), and in gemm_pl4_kernel all 16 pieces of a K-tile go into k-step 1, the step
-// that also carries the next step's 16 fragment reads, while k-step 0 carries none (a stage can only be refilled
-// after the mid-tile barrier). Here every k-step carries 8 pieces + 16 reads + 64 MFMAs:
-//   k-step h: MFMAs on the fragments of half-stage h (registers, set h & 1); under them the fragments of h + 1 are
-//   read (stage (h + 1) % 4, set (h + 1) & 1) and the DMA of half-stage h + 3 goes into stage (h + 3) % 4 = the
-//   stage of h - 1, whose reads every wave retired before the barrier that ended k-step h - 2; then lgkmcnt(0) +
-//   vmcnt(8) (this wave's pieces of h + 2 landed; those of h + 3 may stay in flight) and ONE barrier (asm
-//   s_barrier with a memory clobber: the builtin does not stop the compiler from hoisting LDS reads above it).
-// Every step runs the same body (reads and fetch clamped past the end): one loop, 178 VGPRs, no spills.
-// MEASURED SLOWER (profiles/r4_gemm_half_stage_ab.jsonl: +4.8 % on the 8192x4096x4096 forward, +8.3 % on the
-// flagship step): the extra barrier per K-tile and the half-size DMA bursts cost more than the issue clustering they
-// remove. Kept opt-in (FAN_GEMM_HALF=1) and bit-identical (tests/test_gpu_gemm_half_stage.py).
-// A half-stage's DMA has two k-steps to land, as before. Images: K-contiguous operands as [rows][32 k] (64-B rows,
-// 16-B chunk c of row r at slot c ^ ((r >> 1) & 3): conflict-free ds_read_b128), MN-contiguous ones as
-// [32 k][128 columns] per 128-column half (the ds_read_b64_tr_b16 image of gemm_pl4_kernel, 32 k-rows). The
-// MFMAs run in the same k order, so results are bit-identical to gemm_pl4_kernel.
-template <bool KCONTIG, int OUTER, int NT>
-__device__ __forceinline__ uint32_t piece_off_h(int64_t ld, int o0, int wave, int lane, int i) {
-  constexpr int IB = NT * 16;
-  const int t = wave * 64 + lane;
-  if (KCONTIG) {
-    const int row = i * (IB / 64) + (t >> 2);  // rows of 64 B
-    const int c = (t & 3) ^ ((row >> 1) & 3);
-    return (uint32_t)(((int64_t)(o0 + row) * ld + c * 8) * 2);
-  } else {
-    constexpr int PER_HALF = (32 * 256) / IB;
-    const int half = i / PER_HALF;
-    const int krow = (i % PER_HALF) * (IB / 256) + (t >> 4);  // k-rows of 256 B
-    const int cs = t & 15;
-    const int blk = (cs >> 1) ^ mn_swz(krow);
-    return (uint32_t)(((int64_t)krow * ld + o0 + half * 128 + blk * 16 + (cs & 1) * 8) * 2);
-  }
-}
-
-template <bool KCONTIG>
-__device__ __forceinline__ s16x8 read_frag_h(const char* lds, int o, int lane) {
-  if (KCONTIG) {
-    const int row = o + (lane & 15);
-    const int chunk = lane >> 4;
-    return *reinterpret_cast<const s16x8*>(lds + row * 64 + ((chunk ^ ((row >> 1) & 3)) << 4));
-  } else {
-    const char* h = lds + (o >> 7) * (32 * 256);
-    const int oo = o & 127;
-    const int q = (lane & 15) >> 2, p = lane & 3;
-    const int kb = 8 * (lane >> 4) + q;
-    const int blk = oo >> 4;
-    const int off0 = kb * 256 + ((blk ^ mn_swz(kb)) << 5) + 8 * p;
-    const int off1 = (kb + 4) * 256 + ((blk ^ mn_swz(kb + 4)) << 5) + 8 * p;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(h + off0));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(h + off1));
-    s16x8 r;
-    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-    return r;
-  }
-}
-
-template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false>
-__global__ void __launch_bounds__(256, 1)
-    gemm_pl4h_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
-                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
-                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
-                     float* __restrict__ colsum, WireOut wo) {
-  constexpr int BM = 256, BN = 256, NT = 256, HK = 32, IB = NT * 16;
-  constexpr int A_BYTES = BM * HK * 2, STAGE = A_BYTES + BN * HK * 2;  // 16 + 16 KiB
-  constexpr int GA = A_BYTES / IB, G = GA + BN * HK * 2 / IB;         // 4 + 4 pieces per wave and half-stage
-  constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NJ = WTN / 16;
-  constexpr int Q = MI * NJ, R = MI + NJ;
-  constexpr int RSP = (Q * 3 / 4) / R, DSP = Q / G;  // 3 and 8
-  static_assert(RSP >= 1 && DSP >= 1 && G * DSP <= Q, "schedule");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / 2, wn = wave % 2;
-  const uint32_t lds0 = lds_addr_of(smem);
-  auto tile_body = [&](int v) __attribute__((always_inline)) {
-  const int wg = xcd_remap(v, tiles * split_k);
-  const int tile = wg % tiles, ksplit = wg / tiles;
-  const int GM = tiles_m >= 4 ? 4 : tiles_m;
-  const int grp = tile / (GM * tiles_n);
-  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
-  const int in_grp = tile % (GM * tiles_n);
-  const int m0 = (grp * GM + in_grp % gm) * BM;
-  const int n0 = (in_grp / gm) * BN;
-  const int k_per = K / split_k;
-  const int kbeg = ksplit * k_per;
-  const int nh = k_per / HK;
-
-  const int im = SPLIT ? 0 : m0 / BM;
-  const int cs0 = SPLIT ? (m0 == 0 ? 0 : nh) : im * nh / tiles_m;
-  const int cs1 = SPLIT ? nh : (im + 1) * nh / tiles_m;
-  const bool do_colsum = COLSUM && wm == 0;
-  float cs[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) cs[j] = 0.f;
-
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 fa[2][MI], fb[2][NJ];
-
-  uint32_t off[G];
-#pragma unroll
-  for (int p = 0; p < GA; ++p) off[p] = piece_off_h<AK, BM, NT>(lda, m0, wave, lane, p);
-#pragma unroll
-  for (int p = GA; p < G; ++p) off[p] = piece_off_h<BKC, BN, NT>(ldb, n0, wave, lane, p - GA);
-  const int64_t a_step = AK ? (int64_t)HK * 2 : (int64_t)HK * lda * 2;
-  const int64_t b_step = BKC ? (int64_t)HK * 2 : (int64_t)HK * ldb * 2;
-  const char* a_k0 = reinterpret_cast<const char*>(A) + (AK ? (int64_t)kbeg * 2 : (int64_t)kbeg * lda * 2);
-  const char* b_k0 = reinterpret_cast<const char*>(B) + (BKC ? (int64_t)kbeg * 2 : (int64_t)kbeg * ldb * 2);
-
-  // glds piece p of half-stage `src` (clamped by the caller to the last one) into LDS stage `stg` & 3
-  auto piece = [&](int stg, int src, int p) __attribute__((always_inline)) {
-    const uint32_t st = lds0 + (stg & 3) * STAGE + wave * 1024;
-    if (p < GA) glds16_s(a_k0 + src * a_step, off[p], st + p * IB);
-    else glds16_s(b_k0 + src * b_step, off[p], st + A_BYTES + (p - GA) * IB);
-  };
-  auto read_next = [&](const char* st, int set, int r) __attribute__((always_inline)) {
-    if (r < MI) fa[set][r] = read_frag_h<AK>(st, wm * WTM + r * 16, lane);
-    else fb[set][r - MI] = read_frag_h<BKC>(st + A_BYTES, wn * WTN + (r - MI) * 16, lane);
-  };
-  auto block = [&](auto cur_c, auto read_c, auto dma_c, const char* rd_st, int dma_stg, int dma_src,
-                   bool csk) __attribute__((always_inline)) {
-    constexpr int cur = decltype(cur_c)::value;
-    constexpr bool READ = decltype(read_c)::value, DMA = decltype(dma_c)::value;
-    if (COLSUM && csk)
-      static_for<NJ>([&](auto jc) __attribute__((always_inline)) { cs[jc.value] += frag_sum(fb[cur][jc.value]); });
-    static_for<MI * NJ>([&](auto qc) __attribute__((always_inline)) {
-      constexpr int q = decltype(qc)::value;
-      if constexpr (READ && q % RSP == 0 && q / RSP < R) read_next(rd_st, cur ^ 1, q / RSP);
-#ifndef FAN_GEMM_NODMA
-      if constexpr (DMA && q % DSP == DSP / 2 && q / DSP < G) piece(dma_stg, dma_src, q / DSP);
-#endif
-      mfma_acc(acc[q / NJ][q % NJ], fa[cur][q / NJ], fb[cur][q % NJ]);
-    });
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-
-  // prologue: half-stages 0, 1, 2 in flight (past the end: the last one again); retire 0 AND 1 (step 0 reads the
-  // fragments of 1; only 2 may stay in flight), barrier, read the fragments of 0
-#pragma unroll
-  for (int p = 0; p < G; ++p) piece(0, 0, p);
-#pragma unroll
-  for (int p = 0; p < G; ++p) piece(1, min(1, nh - 1), p);
-#pragma unroll
-  for (int p = 0; p < G; ++p) piece(2, min(2, nh - 1), p);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-  asm volatile("s_barrier" ::: "memory");
-#pragma unroll
-  for (int r = 0; r < R; ++r) read_next(smem, 0, r);
-
-  // one k-step h (set h & 1): the fragments of h + 1 are read and half-stage h + 3 is fetched on EVERY step; past
-  // the end both are clamped to valid memory (the last half-stage fetched again into a consumed stage, fragments
-  // nobody uses), which keeps one loop body (a tail with compile-time flags doubles the live ranges: spills)
-  auto kstep = [&](int h, auto cur_c) __attribute__((always_inline)) {
-    const bool csk = do_colsum && h >= cs0 && h < cs1;
-    block(cur_c, T_{}, T_{}, smem + ((h + 1) & 3) * STAGE, h + 3, min(h + 3, nh - 1), csk);
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(G) : "memory");
-    asm volatile("s_barrier" ::: "memory");
-  };
-  for (int h = 0; h < nh; h += 2) {  // nh is even (K % 64 == 0): pairs keep the register set a constant
-    kstep(h, I0{});
-    kstep(h + 1, I1{});
-  }
-
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
-  if (COLSUM && do_colsum && (!SPLIT || m0 == 0))
-    colsum_finish<NJ, WTN, kEpiNone, true>(
-        cs, lane, n0 + wn * WTN, ws + (SPLIT ? (int64_t)split_k * M * N + (int64_t)ksplit * N : (int64_t)im * N), wo,
-        N);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
-                                                 aux, ldaux, M, N, ksplit, ws, wo);
-  if constexpr (SPLIT && is_wire_epi(EPI)) {
-    if (wo.fix) split_fixup<BM, BN>(tile, m0, n0, ws, split_k, reinterpret_cast<float*>(C), ldc, M, N, colsum, wo, smem);
-  }
-  };
-  if constexpr (COLSUM) {
-    tile_body(blockIdx.x);
-  } else {
-    for (int v = blockIdx.x; v < tiles * split_k; v += gridDim.x) {
-      tile_body(v);
-      __syncthreads();
-    }
-  }
-}
-
-// Two workgroups per CU (occupancy 2: two waves per SIMD from DIFFERENT workgroups). 256x128 tiles, 4 waves of
-// 128x64 (128 AGPR accumulators), a ring of THREE 32-k half-stages (24 KiB each: 72 KiB per workgroup, 144 per CU),
-// one barrier per half-stage. Why: in gemm_pl4_kernel (one wave per SIMD) the SIMD idles whenever its only wave
-// stalls — on the LDS-DMA issue (a build without it is 12-13 % faster), the barrier, the fragment reads, the
-// epilogue's stores — and every CU writes its tile's output at the same moment. Two independent workgroups per CU
-// stall at different times (their barriers are their own), so one's MFMAs fill the other's stalls, and their
-// epilogues fall at different times. The 8-wave gemm_pl_kernel also ran two waves per SIMD, but of ONE workgroup,
-// sharing its barriers and DMA phases. Fragments single-buffered (the other workgroup covers the read latency):
-//   half-stage h: wait own pieces of h (vmcnt(G): h + 1's may stay in flight), barrier (everyone's pieces of h
-//   landed, everyone's reads of h - 1 retired), DMA of h + 2 into stage (h + 2) % 3 = the stage of h - 1, the 12
-//   fragment reads of h, 32 MFMAs.
-// Same k order as gemm_pl4_kernel's 256x128 tiles: bit-identical results. Opt-in (FAN_GEMM_OCC2=1): it replaces the
-// persistent 256x256 kernel of unsplit, bias-gradient-free plans.
-template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM>
-__global__ void __launch_bounds__(256, 2)
-    gemm_pl2h_kernel(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B, int64_t ldb,
-                     TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias, const TC* __restrict__ aux,
-                     int64_t ldaux, int M, int N, int K, int split_k, float* __restrict__ ws,
-                     float* __restrict__ colsum, WireOut wo) {
-  constexpr int BM = 256, BN = 128, NT = 256, HK = 32, IB = NT * 16;
-  constexpr int A_BYTES = BM * HK * 2, STAGE = A_BYTES + BN * HK * 2;  // 16 + 8 KiB
-  constexpr int GA = A_BYTES / IB, G = GA + BN * HK * 2 / IB;         // 4 + 2 pieces per wave and half-stage
-  constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NJ = WTN / 16;
-  constexpr int Q = MI * NJ, DSP = Q / G;  // 32 MFMAs, a DMA piece every 5
-  static_assert(G * DSP <= Q, "schedule");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  (void)split_k; (void)colsum;
-
-  const int tiles_n = N / BN, tiles_m = M / BM, tiles = tiles_m * tiles_n;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / 2, wn = wave % 2;
-  const uint32_t lds0 = lds_addr_of(smem);
-  auto tile_body = [&](int v) __attribute__((always_inline)) {
-  const int tile = xcd_remap(v, tiles);
-  const int GM = tiles_m >= 4 ? 4 : tiles_m;
-  const int grp = tile / (GM * tiles_n);
-  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
-  const int in_grp = tile % (GM * tiles_n);
-  const int m0 = (grp * GM + in_grp % gm) * BM;
-  const int n0 = (in_grp / gm) * BN;
-  const int nh = K / HK;
-
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  uint32_t off[G];
-#pragma unroll
-  for (int p = 0; p < GA; ++p) off[p] = piece_off_h<AK, BM, NT>(lda, m0, wave, lane, p);
-#pragma unroll
-  for (int p = GA; p < G; ++p) off[p] = piece_off_h<BKC, BN, NT>(ldb, n0, wave, lane, p - GA);
-  const int64_t a_step = AK ? (int64_t)HK * 2 : (int64_t)HK * lda * 2;
-  const int64_t b_step = BKC ? (int64_t)HK * 2 : (int64_t)HK * ldb * 2;
-  const char* a_k0 = reinterpret_cast<const char*>(A);
-  const char* b_k0 = reinterpret_cast<const char*>(B);
-
-  // glds piece p of half-stage `src` (clamped by the caller) into LDS stage `stg` (0..2)
-  auto piece = [&](int stg, int src, int p) __attribute__((always_inline)) {
-    const uint32_t st = lds0 + stg * STAGE + wave * 1024;
-    if (p < GA) glds16_s(a_k0 + src * a_step, off[p], st + p * IB);
-    else glds16_s(b_k0 + src * b_step, off[p], st + A_BYTES + (p - GA) * IB);
-  };
-
-  // prologue: half-stages 0 and 1 in flight
-#pragma unroll
-  for (int p = 0; p < G; ++p) piece(0, 0, p);
-#pragma unroll
-  for (int p = 0; p < G; ++p) piece(1, min(1, nh - 1), p);
-
-  int st = 0;  // stage of h
-  for (int h = 0; h < nh; ++h) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-    asm volatile("s_barrier" ::: "memory");
-    const char* rd = smem + st * STAGE;
-    const int dst = st == 0 ? 2 : st - 1;  // (h + 2) % 3
-    const int src = min(h + 2, nh - 1);    // past the end: the last half-stage again (keeps vmcnt's count)
-    s16x8 fa[MI], fb[NJ];
-#pragma unroll
-    for (int r = 0; r < MI; ++r) fa[r] = read_frag_h<AK>(rd, wm * WTM + r * 16, lane);
-#pragma unroll
-    for (int r = 0; r < NJ; ++r) fb[r] = read_frag_h<BKC>(rd + A_BYTES, wn * WTN + r * 16, lane);
-    static_for<Q>([&](auto qc) __attribute__((always_inline)) {
-      constexpr int q = decltype(qc)::value;
-#ifndef FAN_GEMM_NODMA
-      if constexpr (q % DSP == 0 && q / DSP < G) piece(dst, src, q / DSP);
-#endif
-      mfma_acc(acc[q / NJ][q % NJ], fa[q / NJ], fb[q % NJ]);
-    });
-    st = st == 2 ? 0 : st + 1;
-  }
-
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(acc[i][j]));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail pieces write the LDS too
-  __syncthreads();
-  store_tile<MI, NJ, WTN, EPI, TC, ACCUM, false>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
-                                                 aux, ldaux, M, N, 0, ws, wo);
-  };
-  for (int v = blockIdx.x; v < tiles; v += gridDim.x) {
-    tile_body(v);
-    __syncthreads();  // every wave's staging reads done before the next tile's DMA overwrites the LDS
-  }
 }
 
 // Ordered split-K reduction + epilogue (deterministic: slabs summed in split order). SK > 0: the split count as a
@@ -2188,16 +1578,9 @@ inline int persist_grid(int grid) {
 
 // Launches the main loop; returns the number of bias-gradient partial slabs it left in the workspace for an ordered
 // reduce (split_k with split-K; without: the pipelined loop's tile rows, 0 = colsum written by the kernel).
-// With wo.fix set (split-K wire epilogue), the 4-wave pipelined kernels reduce the slabs themselves (split_fixup)
-// and *fixed says so; every other kernel leaves them to the reduce kernel.
 template <int BM, int BN, int WM, int WN, bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT>
-int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, bool* fixed = nullptr) {
+int launch_main(const GemmArgs& a, int sk, const WireOut& wo, hipStream_t s) {
   const int grid = cdiv_i(a.M, BM) * cdiv_i(a.N, BN) * sk;
-  WireOut wo = wo_in;  // the kernels without the fixup get no counters
-  wo.fix = nullptr;
-  WireOut wf = wo_in;  // the 4-wave pipelined kernels'
-  if (!(SPLIT && is_wire_epi(EPI)) || grid / sk > kFixTiles) wf.fix = nullptr;
-  if (fixed) *fixed = false;
   if constexpr (BM == 256 && BN == 256 && WM * WN == 8) {
     // the pipelined loops have no edge path: aligned shapes only
     const int mode = main_loop_mode();
@@ -2211,29 +1594,21 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
     // (and the in-kernel wire encode: since the 4-wave kernel became persistent, the 4096^2 bwd-weight with the wire
     // + bias-gradient epilogue runs faster in the step there, 1.036-1.038 vs 1.042-1.052 ms/step,
     // profiles/r2_pl3_wire_ab.txt; in isolation it measured +13 vs +7 us for the encode)
-    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192 || EPI == kEpiReluMask || is_bits_epi(EPI)));
+    const bool pl4 = mode == 3 || (mode == 2 && (!BKC || a.K / sk >= 8192 || EPI == kEpiReluMask));
     if (pl4 && aligned && (!a.colsum || a.workspace)) {
       constexpr int lds = 2 * (BM + BN) * BK * 2;
       auto launch = [&](auto k, bool persist) {  // persist: the kernel loops over tiles (not with colsum)
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
                            (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
-                           (float*)a.workspace, a.colsum, wf);
-        if (fixed) *fixed = wf.fix != nullptr;
+                           (float*)a.workspace, a.colsum, wo);
       };
-      const bool half = gemm_half_stage_flag().load(std::memory_order_relaxed) != 0;
-      if constexpr (!SPLIT && !ACCUM && sizeof(TC) == 2 && !is_wire_epi(EPI) && !is_bits_epi(EPI)) {
-        // overlapped tile transitions (pl4_run OVL, opt-in)
-        if (gemm_ovl_flag().load(std::memory_order_relaxed) != 0 && !a.colsum && sk == 1 && !half &&
+      if constexpr (!SPLIT && !ACCUM && sizeof(TC) == 2 && !is_wire_epi(EPI)) {
+        // overlapped tile transitions (pl4_run OVL, default on)
+        if (gemm_ovl_flag().load(std::memory_order_relaxed) != 0 && !a.colsum && sk == 1 &&
             a.K >= 2 * BK) {  // (the last k-step fetches the next tile's K-tiles 0 AND 1)
           constexpr int lds_o = 2 * (BM + BN) * BK * 2 + 4 * 16 * (64 + 4) * 4;
-          // (not with the ReLU-mask epilogue: its activation loads, 16 rows x 64 B per instruction in the
-          // transposed layout, measured slower than the staged 4 rows x 256 B: profiles/r5_gemm_trn_ab.txt)
-          const bool trn = gemm_trn_flag().load(std::memory_order_relaxed) != 0 && EPI != kEpiReluMask;
-          const bool edma = gemm_edma_flag().load(std::memory_order_relaxed) != 0;
-          auto k = trn ? gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, true>
-                       : edma ? gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, false, true>
-                              : gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true, false>;
+          auto k = gemm_pl4_kernel<AK, BKC, EPI, TC, false, false, false, 256, 256, true>;
           FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds_o));
           hipLaunchKernelGGL(k, persist_grid(grid), 256, lds_o, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B,
                              a.ldb, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K,
@@ -2241,30 +1616,13 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
           return 0;
         }
       }
-      if constexpr (!SPLIT && !is_wire_epi(EPI)) {
-        // two workgroups per CU on 256x128 tiles (gemm_pl2h_kernel, opt-in)
-        if (gemm_occ2_flag().load(std::memory_order_relaxed) != 0 && !a.colsum && sk == 1 && a.K % 32 == 0) {
-          constexpr int lds2 = 3 * (256 + 128) * 32 * 2;
-          auto k = gemm_pl2h_kernel<AK, BKC, EPI, TC, ACCUM>;
-          FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds2));
-          const int tiles2 = (a.M / 256) * (a.N / 128);
-          const int cap = gemm_persist_flag().load(std::memory_order_relaxed);
-          const int g2 = cap > 0 && tiles2 > 2 * cap ? 2 * cap : tiles2;
-          hipLaunchKernelGGL(k, g2, 256, lds2, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb, (TC*)a.C,
-                             a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, 1,
-                             (float*)a.workspace, a.colsum, wo);
-          return 0;
-        }
-      }
       if constexpr (!BKC) {
         if (a.colsum) {
-          if (half) launch(gemm_pl4h_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);
-          else launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);
+          launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, true>, false);
           return SPLIT ? sk : a.M / BM;
         }
       }
-      if (half) launch(gemm_pl4h_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>, true);
-      else launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>, true);
+      launch(gemm_pl4_kernel<AK, BKC, EPI, TC, ACCUM, SPLIT, false>, true);
       return 0;
     }
     if ((mode == 2 || mode == 5) && aligned && (!a.colsum || a.workspace)) {
@@ -2297,8 +1655,7 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda,
                            (const bf16_t*)a.B, a.ldb, (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux,
-                           a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace, a.colsum, wf);
-        if (fixed) *fixed = wf.fix != nullptr;
+                           a.ldaux, a.M, a.N, a.K, sk, (float*)a.workspace, a.colsum, wo);
       };
       if constexpr (!BKC) {
         if (a.colsum) {
@@ -2322,8 +1679,7 @@ int launch_main(const GemmArgs& a, int sk, const WireOut& wo_in, hipStream_t s, 
         FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         hipLaunchKernelGGL(k, persist ? persist_grid(grid) : grid, 256, lds, s, (const bf16_t*)a.A, a.lda, (const bf16_t*)a.B, a.ldb,
                            (TC*)a.C, a.ldc, (const bf16_t*)a.bias, (const TC*)a.aux, a.ldaux, a.M, a.N, a.K, sk,
-                           (float*)a.workspace, a.colsum, wf);
-        if (fixed) *fixed = wf.fix != nullptr;
+                           (float*)a.workspace, a.colsum, wo);
       };
       if constexpr (!BKC) {
         if (a.colsum) {
@@ -2386,9 +1742,7 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   WireOut wo{a.wire, a.wire_shard, a.wire_own, a.wire_period, a.wire_codec,
                    a.wire_shard > 0 ? 1.0f / (float)a.wire_shard : 0.f,
                    a.colsum && a.wire ? (int)(a.wire_off + (int64_t)a.M * a.ldc) : 0,
-                   a.upd_master, a.upd_lp, a.upd_mom, a.upd,
-                   sk > 1 && is_wire_epi(EPI) && gemm_fixup_flag().load(std::memory_order_relaxed) != 0
-                       ? gemm_fix_counters(s) : nullptr
+                   a.upd_master, a.upd_lp, a.upd_mom, a.upd
 #ifdef FAN_GEMM_STAMPS
                    , (unsigned long long*)gemm_stamp_buffer()
 #endif
@@ -2396,20 +1750,13 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   wo.off = (uint32_t)a.wire_off;
   wo.prio = gemm_prio_flag().load(std::memory_order_relaxed);
 
-  if constexpr (is_bits_epi(EPI)) {  // no split-K (the 4-column reduce path cannot write mask bytes)
-    FAN_CHECK(sk == 1, "mask-bit epilogues: no split-K");
-    launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>(a, sk, wo, s);
-    return;
-  }
   if (sk > 1) {
     // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + p*N]), then an ordered reduce that
     // applies the epilogue (deterministic: slabs summed in split order)
     // (the split main loop only writes slabs: the wire / update variants share one kernel)
     constexpr int kMainEpi = EPI == kEpiWireUpd ? kEpiWire : EPI;
-    bool fixed = false;  // the slabs already reduced in the GEMM (split_fixup)
-    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, kMainEpi, TC, ACCUM, true>(a, sk, wo, s, &fixed);
+    const int parts = launch_main<BM, BN, WM, WN, AK, BKC, kMainEpi, TC, ACCUM, true>(a, sk, wo, s);
     if constexpr (is_wire_epi(EPI)) {
-      if (fixed) return;
       const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
       const bool lane4 = gemm_reduce4_flag().load(std::memory_order_relaxed) != 0;
       with_split_count(sk, [&](auto skc) {
@@ -2452,14 +1799,6 @@ void launch_epi(const GemmArgs& a, int sk, hipStream_t s) {
     FAN_EPI_CASE(kEpiBias)
     FAN_EPI_CASE(kEpiBiasRelu)
     FAN_EPI_CASE(kEpiReluMask)
-    case kEpiBiasReluBits:  // mask-bit epilogues: bf16 output only (the 8-column store path writes / reads the bits)
-      FAN_CHECK(a.c_bf16 && !a.accumulate, "mask-bit epilogues: bf16 output, no accumulate");
-      launch_typed<BM, BN, WM, WN, AK, BKC, kEpiBiasReluBits, bf16_t, false>(a, sk, s);
-      break;
-    case kEpiReluBits:
-      FAN_CHECK(a.c_bf16 && !a.accumulate, "mask-bit epilogues: bf16 output, no accumulate");
-      launch_typed<BM, BN, WM, WN, AK, BKC, kEpiReluBits, bf16_t, false>(a, sk, s);
-      break;
     case kEpiWire:  // only the bwd-weight layout (A and B MN-contiguous) produces wire-ready gradients
       if constexpr (!AK && !BKC) {
         FAN_CHECK(!a.c_bf16 && !a.accumulate, "wire epilogue: f32, no accumulate");

@@ -51,34 +51,10 @@ std::atomic<int>& gemm_ovl_flag() {
   return flag;
 }
 
-std::atomic<int>& gemm_trn_flag() {
-  static std::atomic<int> flag{[] {
-    const char* e = getenv("FAN_GEMM_TRN");
-    return e && e[0] == '1' ? 1 : 0;
-  }()};
-  return flag;
-}
-
-std::atomic<int>& gemm_edma_flag() {
-  static std::atomic<int> flag{[] {
-    const char* e = getenv("FAN_GEMM_EDMA");
-    return e && e[0] == '1' ? 1 : 0;
-  }()};
-  return flag;
-}
-
 std::atomic<int>& gemm_reduce4_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_REDUCE4");
     return e && e[0] == '0' ? 0 : 1;
-  }()};
-  return flag;
-}
-
-std::atomic<int>& gemm_occ2_flag() {
-  static std::atomic<int> flag{[] {
-    const char* e = getenv("FAN_GEMM_OCC2");
-    return e && e[0] == '1' ? 1 : 0;
   }()};
   return flag;
 }
@@ -92,40 +68,6 @@ std::atomic<int>& gemm_main_loop_flag() {
     return m == 1 || m == 4 ? 2 : m;
   }()};
   return flag;
-}
-
-std::atomic<int>& gemm_half_stage_flag() {
-  static std::atomic<int> flag{[] {
-    const char* e = getenv("FAN_GEMM_HALF");
-    return e ? atoi(e) : 0;
-  }()};
-  return flag;
-}
-
-std::atomic<int>& gemm_fixup_flag() {
-  static std::atomic<int> flag{[] {
-    const char* e = getenv("FAN_GEMM_FIXUP");
-    return e ? atoi(e) : 0;
-  }()};
-  return flag;
-}
-
-unsigned* gemm_fix_counters(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, unsigned*> bufs;
-  int dev = 0;
-  FAN_HIP_CHECK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = bufs.find({dev, s});
-  if (it != bufs.end()) return it->second;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  FAN_HIP_CHECK(hipStreamIsCapturing(s, &st));
-  if (st != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture: the reduce kernel runs
-  unsigned* p = nullptr;
-  FAN_HIP_CHECK(hipMalloc(&p, kFixTiles * sizeof(unsigned)));
-  FAN_HIP_CHECK(hipMemset(p, 0, kFixTiles * sizeof(unsigned)));
-  bufs[{dev, s}] = p;
-  return p;
 }
 
 std::atomic<int>& gemm_persist_flag() {
@@ -309,17 +251,13 @@ GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm, int tile_
 bool gemm_bf16_supported(const GemmArgs& a) {
   const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn, a.tile_waves);
   if (p.bm == 0) return false;
-  if (a.lda % 8 || a.ldb % 8 || a.ldc % 4 || (a.aux && !is_bits_epi(a.epilogue) && a.ldaux % 4)) return false;
+  if (a.lda % 8 || a.ldb % 8 || a.ldc % 4 || (a.aux && a.ldaux % 4)) return false;
   if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return false;
   if (((uintptr_t)a.C) & (a.c_bf16 ? 7 : 15)) return false;
   if (a.accumulate && a.c_bf16) return false;
   if (p.split_k > 1 && a.workspace == nullptr) return false;
   if (a.colsum && a.b_kcontig) return false;
   if (p.bm == 224 && (!a.a_kcontig || a.colsum)) return false;  // 224-row tiles: K-contiguous A image only
-  if (is_bits_epi(a.epilogue)) {  // 1-bit ReLU mask plane in aux: bf16 output, one K pass, 8-column groups
-    if (!a.c_bf16 || a.accumulate || !a.aux || p.split_k != 1 || a.N % 8 || a.ldaux * 8 < a.N || a.colsum)
-      return false;
-  }
   if (a.epilogue == kEpiWire) {
     if (a.a_kcontig || a.b_kcontig || a.c_bf16 || a.accumulate || !a.wire || a.N % 16) return false;
     if (a.wire_shard <= 0 || a.wire_shard % 256 || a.ldc % 16) return false;
@@ -335,7 +273,7 @@ void launch_gemm_bf16(const GemmArgs& a, hipStream_t s) {
   const GemmPlan p = gemm_bf16_plan(a.M, a.N, a.K, a.split_k, a.tile_bm, a.tile_bn, a.tile_waves);
   if (a.c_bf16 && !a.wire) {  // the bf16 epilogue stores 8 columns (16 B) per lane (store_tile, epi8_bf16)
     const bool mask = a.epilogue == kEpiReluMask;
-    const bool bias = a.epilogue == kEpiBias || a.epilogue == kEpiBiasRelu || a.epilogue == kEpiBiasReluBits;
+    const bool bias = a.epilogue == kEpiBias || a.epilogue == kEpiBiasRelu;
     FAN_CHECK(((uintptr_t)a.C & 15) == 0 && a.ldc % 8 == 0 && (!bias || ((uintptr_t)a.bias & 15) == 0) &&
                   (!mask || (((uintptr_t)a.aux & 15) == 0 && a.ldaux % 8 == 0)),
               "gemm_bf16: bf16 output, bias and activation must be 16-B aligned with ldc, ldaux % 8 == 0");

@@ -12,7 +12,6 @@ no gather/scatter copies, no separate optimizer pass.
 """
 from __future__ import annotations
 
-import os
 
 import math
 from dataclasses import dataclass
@@ -141,8 +140,8 @@ class MLP:
         self.sync_lp()
 
     def repad(self, i: int, n_pad: int):
-        """Grow layer i's bucket planes to ``n_pad`` elements (values kept, new tail zero): the trainer's row-panel
-        layout of a bucket pads it to whole panels."""
+        """Grow layer i's bucket planes to ``n_pad`` elements (values kept, new tail zero): an engine layout that pads
+        a bucket further than the model's default."""
         l = self.layers[i]
         if n_pad <= l.n_pad:
             return
@@ -166,35 +165,14 @@ class MLP:
         self.act = [torch.empty(mb, c, dtype=adt, device=dev) for c in self.sizes[:-1]]
         self.logits = torch.empty(mb, self.sizes[-1], dtype=torch.float32, device=dev)
         self.dz = [None] + [torch.empty(mb, c, dtype=adt, device=dev) for c in self.sizes[1:]]
-        # 1-bit ReLU masks of the hidden activations (uint8 [mb][c/8]): written by the forward GEMM, read by the
-        # bwd-data GEMM instead of the bf16 activation (ops/gemm.py EPI_RELU_BITS)
-        self.mask = [None] * self.L
-        for i in range(1, self.L):
-            if self._relu_at(i - 1) and self._bits_ok(mb, i):
-                self.mask[i] = torch.empty(mb, self.sizes[i] // 8, dtype=torch.uint8, device=dev)
         self.loss_rows = torch.empty(mb, dtype=torch.float32, device=dev)
         self._act_mb = mb
-
-    def _bits_ok(self, mb: int, i: int) -> bool:
-        """Activation i (output of layer i - 1, input of layer i) through mask bits (opt-in, FAN_RELU_BITS=1): bf16
-        GPU model, and both GEMMs (layer i - 1's forward, layer i's bwd-data) on whole-wave unsplit static plans.
-        Measured slower on the flagship step (1.047-1.049 vs 1.023-1.035 ms/step, profiles/r5_relu_bits_ab.txt):
-        the bwd-data GEMMs gain 4-11 us, but the forward's extra byte stores cost 7-10 us per GEMM, and the
-        bwd-weight GEMM that follows each bwd-data GEMM loses the activation the mask read had just pulled into the
-        MALL (+5 / +21 us)."""
-        if not (self.device.type == "cuda" and self.dtype == torch.bfloat16 and self.bias):
-            return False
-        if os.environ.get("FAN_RELU_BITS", "0") != "1":
-            return False
-        c_in, c, c_out = self.sizes[i - 1], self.sizes[i], self.sizes[i + 1]
-        return G.mask_bits_supported(mb, c, c_in) and G.mask_bits_supported(mb, c, c_out)
 
     # ------------------------------------------------------------------ compute
     def forward_layer(self, i: int):
         l = self.layers[i]
         out = self.act[i + 1] if i + 1 < self.L else self.logits
-        mask = self.mask[i + 1] if i + 1 < self.L else None
-        G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i), mask_out=mask)
+        G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i))
 
     def loss_backward(self, labels, grad_scale: float):
         NN.softmax_xent(self.logits, labels, self.dz[self.L], self.loss_rows, grad_scale)
@@ -219,23 +197,11 @@ class MLP:
             G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
             NN.col_sum(self.dz[i + 1], l.gb)
 
-    def backward_weight_rows(self, i: int, r0: int, r1: int, wire, with_bias: bool):
-        """Rows [r0, r1) of dW of layer i (a row panel: a contiguous flat range of the bucket), BFP-encoded into
-        ``wire`` (that panel's chunk of the wire buffer); ``with_bias``: the panel that ends at the last row also
-        produces the bias gradient (fused colsum, the bucket segment right after dW)."""
-        l = self.layers[i]
-        G.linear_bwd_weight(self.act[i][:, r0:r1], self.dz[i + 1], l.gw[r0:r1],
-                            bias_grad=l.gb if (with_bias and self.bias) else None, wire=wire)
-
     def backward_data(self, i: int):
         if i == 0:
             return
         l = self.layers[i]
-        if self.mask[i] is not None:
-            G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i], relu_bits=self.mask[i])
-        else:
-            G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i],
-                              relu_input=self.act[i] if self._relu_at(i - 1) else None)
+        G.linear_bwd_data(self.dz[i + 1], l.w, self.dz[i], relu_input=self.act[i] if self._relu_at(i - 1) else None)
 
     def forward(self, x):
         """Inference forward (returns f32 logits)."""

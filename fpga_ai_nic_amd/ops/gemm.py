@@ -18,9 +18,6 @@ import torch
 from .. import _ext
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK, EPI_WIRE = 0, 1, 2, 3, 4
-# ReLU through a 1-bit mask plane (uint8 [M][N/8], bit n % 8 of byte n / 8 = output(m, n) > 0): the forward writes
-# it beside its bf16 activation, the bwd-data GEMM reads it instead of the activation (1/16 of the bytes)
-EPI_BIAS_RELU_BITS, EPI_RELU_BITS = 6, 7
 
 _ws: dict = {}
 
@@ -83,9 +80,6 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
             _nn.col_sum(B.t() if b_t else B, colsum)
             return C
         if A.dtype == torch.bfloat16:
-            if epilogue in (EPI_BIAS_RELU_BITS, EPI_RELU_BITS) and (C.dtype != torch.bfloat16 or accumulate):
-                raise ValueError("mask-bit epilogues: bf16 output, no accumulate")
-            # (mask-bit planes are read / written one byte per lane: no alignment of their own)
             if C.dtype == torch.bfloat16 and not _aligned16(C, bias, aux if epilogue == EPI_RELU_MASK else None):
                 # the bf16 epilogue stores 16 B per lane: stage misaligned operands through aligned copies
                 Ct = torch.empty(C.shape, dtype=C.dtype, device=C.device)
@@ -118,15 +112,9 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
         r = torch.relu(r)
     if epilogue == EPI_RELU_MASK:
         r = r * (aux.float() > 0)
-    if epilogue == EPI_BIAS_RELU_BITS:
-        r = torch.relu(r + bias.float())
-    if epilogue == EPI_RELU_BITS:
-        r = r * unpack_mask_bits(aux, r.shape[1])
     if accumulate:
         r = r + C.float()
     C.copy_(r.to(C.dtype))
-    if epilogue == EPI_BIAS_RELU_BITS:
-        aux.copy_(pack_mask_bits(C > 0))
     if colsum is not None:
         colsum.copy_(b.sum(0).to(colsum.dtype))
     return C
@@ -150,7 +138,7 @@ def gemm_wgrad_group(problems, wire=None):
     ``wire=(buf, shard, own, codec[, period])`` BFP-encoded into the bucket's wire buffer at flat offset ``off``,
     the bias segment right after C) and colsum = the column sums of dY (the fused bias gradient). 256x128 tiles, one
     per workgroup, no split-K: a transformer layer's projections (each too small to fill the CUs alone) fill them
-    together (csrc/gemm/gemm_pair.hip launch_gemm_wgrad_group)."""
+    together (csrc/gemm/gemm_group.hip launch_gemm_wgrad_group)."""
     Cx = _ext.require()
     Xs = [p[0] for p in problems]
     dYs = [p[1] for p in problems]
@@ -229,11 +217,6 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
     from . import gemm_tune
 
     T = gemm_tune.tuner()
-    if epilogue in (EPI_BIAS_RELU_BITS, EPI_RELU_BITS):  # the static plan, which must not split K (mask_bits_supported)
-        if static[2] != 1:
-            raise ValueError(f"mask-bit epilogue: the plan of M={M} N={N} K={K} splits K")
-        run(tuple(static[:3]), tw)
-        return
     if (tile is not None or split_k is not None or not T.enabled or accumulate
             or torch.cuda.is_current_stream_capturing() or _shares_storage(C, A, B, aux, bias)):
         run(tuple(static[:3]), tw, update)
@@ -253,42 +236,13 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
         run(plan, 0, update)
 
 
-def pack_mask_bits(m):
-    """bool [M][N] -> uint8 [M][N/8] (bit j of byte k: column 8k + j), the mask-bit epilogues' plane layout."""
-    M, N = m.shape
-    w = (1 << torch.arange(8, device=m.device, dtype=torch.int32))
-    return (m.reshape(M, N // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
-
-
-def unpack_mask_bits(bits, N):
-    w = (1 << torch.arange(8, device=bits.device, dtype=torch.int32))
-    return ((bits[:, : N // 8].to(torch.int32).unsqueeze(-1) & w) != 0).reshape(bits.shape[0], -1)[:, :N].float()
-
-
-def mask_bits_supported(M: int, N: int, K: int) -> bool:
-    """Shapes whose bf16 GEMM's plan is the static one without split-K on a whole wave of workgroups (the mask-bit
-    epilogues' condition: no slab reduce, and the same plan as the activation-reading epilogues — which the tuner
-    never re-plans for whole-wave grids — so both schedules round alike)."""
-    if N % 8 or M <= 0:
-        return False
-    p = _ext.require().gemm_plan(M, N, K, 0, 0, 0, 0)
-    if p[0] == 0 or p[2] != 1:
-        return False
-    cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
-    return (-(-M // p[0]) * -(-N // p[1])) % cus == 0
-
-
-def linear_fwd(x, w, b, out, relu: bool, mask_out=None):
-    """Y = X · W + b (ReLU); with ``mask_out`` (uint8 [M][N/8]) the ReLU's mask bits are written there too."""
-    if relu and mask_out is not None:
-        return gemm(x, False, w, False, out, EPI_BIAS_RELU_BITS, bias=b, aux=mask_out)
+def linear_fwd(x, w, b, out, relu: bool):
+    """Y = X · W + b (ReLU)."""
     return gemm(x, False, w, False, out, EPI_BIAS_RELU if relu else EPI_BIAS, bias=b)
 
 
-def linear_bwd_data(dz, w, out, relu_input=None, relu_bits=None):
-    """dX = dZ · Wᵀ, optionally masked by (relu_input > 0) or by the forward's mask bits (ReLU backward fused)."""
-    if relu_bits is not None:
-        return gemm(dz, False, w, True, out, EPI_RELU_BITS, aux=relu_bits)
+def linear_bwd_data(dz, w, out, relu_input=None):
+    """dX = dZ · Wᵀ, optionally masked by (relu_input > 0) (ReLU backward fused)."""
     if relu_input is not None:
         return gemm(dz, False, w, True, out, EPI_RELU_MASK, aux=relu_input)
     return gemm(dz, False, w, True, out, EPI_NONE)

@@ -78,16 +78,9 @@ class DataParallelTrainer:
     def __init__(self, model: MLP, engine: CompressedAllReduce | None, *, lr: float = 0.1,
                  weight_decay: float = 0.0, momentum: float = 0.0, nesterov: bool = False,
                  loss_scale: float = 1.0, average: bool = True, profile: bool = False, prepack: bool = True,
-                 commit_at_end: bool | None = None, panels: int | None = None, panel_submit: str = "split",
-                 fused_update: bool | None = None, gemm_inflight: str | None = None):
-        """``panels`` (default env FAN_PANELS, else off; < 2 disables): the
-        last-issued bucket (layer 0: no backward left to hide its exchange behind) is computed as row panels of dW,
-        each submitted as a request of its own right after its GEMM (multi-rank C++ engine, mesh, GEMM-encoded
-        wire only). ``panel_submit='whole'`` computes
-        the same panels but submits the bucket as one request of the same chunked layout (the unsplit schedule,
-        bit-identical results).
-
-        ``fused_update`` (default env FAN_FUSED_UPDATE, else on): with a single-rank engine (world 1, requests
+                 commit_at_end: bool | None = None, fused_update: bool | None = None,
+                 gemm_inflight: str | None = None):
+        """``fused_update`` (default env FAN_FUSED_UPDATE, else on): with a single-rank engine (world 1, requests
         inline: the all-reduce of one rank is the identity) and the GEMM-encoded wire, the bwd-weight GEMM's epilogue
         takes each encoded gradient group through its BFP round trip in registers and applies the SGD update to the
         layer's weights in place — the engine's decode + SGD pass over the whole bucket (master read + write, bf16
@@ -139,20 +132,6 @@ class DataParallelTrainer:
         # (FAN_LAST_ON_PRODUCER=0: on the comm stream like the others)
         self.last_on_producer = (self.cuda and engine is not None and not getattr(engine, "inline", True)
                                  and hasattr(engine, "C") and os.environ.get("FAN_LAST_ON_PRODUCER", "1") != "0")
-        self.panel_submit = panel_submit
-        self.panel_plans: dict[int, dict] = {}
-        # opt-in (FAN_PANELS=4): measured on the one-GPU pool the split costs more than it hides — each panel adds a
-        # GEMM launch at a quarter of the rows (more split-K slabs) and a request with two P2P rounds, and there the
-        # "exchange" it would hide is local (forced 1-rank path: 1.263 vs 1.127 ms/step; two ranks time-sharing one
-        # GPU: 5.06-5.30 vs 4.61-4.70 ms/step, profiles/r3_panels_ab.txt). It stays off until an 8-GPU run shows
-        # the layer-0 exchange it is built to overlap.
-        P = int(os.environ.get("FAN_PANELS", "0")) if panels is None else int(panels)
-        if self.prepack and P >= 2 and hasattr(engine, "panel_plan") and not self.shard:
-            l0 = model.layers[0]
-            pp = engine.panel_plan(l0.cin, l0.cout, P)
-            if pp is not None:
-                model.repad(0, pp["n_pad"])
-                self.panel_plans[0] = pp
 
     def _sgd_local(self, l):
         wire.sgd(wire.as_bytes(l.grad), l.n_pad, 1, l.master, codec="raw_f32", lp=l.lp, mom=l.mom, lr=self.lr,
@@ -197,32 +176,6 @@ class DataParallelTrainer:
                 x.synchronize()
         self.pending[i] = None
 
-    def _backward_weight_panels(self, i: int):
-        """dW of layer i as row panels (see ``panels``): panel p's GEMM encodes its rows straight into chunk p of
-        the wire buffer, then chunk p is submitted (deferred) while panel p+1's GEMM runs."""
-        m, l, pp, eng = self.m, self.m.layers[i], self.panel_plans[i], self.engine
-        R, C, S, N = pp["rows"], pp["chunks"], pp["shard"], eng.world
-        buf, shard, own, codec, period = eng.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout,
-                                                            layout=(S, C))
-        sb = wire.shard_bytes(codec, S)
-        ext = N * S
-        kw = dict(lr=self.lr, grad_scale=self.grad_scale, weight_decay=self.wd, momentum=self.momentum,
-                  nesterov=self.nesterov, defer=True)
-        hs = []
-        for p in range(C):
-            r0, r1 = p * R, min((p + 1) * R, l.cin)
-            chunk = buf[p * N * sb:(p + 1) * N * sb]
-            m.backward_weight_rows(i, r0, r1, (chunk, S, own, codec, period), with_bias=p == C - 1)
-            if self.panel_submit == "split":
-                sl = slice(p * ext, (p + 1) * ext)
-                hs.append(eng.allreduce_sgd(l.grad[sl], l.master[sl], None if l.lp is None else l.lp[sl],
-                                            None if l.mom is None else l.mom[sl], n_valid=min(l.n, (p + 1) * ext) - p * ext,
-                                            prepacked=(chunk, ext), layout=(S, 1), name=f"fc{i}.p{p}", **kw))
-        if self.panel_submit != "split":
-            hs.append(eng.allreduce_sgd(l.grad, l.master, l.lp, l.mom, n_valid=l.n, prepacked=(buf, C * ext),
-                                        layout=(S, C), name=f"fc{i}", **kw))
-        return hs
-
     def _wait_updates(self):
         """Every outstanding update has landed (GPU-side order on the current stream; host waits on CPU)."""
         for i in range(self.m.L):
@@ -245,13 +198,6 @@ class DataParallelTrainer:
         try:
             for i in reversed(range(m.L)):
                 l = m.layers[i]
-                if i in self.panel_plans and self.engine is not None:
-                    with tracing.range(f"bwd{i}"):
-                        hs = self._backward_weight_panels(i)
-                        m.backward_data(i)
-                        self.pending[i] = hs if self.commit_at_end else [h.commit_after_current() for h in hs]
-                        self.last_handle = hs[-1]
-                    continue
                 with tracing.range(f"bwd{i}"):
                     # the bwd-weight GEMM encodes dW (and the fused bias gradient) straight into the wire buffer;
                     # the zero tail (padding, or the bias segment of a bias-free model) is encoded once

@@ -205,7 +205,7 @@ class NativeAllReduce:
         return torch.cuda.ExternalStream(self.C.stream, device=self.device)
 
     def layout(self, n: int, shard: int = 0, chunks: int = 0) -> BucketLayout:
-        """Bucket layout; ``shard`` / ``chunks`` > 0: an explicit chunked mesh layout (row-panel buckets)."""
+        """Bucket layout; ``shard`` / ``chunks`` > 0: an explicit chunked mesh layout."""
         d = self.C.layout(int(n), int(shard), int(chunks))
         return BucketLayout(n=d["n"], n_pad=d["n_pad"], algo=self.algo, world=self.world, shard=d["shard"],
                             slice_elems=d["slice"], blocks=d["blocks"], rings=d["rings"], part=d["part"],
@@ -213,31 +213,6 @@ class NativeAllReduce:
 
     def wire_bytes(self, L: BucketLayout) -> int:
         return int(self.C.wire_bytes(L.n))
-
-    def panel_plan(self, cin: int, cout: int, panels: int):
-        """Row-panel layout of a [W (cin x cout) | b (cout)] bucket in ``panels`` chunks (or None when this engine /
-        shape cannot take one): every chunk holds R whole rows of dW (R*cout = world shards of 256-multiple size,
-        R % 8 == 0 for 16-B aligned operand slices), the last chunk the remaining rows + the bias. The trainer
-        computes dW panel by panel and submits each chunk as a request of its own as soon as its GEMM is enqueued,
-        so chunk p's exchange overlaps panel p+1's GEMM (the reference overlaps each request with the following
-        backward, sw/mlp_mpi_example_f32.cpp:752-764)."""
-        if (self.algo != "mesh" or not self.prepack or self.inline or panels < 2 or cout % 16
-                or self.codec not in ("bfp_rne", "bfp_trunc")):
-            return None
-        N = self.world
-        R = -(-max(8, -(-(cin + 1) // panels)) // 8) * 8
-        while R <= cin:
-            C = -(-(cin + 1) // R)
-            last_rows = cin - (C - 1) * R
-            if R % 8 == 0 and (R * cout) % (256 * N) == 0 and C >= 2 and last_rows >= 8:
-                S = R * cout // N
-                try:
-                    self.C.layout(cin * cout + cout, S, C)
-                except RuntimeError:
-                    return None
-                return {"rows": R, "chunks": C, "shard": S, "n_pad": C * N * S}
-            R += 8
-        return None
 
     def prepack_target(self, grad: torch.Tensor, n: int, static_from: int | None = None, layout=None):
         """Wire target for a producer that encodes the gradient itself (GEMM ``kEpiWire`` epilogue):
@@ -250,7 +225,7 @@ class NativeAllReduce:
         shard, shards, own = self.C.prepack_shape(int(n))
         if shard == 0 or n % 16:
             return None
-        if layout is not None:  # explicit chunked layout (row panels): shard x world x chunks
+        if layout is not None:  # explicit chunked layout: shard x world x chunks
             shard, shards = int(layout[0]), int(layout[1]) * self.world
         need = shards * wire.shard_bytes(self.codec_id, shard)
         static_from = n if static_from is None else int(static_from)
@@ -272,7 +247,7 @@ class NativeAllReduce:
                       name: str = "bucket", prepacked=None, layout=None, on_producer: bool = False) -> NativeHandle:
         """``prepacked=(wire_u8, elems)``: flat elements [0, elems) were already encoded into ``wire_u8``
         (from :meth:`prepack_target`); the engine encodes the rest and skips its pack pass. ``layout=(shard,
-        chunks)``: an explicit chunked mesh layout (see :meth:`panel_plan`). ``on_producer``: run the request on the
+        chunks)``: an explicit chunked mesh layout (shard elements x world x chunks). ``on_producer``: run the request on the
         current (producer) stream instead of the engine's comm stream — the last request of a backward, which has
         nothing left to overlap with (saves two cross-stream hand-offs on the critical path)."""
         n_valid = int(n_valid if n_valid is not None else master.numel())

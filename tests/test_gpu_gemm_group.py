@@ -1,9 +1,7 @@
 """Grouped GEMM launches and tensors inside a multi-tensor gradient bucket.
 
-* ``gemm_bwd_pair``: one layer's bwd-data (ReLU-mask epilogue, bf16) and bwd-weight (f32) in ONE dispatch
-  (csrc/gemm/gemm_pair.hip, the reference's PASS_BWD shape, sw/mlp_mpi_example_f32.cpp:741-742) is bit-identical to
-  the two separate launches of the same tiles, and both match fp32 torch within the bf16 bounds, for several
-  workgroup splits (including splits that leave one problem more workgroups than tiles);
+* ``gemm_wgrad_group``: up to 8 bwd-weight GEMMs in ONE dispatch (csrc/gemm/gemm_group.hip) against fp32 torch, and
+  its wire epilogue against the oracle's encode of its own f32 result;
 * the wire epilogue's flat offset (GemmArgs::wire_off): a weight matrix placed at an offset inside a larger bucket
   (a transformer layer's bucket, bench/bert_overlap.py) encodes exactly the bytes the oracle packs for the whole
   bucket at those positions, with its fused bias gradient encoded right after it.
@@ -18,40 +16,6 @@ from fpga_ai_nic_amd.ops import gemm as G
 from fpga_ai_nic_amd.ops import wire
 
 pytestmark = pytest.mark.gpu
-
-
-@pytest.mark.parametrize("M,cin,cout,bn,g0,g1", [(1024, 1024, 512, 128, 64, 64), (2048, 512, 1024, 256, 64, 32),
-                                                  (512, 512, 256, 128, 128, 128), (768, 1024, 768, 256, 8, 8)])
-def test_bwd_pair_matches_separate_launches(M, cin, cout, bn, g0, g1):
-    C = _ext.require()
-    torch.manual_seed(M + cin)
-    X = (torch.rand(M, cin, device="cuda") * 2 - 1).to(torch.bfloat16)
-    dZ = ((torch.rand(M, cout, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
-    W = ((torch.rand(cin, cout, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
-    dX = torch.empty(M, cin, device="cuda", dtype=torch.bfloat16)
-    dW = torch.empty(cin, cout, device="cuda")
-    G.gemm(dZ, False, W, True, dX, G.EPI_RELU_MASK, aux=X, tile=(256, 256), split_k=1)
-    G.gemm(X, True, dZ, False, dW, G.EPI_NONE, tile=(256, bn), split_k=1)
-    dX2 = torch.full_like(dX, 3.0)
-    dW2 = torch.full_like(dW, 3.0)
-    C.gemm_bwd_pair(dZ, W, X, dX2, dW2, bn, g0, g1)
-    torch.cuda.synchronize()
-    assert torch.equal(dX, dX2) and torch.equal(dW, dW2)
-    rx = (dZ.float() @ W.float().t()) * (X.float() > 0)
-    rw = X.float().t() @ dZ.float()
-    assert (dX2.float() - rx).abs().max() <= 2e-2 * rx.abs().max() + 1e-6
-    assert (dW2 - rw).abs().max() <= 1e-3 * rw.abs().max() + 1e-6
-
-
-def test_bwd_pair_rejects_bad_grids():
-    C = _ext.require()
-    X = torch.zeros(256, 256, device="cuda", dtype=torch.bfloat16)
-    dZ = torch.zeros(256, 256, device="cuda", dtype=torch.bfloat16)
-    W = torch.zeros(256, 256, device="cuda", dtype=torch.bfloat16)
-    dX = torch.empty_like(X)
-    dW = torch.empty(256, 256, device="cuda")
-    with pytest.raises(RuntimeError):
-        C.gemm_bwd_pair(dZ, W, X, dX, dW, 256, 12, 8)  # not a multiple of the XCD count
 
 
 @pytest.mark.parametrize("codec", ["bfp_rne", "bfp_trunc"])

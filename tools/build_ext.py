@@ -130,6 +130,15 @@ def build(jobs: int = 8, verbose: bool = False, clean: bool = False) -> str:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, OUT)
         print(f"[build_ext] linked {os.path.relpath(OUT, ROOT)}", flush=True)
+        # the LDS-DMA statements leave M0 written (hipcc ignores an "m0" clobber): no kernel that runs them may hold a
+        # compiler value in M0 (tools/check_m0.py)
+        if os.path.exists(f"{os.path.dirname(HIPCC)}/../lib/llvm/bin/clang-offload-bundler"):
+            sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+            import check_m0  # noqa: WPS433
+
+            if check_m0.main(["check_m0", BUILD]) != 0:
+                os.remove(OUT)
+                raise RuntimeError("M0 contract violated by a compiled kernel (tools/check_m0.py)")
     with open(stamp_path, "w") as f:
         f.write(stamp)
     return OUT
