@@ -3,6 +3,7 @@
 #include "bfp/bfp_format.h"
 #include "comm/planner.h"
 #include "gemm/gemm.h"
+#include "gemm/gemm_chain.h"
 #include "gemm/gemm_group.h"
 #include "nn/nn.h"
 
@@ -197,6 +198,67 @@ void gemm_wgrad_group(const std::vector<at::Tensor>& Xs, const std::vector<at::T
   launch_gemm_wgrad_group(g.data(), (int)n, fan_stream());
 }
 
+// The GEMMs of one MLP pass as ONE persistent launch (gemm_chain.h). kind 0 (forward): A0 = X [M][K0], Bs[i] = W_i
+// [K_i][N_i], Cs[i] = the layer outputs (bf16 hidden, the last bf16 or f32 logits), biases[i]; kind 1 (backward data):
+// A0 = dZ [M][K0], Bs[i] = W [N_i][K_i] (K-contiguous), Cs[i] = dX outputs (bf16), auxes[i] = the ReLU-mask
+// activations; epis[i]: each stage's epilogue (the chain checks it is one of its configurations). Stage i + 1 reads Cs[i]. counters: int32 GPU tensor of at least gemm_chain_words(n, M) elements,
+// zero before the first call (the kernel leaves it zero). Returns false (nothing launched) when the chain does not
+// take these shapes / layouts; dry_run: only that check.
+bool gemm_chain(int64_t kind, const at::Tensor& A0, const std::vector<at::Tensor>& Bs, const std::vector<at::Tensor>& Cs,
+                const std::vector<c10::optional<at::Tensor>>& biases,
+                const std::vector<c10::optional<at::Tensor>>& auxes, const std::vector<int64_t>& epis,
+                at::Tensor& counters, bool dry_run) {
+  const int n = (int)Bs.size();
+  TORCH_CHECK(n >= 1 && (int)Cs.size() == n && (int)biases.size() == n && (int)auxes.size() == n &&
+                  (int)epis.size() == n,
+              "gemm_chain: one B, C, bias, aux and epilogue entry per stage");
+  if (n > gemm_chain_max_stages()) return false;
+  std::vector<GemmArgs> g(n);
+  for (int i = 0; i < n; ++i) {
+    const at::Tensor& A = i == 0 ? A0 : Cs[i - 1];
+    const at::Tensor& B = Bs[i];
+    const at::Tensor& C = Cs[i];
+    for (const at::Tensor* t : {&A, &B, &C})
+      if (!t->is_cuda() || t->dim() != 2 || t->stride(1) != 1) return false;
+    if (A.scalar_type() != at::kBFloat16 || B.scalar_type() != at::kBFloat16) return false;
+    GemmArgs& a = g[i];
+    a.A = A.data_ptr();
+    a.B = B.data_ptr();
+    a.C = C.data_ptr();
+    a.lda = A.stride(0);
+    a.ldb = B.stride(0);
+    a.ldc = C.stride(0);
+    a.M = (int)A.size(0);
+    a.K = (int)A.size(1);
+    a.N = (int)(kind == kChainBwdData ? B.size(0) : B.size(1));
+    if ((kind == kChainBwdData ? B.size(1) : B.size(0)) != a.K || C.size(0) != a.M || C.size(1) != a.N) return false;
+    a.a_kcontig = true;
+    a.b_kcontig = kind == kChainBwdData;
+    a.c_bf16 = C.scalar_type() == at::kBFloat16;
+    if (!a.c_bf16 && C.scalar_type() != at::kFloat) return false;
+    a.split_k = 1;
+    if (kind == kChainFwd) {
+      if (!biases[i] || biases[i]->scalar_type() != at::kBFloat16 || biases[i]->numel() < a.N) return false;
+      a.bias = biases[i]->data_ptr();
+      a.epilogue = (int)epis[i];
+    } else {
+      if (!auxes[i] || auxes[i]->scalar_type() != at::kBFloat16 || auxes[i]->dim() != 2 ||
+          auxes[i]->stride(1) != 1 || auxes[i]->size(0) != a.M || auxes[i]->size(1) != a.N)
+        return false;
+      a.aux = auxes[i]->data_ptr();
+      a.ldaux = auxes[i]->stride(0);
+      a.epilogue = (int)epis[i];
+    }
+  }
+  if (!gemm_chain_supported(g.data(), n, (int)kind)) return false;
+  TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.is_contiguous() &&
+                  counters.numel() >= gemm_chain_counter_words(n, g[0].M),
+              "gemm_chain: counters must be a contiguous int32 GPU tensor of gemm_chain_words(n, M) elements");
+  if (dry_run) return true;
+  launch_gemm_chain(g.data(), n, (int)kind, reinterpret_cast<unsigned*>(counters.data_ptr()), fan_stream());
+  return true;
+}
+
 int64_t gemm_wgrad_group_ws_floats(const std::vector<std::pair<int64_t, int64_t>>& mn) {
   int64_t w = 0;
   for (const auto& p : mn) w += ((p.first / 256) * p.second + 3) / 4 * 4;
@@ -265,6 +327,11 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("wire_shard") = 0, pybind11::arg("wire_own") = -1, pybind11::arg("wire_codec") = 1,
         pybind11::arg("wire_period") = 0);
   m.def("gemm_wgrad_group_ws", &gemm_wgrad_group_ws_floats, "f32 workspace elements for a group of (M, N) problems");
+  m.def("gemm_chain", &gemm_chain, "the GEMMs of one MLP pass as one persistent launch (row-panel hand-offs)",
+        pybind11::arg("kind"), pybind11::arg("A0"), pybind11::arg("Bs"), pybind11::arg("Cs"), pybind11::arg("biases"),
+        pybind11::arg("auxes"), pybind11::arg("epis"), pybind11::arg("counters"), pybind11::arg("dry_run") = false);
+  m.def("gemm_chain_words", &gemm_chain_counter_words, "int32 words of a layer-chain counter block",
+        pybind11::arg("n"), pybind11::arg("M"));
   m.def("gemm_set_prio", [](int on) { gemm_prio_flag().store(on); },
         "4-wave pipelined GEMM waves at s_setprio 2 (another stream's kernels issue in their stalls)");
   m.def("gemm_prio", []() { return gemm_prio_flag().load(); });

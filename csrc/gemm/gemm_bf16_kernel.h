@@ -213,7 +213,17 @@ __device__ __forceinline__ void epi4(float v[4], TC* __restrict__ C, int64_t ldc
 // epilogue of a 256x256 bf16 tile is store-ISSUE-bound (MI355X_MICROARCH.md per-instruction table: a dwordx2 store
 // tail runs at about half the rate of dwordx4), so the bf16 outputs are written 8 columns per lane. Same
 // arithmetic, element for element, as epi4.
-template <int EPI, bool ACCUM>
+// 16-B store that writes through the XCD's L2 (sc1): the bytes are in memory once the storing wave's vmcnt reaches
+// zero, so a workgroup on another XCD can read them after a counter hand-off with no release fence (the layer-chain
+// GEMM's producer stages; MI355X_MICROARCH.md § visibility, publish-large: write-through beats plain stores + a
+// release fence for tens of KB per workgroup). Not tracked by the compiler: every wait on it is an explicit vmcnt.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_wt16(void* p, const uint4& o) {
+  const u32x4_t v = {o.x, o.y, o.z, o.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int EPI, bool ACCUM, bool WT = false>
 __device__ __forceinline__ void epi8_bf16(float v[8], bf16_t* __restrict__ C, int64_t ldc,
                                           const bf16_t* __restrict__ bias, const uint4* mask, int row, int col) {
   auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
@@ -241,7 +251,8 @@ __device__ __forceinline__ void epi8_bf16(float v[8], bf16_t* __restrict__ C, in
   }
   const uint4 o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                              pack_bf16x2(v[6], v[7]));
-  *reinterpret_cast<uint4*>(p) = o;
+  if constexpr (WT) store_wt16(p, o);
+  else *reinterpret_cast<uint4*>(p) = o;
 }
 
 // kEpiWire target (GemmArgs::wire*): passed by value as one kernel argument.
@@ -426,13 +437,14 @@ __device__ __forceinline__ void colsum_finish(float (&cs)[NJ], int lane, int col
 // groups (one lane per group: 16-B mantissa store + exponent byte). Caller: all LDS operand reads retired.
 // SW (bf16 8-column path only): staged columns per pass over a 16-row block — WTN, or 64 (two halves: 17 KiB of
 // staging for 4 waves instead of 33, beside the operand stages of the overlapped persistent loop).
-template <int MI, int NJ, int WTN, int EPI, typename TC, bool ACCUM, bool SPLIT, int SW = WTN>
+template <int MI, int NJ, int WTN, int EPI, typename TC, bool ACCUM, bool SPLIT, int SW = WTN, bool WT = false>
 __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* smem, int wave, int lane, int row0,
                                            int col0, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                            const TC* __restrict__ aux, int64_t ldaux, int M, int N, int ksplit,
                                            float* __restrict__ ws, const WireOut& wo, bool mn_edge = false) {
   static_assert(SW == WTN || (SW == 64 && WTN % 64 == 0 && sizeof(TC) == 2 && !SPLIT && !is_wire_epi(EPI)),
                 "64-column staging: bf16 8-column path only");
+  static_assert(!WT || (sizeof(TC) == 2 && !SPLIT && !is_wire_epi(EPI)), "write-through stores: the bf16 8-column path");
   constexpr int EW = SW + 4;  // staged row stride in floats (16-B aligned, breaks bank aliasing)
   float* stg = reinterpret_cast<float*>(smem) + wave * (16 * EW);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
@@ -494,7 +506,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
           if (mn_edge && (row >= M || col >= N)) continue;  // N % 8 == 0: an 8-column chunk is wholly in or out
           const uint4* mk = nullptr;
           if constexpr (kPf8) mk = &aq8[i][hv * NP8 + pass];
-          epi8_bf16<EPI, ACCUM>(v, reinterpret_cast<bf16_t*>(C), ldc, bias, mk, row, col);
+          epi8_bf16<EPI, ACCUM, WT>(v, reinterpret_cast<bf16_t*>(C), ldc, bias, mk, row, col);
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // the staged rows are read before the next half / block rewrites them
         }
@@ -1026,6 +1038,117 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Layer-chain GEMM (gemm_chain_kernel, gemm_chain.hip): the GEMMs of a pass — the forward's X -> H1 -> H2 -> logits, the
+// backward's dY -> dH2 -> dH1 — as ONE persistent launch, the GPU form of the reference's single `omp parallel` region
+// whose layers hand over through barriers (sw/mlp_mpi_example_f32.cpp:690-788). Stage s + 1's A operand is stage s's
+// output; an output tile of row panel r (256 rows) of stage s + 1 may start once every tile of row panel r of stage s
+// has stored its output, so layer s + 1's first tiles run under layer s's last tiles and epilogue stores instead of
+// after a grid-wide drain, a kernel boundary and a new fill.
+//   * tickets: workgroup b belongs to group g = b % 8 (one XCD under the round-robin dispatch: speed only) and owns
+//     the row panels [g * ppg, (g + 1) * ppg) of every stage; the group's tickets run stage by stage, row panel by row
+//     panel (a group's 32 workgroups complete whole panels first). Ticket j of group g: the first gridDim / 8 are
+//     static (j = b / 8), the rest come from a per-group atomic head. A workgroup takes its next ticket early in its
+//     current tile (K-tile 1) and polls that ticket's dependency two K-tiles before the end, so the decision at the
+//     last K-tile costs no latency; a dequeued ticket is always held by a running workgroup and depends only on
+//     earlier stages, so the queue cannot deadlock whatever the residency (other streams' kernels, other processes).
+//   * hand-off (MI355X_MICROARCH.md § visibility, valid form "agent-scope atomic adds ... sc1 load poll"): a producer
+//     stage stores its tiles write-through (sc1, store_wt16); the tile's completion is added to its panel's ready
+//     counter by wave 0 lane 0 after every wave's vmcnt(0) and a workgroup barrier (deferred to the next tile's
+//     K-tile 1, whose wait and barrier provide exactly that, or to an explicit drain). The consumer polls the
+//     counter relaxed (sc1), and EVERY wave then issues its own agent acquire (buffer_inv sc1) ahead of its own
+//     LDS-DMA of the panel, so no extra barrier or wait is needed for the acquire.
+//   * state: the counter block (per call site and stream) starts zeroed; the last workgroup to leave (an exit counter)
+//     zeroes it again for the next launch (it is reached only after every workgroup's final add returned). A spin that
+//     exceeds ~4 s stores an error code and gives up (garbage, not a hang); the host reads it (gemm_chain_error).
+constexpr int kChainMaxStages = 8;
+constexpr int kChainLdsCtl = 2 * (256 + 256) * BK * 2 + 4 * 16 * (64 + 4) * 4;  // past the OVL staging rows
+constexpr int kChainLds = kChainLdsCtl + 64;
+constexpr uint32_t kChainSpinLimit = 1u << 22;
+
+struct ChainStageArgs {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  const bf16_t* bias;
+  const void* aux;
+  int64_t lda, ldb, ldc, ldaux;
+  int M, N, K;
+  int tn;      // column tiles
+  int first;   // group-local ticket of this stage's first tile
+  int dep;     // > 0: a tile waits until ready[stage - 1][its row panel] == dep (the previous stage's tn)
+  int signal;  // a finished tile adds 1 to ready[stage][its row panel]
+  int cfg;     // 0: the kernel's first tile configuration, 1: its second
+};
+
+struct ChainArgs {
+  ChainStageArgs st[kChainMaxStages];
+  int nstages;
+  int total;   // tickets per group
+  int ppg;     // row panels per group
+  int panels;  // row panels of the pass (M / 256)
+  unsigned* ctr;
+  int prio;
+  int flags;  // diagnostic builds of the schedule (kChainNoAcquire: unsafe; kChainRowsFastest)
+};
+constexpr int kChainNoAcquire = 1;    // skip the consumer's acquire (diagnostic A/B only: visibility not guaranteed)
+constexpr int kChainRowsFastest = 2;  // a group's tiles rows-fastest (all its panels' column c, then c + 1) instead of
+                                      // panel by panel
+
+// counter block (uint32 words, one 64-B line each): head[8], exit, error, ready[stage][panel]
+__host__ __device__ constexpr int chain_ctr_words(int nstages, int panels) { return (10 + nstages * panels) * 16; }
+__device__ __forceinline__ int chain_ready_word(const ChainArgs& ca, int s, int panel) {
+  return (10 + s * ca.panels + panel) * 16;
+}
+__device__ __forceinline__ int chain_stage_of(const ChainArgs& ca, int t) {
+  int s = 0;
+  while (s + 1 < ca.nstages && t >= ca.st[s + 1].first) ++s;
+  return s;
+}
+
+// per-workgroup chain state (wave-uniform): the ticket to run next, whether its dependency is known to be met, and
+// the ready-counter word of a finished tile whose completion is not yet published (-1: none)
+struct ChainState {
+  int ticket;
+  int ready;
+  int pending;
+};
+
+__device__ __forceinline__ void chain_add(unsigned* ctr, int word) {
+  __hip_atomic_fetch_add(ctr + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned chain_poll(const unsigned* ctr, int word) {
+  return __hip_atomic_load(ctr + word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// this wave's agent-scope acquire: its L1 invalidated before its own later loads (no wait needed for them)
+__device__ __forceinline__ void chain_acquire(int flags = 0) {
+  if (!(flags & kChainNoAcquire)) asm volatile("buffer_inv sc1" ::: "memory");
+}
+// row panel (group-local) and column tile of a stage's k-th tile in its group's ticket order
+__device__ __forceinline__ void chain_tile_rc(const ChainArgs& ca, int tn, int k, int& r, int& c) {
+  if (ca.flags & kChainRowsFastest) {
+    r = k % ca.ppg;
+    c = k / ca.ppg;
+  } else {
+    r = k / tn;
+    c = k % tn;
+  }
+}
+
+// dependency word / target of ticket t (group-local); word < 0: none
+__device__ __forceinline__ void chain_dep_of(const ChainArgs& ca, int t, int& word, unsigned& target) {
+  word = -1;
+  target = 0;
+  if (t >= ca.total) return;
+  const int s = chain_stage_of(ca, t);
+  const ChainStageArgs& S = ca.st[s];
+  if (S.dep <= 0) return;
+  int r, c;
+  chain_tile_rc(ca, S.tn, t - S.first, r, c);
+  word = chain_ready_word(ca, s - 1, (int)(blockIdx.x & 7) * ca.ppg + r);
+  target = (unsigned)S.dep;
+}
+
 // The body of gemm_pl4_kernel as a device function: this workgroup runs virtual blocks v0, v0 + vstep, ... of the
 // problem's tiles * split_k (COLSUM: the one tile v0). gemm_pl4_kernel passes (blockIdx.x, gridDim.x); the grouped
 // kernel (gemm_groupn_kernel) gives each of its problems its own range of workgroups. vstep must be a multiple
@@ -1036,13 +1159,18 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8
 // free after its barrier), and the next tile waits only for its K-tile 0 (vmcnt(G + kS): the epilogue's kS stores
 // are the youngest) and then for K-tile 1 with those stores still allowed in flight — vmcnt counts loads, stores and
 // LDS-DMA together, in issue order (MI355X_MICROARCH.md). Same arithmetic: bit-identical to OVL off.
+// CHAIN (gemm_chain_kernel): tiles come from the chain's ticket queue instead of the static stride (v0 / vstep
+// unused), each tile of a dependent stage after its row panel's hand-off (see the layer-chain comment above); the
+// run returns to the chain loop when the next ticket belongs to another stage or is not known ready (chs). WT: the
+// bf16 epilogue stores write through the L2 (a producer stage of the chain).
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false>
+          int BM_ = 256, bool OVL = false, bool CHAIN = false, bool WT = false>
 __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
                                         int64_t ldb, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                         const TC* __restrict__ aux, int64_t ldaux, int M, int N, int K, int split_k,
                                         float* __restrict__ ws, float* __restrict__ colsum, const WireOut& wo, int v0,
-                                        int vstep) {
+                                        int vstep, const ChainArgs* ca = nullptr, ChainState* chs = nullptr,
+                                        int stage = 0) {
   constexpr int BM = BM_, BN = BN_, NT = 256;
   constexpr int A_BYTES = OpTile<BM, NT>::BYTES;
   constexpr int STAGE = A_BYTES + OpTile<BN, NT>::BYTES;
@@ -1085,15 +1213,31 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   // next tile starts its operand DMA while the previous tile's epilogue stores drain, instead of a new workgroup
   // waiting for the old one to retire (the 2-round grids: 8192x4096 forward and bwd-data). Not with the fused
   // bias gradient: its extra live registers would spill in the loop (the launcher gives it one tile per workgroup).
-  auto tile_body = [&](int v, bool first, int vn) __attribute__((always_inline)) {
-  const int wg = xcd_remap(v, tiles * split_k);
-  const int tile = wg % tiles, ksplit = wg / tiles;
+  static_assert(!CHAIN || (!SPLIT && !COLSUM && !ACCUM && BM == 256), "layer chain: unsplit 256-row tiles");
+  // output tile origin of virtual block v (CHAIN: of group-local ticket v, row panel by row panel)
   const int GM = tiles_m >= 4 ? 4 : tiles_m;
-  const int grp = tile / (GM * tiles_n);
-  const int gm = (tiles_m - grp * GM) < GM ? (tiles_m - grp * GM) : GM;
-  const int in_grp = tile % (GM * tiles_n);
-  const int m0 = (grp * GM + in_grp % gm) * BM;
-  const int n0 = (in_grp / gm) * BN;
+  auto tile_origin = [&](int v, int& m, int& n) __attribute__((always_inline)) {
+    if constexpr (CHAIN) {
+      int r, c;
+      chain_tile_rc(*ca, ca->st[stage].tn, v - ca->st[stage].first, r, c);
+      m = ((int)(blockIdx.x & 7) * ca->ppg + r) * BM;
+      n = c * BN;
+    } else {
+      const int t1 = xcd_remap(v, tiles * split_k) % tiles;
+      const int g1 = t1 / (GM * tiles_n);
+      const int gm1 = (tiles_m - g1 * GM) < GM ? (tiles_m - g1 * GM) : GM;
+      const int i1 = t1 % (GM * tiles_n);
+      m = (g1 * GM + i1 % gm1) * BM;
+      n = (i1 / gm1) * BN;
+    }
+  };
+  // CHAIN: the next ticket, whether its dependency is met, whether this run continues with it (same stage, OVL)
+  int ch_next = 0, ch_rdy = 0;
+  bool ch_cont = false;
+  auto tile_body = [&](int v, bool first, int vn) __attribute__((always_inline)) {
+  const int ksplit = CHAIN ? 0 : xcd_remap(v, tiles * split_k) / tiles;
+  int m0, n0;
+  tile_origin(v, m0, n0);
   const int k_per = K / split_k;
   const int kbeg = ksplit * k_per;
   const int nk = k_per / BK;
@@ -1181,26 +1325,62 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 #pragma unroll
   for (int r = 0; r < R; ++r) read_next(smem, 0, 0, r);
 
+  // CHAIN ticket control, run after a K-tile's barrier by every wave (the values live in wave 0 lane 0): at K-tile 1
+  // publish the previous tile (every wave's stores retired: each waited vmcnt(0) before this barrier) and take the
+  // next ticket; at nk - 3 poll its dependency (the dequeue returned by now); at nk - 2 post both to the LDS; at the
+  // last K-tile every wave reads them (chain_decide). The host guarantees nk >= 6.
+  unsigned ch_deq = 0, ch_poll = 0, ch_tgt = 0;
+  int ch_word = -1;
+  int* const ch_ctl = reinterpret_cast<int*>(smem + kChainLdsCtl);
+  auto chain_hook = [&](int kt) __attribute__((always_inline)) {
+    if constexpr (CHAIN) {
+      if (kt == 1) {
+        if (wave == 0 && lane == 0) {
+          if (chs->pending >= 0) chain_add(ca->ctr, chs->pending);
+          ch_deq = __hip_atomic_fetch_add(ca->ctr + (blockIdx.x & 7) * 16, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        }
+        chs->pending = -1;
+      } else if (kt == nk - 3) {
+        if (wave == 0 && lane == 0) {
+          chain_dep_of(*ca, (int)(gridDim.x >> 3) + (int)ch_deq, ch_word, ch_tgt);
+          ch_poll = ch_word >= 0 ? chain_poll(ca->ctr, ch_word) : 0u;
+        }
+      } else if (kt == nk - 2) {
+        if (wave == 0 && lane == 0) {
+          ch_ctl[0] = (int)(gridDim.x >> 3) + (int)ch_deq;
+          ch_ctl[1] = ch_word < 0 || ch_poll >= ch_tgt;
+        }
+      }
+    }
+  };
+  auto chain_decide = [&]() __attribute__((always_inline)) {
+    if constexpr (CHAIN) {
+      ch_next = __builtin_amdgcn_readfirstlane(ch_ctl[0]);
+      ch_rdy = __builtin_amdgcn_readfirstlane(ch_ctl[1]);
+      ch_cont = OVL && ch_rdy && ch_next < ca->total && chain_stage_of(*ca, ch_next) == stage;
+      if (ch_cont && ca->st[stage].dep > 0) chain_acquire(ca->flags);
+    }
+  };
   auto ktile = [&](int kt, auto more_c, auto more2_c) __attribute__((always_inline)) {
     const char* st = smem + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE;
     const bool csk = do_colsum && kt >= cs0 && kt < cs1;
     FAN_STAMP(0);
     if constexpr (STAGES == 2) {
       constexpr bool kLast = OVL && !decltype(more_c)::value && !decltype(more2_c)::value;
-      if constexpr (kLast) {
-        // the last K-tile: this tile's offsets are dead (its last DMA went out two K-tiles ago); the next tile's
-        // (if any) take their place, for the DMA of its K-tiles 0 and 1 in k-step 1 below
-        if (vn >= 0) {
-          const int t1 = xcd_remap(vn, tiles);
-          const int g1 = t1 / (GM * tiles_n);
-          const int gm1 = (tiles_m - g1 * GM) < GM ? (tiles_m - g1 * GM) : GM;
-          const int i1 = t1 % (GM * tiles_n);
-          const int m1 = (g1 * GM + i1 % gm1) * BM, n1 = (i1 / gm1) * BN;
+      // the last K-tile: this tile's offsets are dead (its last DMA went out two K-tiles ago); the next tile's
+      // (if any) take their place, for the DMA of its K-tiles 0 and 1 in k-step 1 below (CHAIN: known only after
+      // this K-tile's barrier)
+      auto next_offsets = [&](int vnn) __attribute__((always_inline)) {
+        int m1, n1;
+        tile_origin(vnn, m1, n1);
 #pragma unroll
-          for (int p = 0; p < GA; ++p) off[p] = piece_off<AK, BM, NT>(lda, m1, wave, lane, p);
+        for (int p = 0; p < GA; ++p) off[p] = piece_off<AK, BM, NT>(lda, m1, wave, lane, p);
 #pragma unroll
-          for (int p = GA; p < G; ++p) off[p] = piece_off<BKC, BN, NT>(ldb, n1, wave, lane, p - GA);
-        }
+        for (int p = GA; p < G; ++p) off[p] = piece_off<BKC, BN, NT>(ldb, n1, wave, lane, p - GA);
+      };
+      if constexpr (kLast && !CHAIN) {
+        if (vn >= 0) next_offsets(vn);
       }
       block(I0{}, T_{}, F_{}, st, 1, 0, csk, F_{});
       FAN_STAMP(1);
@@ -1211,10 +1391,18 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
       __builtin_amdgcn_s_barrier();
       FAN_STAMP(3);
       if constexpr (kLast) {
+        int vnn = vn;
+        if constexpr (CHAIN) {
+          chain_decide();
+          vnn = ch_cont ? ch_next : -1;
+          if (vnn >= 0) next_offsets(vnn);
+        }
         // fetch the next tile's first two K-tiles under this k-step's MFMAs (no fragment reads here: both stages
         // are free once every wave passed the barrier above)
-        block(I1{}, F_{}, F_{}, smem, 0, 0, csk, T_{}, vn >= 0);
+        block(I1{}, F_{}, F_{}, smem, 0, 0, csk, T_{}, vnn >= 0);
       } else {
+        if constexpr (!decltype(more_c)::value && !decltype(more2_c)::value) chain_decide();
+        else chain_hook(kt);
         block(I1{}, more_c, more2_c, smem + ((kt + 1) & 1) * STAGE, 0, kt + 2, csk, F_{});
         // the next K-tile's k-step-0 fragments (read above, long complete): one wait here instead of the compiler's
         // per-fragment ones in front of the next k-step's MFMAs
@@ -1230,6 +1418,8 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
       FAN_STAMP(2);
       __builtin_amdgcn_s_barrier();
       FAN_STAMP(3);
+      if constexpr (!decltype(more_c)::value && !decltype(more2_c)::value) chain_decide();
+      else chain_hook(kt);
       block(I1{}, more_c, F_{}, smem + ((kt + 1) % 3) * STAGE, 0, 0, csk, F_{});
       if constexpr (decltype(more_c)::value) waitcnt_known<63, 0>();
     }
@@ -1253,16 +1443,35 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   if constexpr (OVL) {
     // staging rows of its own (wave-private) beside the operand stages: nothing to wait for (the operand reads
     // retired before the last barrier; the next tile's DMA into the stages must stay in flight)
-    store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT, kSW>(acc, smem + 2 * STAGE, wave, lane, m0 + wm * WTM,
-                                                        n0 + wn * WTN, C, ldc, bias, aux, ldaux, M, N, ksplit, ws, wo);
+    store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT, kSW, WT>(acc, smem + 2 * STAGE, wave, lane, m0 + wm * WTM,
+                                                            n0 + wn * WTN, C, ldc, bias, aux, ldaux, M, N, ksplit, ws,
+                                                            wo);
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every operand read retired before the epilogue reuses the LDS
-    store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C, ldc, bias,
-                                                   aux, ldaux, M, N, ksplit, ws, wo);
+    store_tile<MI, NJ, WTN, EPI, TC, ACCUM, SPLIT, WTN, WT>(acc, smem, wave, lane, m0 + wm * WTM, n0 + wn * WTN, C,
+                                                            ldc, bias, aux, ldaux, M, N, ksplit, ws, wo);
   }
   };
-  if constexpr (COLSUM) {
+  if constexpr (CHAIN) {
+    // this stage's tiles while the next ticket continues it (the OVL transition already fetched its first K-tiles);
+    // each finished tile's completion goes to the next tile's K-tile 1 or to the chain loop (chs->pending)
+    const ChainStageArgs& S = ca->st[stage];
+    int v = chs->ticket;
+    for (bool first = true;; first = false) {
+      tile_body(v, first, -1);
+      if (S.signal) {
+        int r, c;
+        chain_tile_rc(*ca, S.tn, v - S.first, r, c);
+        chs->pending = chain_ready_word(*ca, stage, (int)(blockIdx.x & 7) * ca->ppg + r);
+      }
+      chs->ticket = ch_next;
+      chs->ready = ch_rdy;
+      if constexpr (!OVL) __syncthreads();  // every wave's staging reads done before the next DMA reuses the LDS
+      if (!ch_cont) break;
+      v = ch_next;
+    }
+  } else if constexpr (COLSUM) {
     if (v0 < tiles * split_k) tile_body(v0, true, -1);
   } else {
     for (int v = v0; v < tiles * split_k; v += vstep) {

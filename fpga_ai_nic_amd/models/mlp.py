@@ -174,6 +174,27 @@ class MLP:
         out = self.act[i + 1] if i + 1 < self.L else self.logits
         G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i))
 
+    def forward_chain(self) -> bool:
+        """Every layer's forward GEMM as ONE layer-chain launch (GPU bf16; ops/gemm.py linear_chain); False when the
+        chain does not take this model / batch (the caller then runs forward_layer per layer)."""
+        if not (self.device.type == "cuda" and self.dtype == torch.bfloat16 and self.L >= 2):
+            return False
+        outs = [self.act[i + 1] for i in range(self.L - 1)] + [self.logits]
+        epis = [G.EPI_BIAS_RELU if self._relu_at(i) else G.EPI_BIAS for i in range(self.L)]
+        return G.linear_chain(G.CHAIN_FWD, self.act[0], [l.w for l in self.layers], outs,
+                              biases=[self._bias_of(l) for l in self.layers], epis=epis, key=("fwd", id(self)))
+
+    def backward_data_chain(self) -> bool:
+        """The bwd-data GEMMs of layers L-1 .. 1 as ONE layer-chain launch (each masked by its input's ReLU); False
+        when the chain does not take them (the caller then runs backward_data per layer)."""
+        if not (self.device.type == "cuda" and self.dtype == torch.bfloat16 and self.L >= 3):
+            return False
+        if not all(self._relu_at(i - 1) for i in range(1, self.L)):
+            return False
+        idx = list(range(self.L - 1, 0, -1))
+        return G.linear_chain(G.CHAIN_BWD_DATA, self.dz[self.L], [self.layers[i].w for i in idx],
+                              [self.dz[i] for i in idx], auxes=[self.act[i] for i in idx], key=("bwd", id(self)))
+
     def loss_backward(self, labels, grad_scale: float):
         NN.softmax_xent(self.logits, labels, self.dz[self.L], self.loss_rows, grad_scale)
         if self._relu_at(self.L - 1):  # ReLU on the classifier output (reference fuse_type 2/3)

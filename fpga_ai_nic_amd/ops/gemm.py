@@ -236,6 +236,62 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
         run(plan, 0, update)
 
 
+# ---------------------------------------------------------------------------------------------------------------
+# Layer chain: the GEMMs of one MLP pass as ONE persistent launch (csrc/gemm/gemm_chain.hip): layer s + 1's tiles of a
+# 256-row panel start as soon as layer s has stored that panel, so the per-launch fill / drain is paid once per pass
+# (the reference runs its whole FWD / BWD loop in one OpenMP region, sw/mlp_mpi_example_f32.cpp:690-788). Same tiles,
+# same k order as the per-GEMM launches: bit-identical outputs. FAN_GEMM_CHAIN=1 enables it.
+CHAIN_FWD, CHAIN_BWD_DATA = 0, 1
+_chain_ctr: dict = {}
+
+
+def chain_enabled() -> bool:
+    import os
+
+    return os.environ.get("FAN_GEMM_CHAIN", "0") == "1"
+
+
+def _chain_counters(key, device, n: int, M: int):
+    """The chain's counter block for one call site (key) and stream: zeroed once, left zeroed by every launch."""
+    Cx = _ext.require()
+    words = int(Cx.gemm_chain_words(n, M))
+    sk = (key, device, torch.cuda.current_stream(device).cuda_stream)
+    t = _chain_ctr.get(sk)
+    if t is None or t.numel() < words:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        t = torch.zeros(words, dtype=torch.int32, device=device)
+        _chain_ctr[sk] = t
+    return t
+
+
+def chain_error(key=None) -> int:
+    """Error word of the chain counter blocks (0: none; else 1 + the ready-counter word a spin gave up on). Host sync."""
+    worst = 0
+    for (k, _, _), t in _chain_ctr.items():
+        if key is None or k == key:
+            worst = max(worst, int(t[9 * 16].item()))
+    return worst
+
+
+def linear_chain(kind: int, a0, ws, outs, biases=None, auxes=None, epis=None, key="chain", dry_run=False) -> bool:
+    """Run the layers' GEMMs as one chain launch; False (nothing launched) when the chain does not take them.
+    kind CHAIN_FWD: a0 = X, ws[i] = W_i [K][N], outs[i] = layer outputs (bf16, the last may be f32 logits), biases,
+    epis[i] = EPI_BIAS_RELU / EPI_BIAS. kind CHAIN_BWD_DATA: a0 = dZ, ws[i] = W [N][K] used transposed, outs[i] = dX
+    (bf16), auxes[i] = the activations whose ReLU mask applies (EPI_RELU_MASK)."""
+    if not (chain_enabled() and a0.is_cuda and a0.dtype == torch.bfloat16 and 2 <= len(ws) <= 8):
+        return False
+    n = len(ws)
+    biases = list(biases) if biases is not None else [None] * n
+    auxes = list(auxes) if auxes is not None else [None] * n
+    epis = list(epis) if epis is not None else [EPI_RELU_MASK if kind == CHAIN_BWD_DATA else EPI_BIAS_RELU] * n
+    ctr = _chain_counters(key, a0.device, n, a0.shape[0])
+    if ctr is None:
+        return False
+    return bool(_ext.require().gemm_chain(kind, a0, list(ws), list(outs), biases, auxes, [int(e) for e in epis], ctr,
+                                          dry_run))
+
+
 def linear_fwd(x, w, b, out, relu: bool):
     """Y = X · W + b (ReLU)."""
     return gemm(x, False, w, False, out, EPI_BIAS_RELU if relu else EPI_BIAS, bias=b)

@@ -117,6 +117,12 @@ class DataParallelTrainer:
         self.fused_update = (fu and self.prepack and bool(getattr(engine, "inline", False))
                              and getattr(engine, "codec", "") == "bfp_rne")
         self.fused_updates = 0
+        # layer-chain launches (ops/gemm.py linear_chain, FAN_GEMM_CHAIN): the forward at every world size; the
+        # bwd-data chain only with the fused world-1 update — with a multi-rank engine each layer's all-reduce is
+        # issued right after its own bwd-weight GEMM and overlaps that layer's bwd-data GEMM, which a chain of the
+        # bwd-data GEMMs would postpone
+        self.chain_fwd = G.chain_enabled()
+        self.chain_bwd = G.chain_enabled()
         gi = os.environ.get("FAN_GEMM_INFLIGHT", "persistent") if gemm_inflight is None else gemm_inflight
         if gi not in ("persistent", "grid"):
             raise ValueError(f"gemm_inflight must be persistent|grid, got {gi!r}")
@@ -153,9 +159,18 @@ class DataParallelTrainer:
         m.act[0] = x
         t0 = time.perf_counter()
         with tracing.range("fwd"):
-            for i in range(m.L):
-                self._wait_layer(i)  # layer i's weights updated (reference: per-layer wait, sw:757-787)
-                m.forward_layer(i)
+            # the whole forward as one layer-chain launch when it takes the model (every layer's update must have
+            # landed first: layer 0's, the last request of the backward, is the one it waits on in practice)
+            if self.cuda and self.chain_fwd:
+                for i in range(m.L):
+                    self._wait_layer(i)
+                chained = m.forward_chain()
+            else:
+                chained = False
+            if not chained:
+                for i in range(m.L):
+                    self._wait_layer(i)  # layer i's weights updated (reference: per-layer wait, sw:757-787)
+                    m.forward_layer(i)
             self.last_handle = None
         if self.profile:
             self._sync()
@@ -195,6 +210,12 @@ class DataParallelTrainer:
             t1 = time.perf_counter()
             self.times["loss"] += t1 - t0
             t0 = t1
+        # world 1 with the fused update on every layer: the bwd-data GEMMs of layers L-1 .. 1 as one layer-chain
+        # launch first (each layer's weights are read there before its bwd-weight GEMM updates them in place)
+        tgts = [(self.engine.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout)
+                 if self.prepack and l.cout % 16 == 0 else None) for l in m.layers]
+        chained = (self.fused_update and self.chain_bwd and all(t is not None for t in tgts)
+                   and m.backward_data_chain())
         try:
             for i in reversed(range(m.L)):
                 l = m.layers[i]
@@ -202,12 +223,12 @@ class DataParallelTrainer:
                     # the bwd-weight GEMM encodes dW (and the fused bias gradient) straight into the wire buffer;
                     # the zero tail (padding, or the bias segment of a bias-free model) is encoded once
                     # (the wire epilogue encodes whole 16-column groups: output widths that are multiples of 16)
-                    tgt = (self.engine.prepack_target(l.grad, l.n, None if m.bias else l.cin * l.cout)
-                           if self.prepack and l.cout % 16 == 0 else None)
+                    tgt = tgts[i]
                     if tgt is not None and self.fused_update:
                         # single-rank engine: bwd-data first (it reads W_i), then dW's BFP round trip + SGD in the
                         # bwd-weight epilogue
-                        m.backward_data(i)
+                        if not chained:
+                            m.backward_data(i)
                         upd = G.LocalUpdate(l.master, l.lp, l.mom, lr=self.lr, grad_scale=self.grad_scale,
                                             weight_decay=self.wd, momentum=self.momentum, nesterov=self.nesterov)
                         # (the bwd-weight GEMMs of layers >= 1 on a second stream, beside the next GEMM, measured 1.5-2 %
