@@ -323,12 +323,17 @@ __device__ __forceinline__ float sgd_apply(float g, float& w, float& m, bool has
 
 // Fused update of the 16-value group at flat index f (shared exponent E already computed): 16-B master / mom
 // loads and stores, one 32-B bf16 store.
-__device__ __forceinline__ void local_update16(const float v[16], uint32_t E, uint32_t f, const WireOut& wo) {
-  float w[16], m[16];
+// (PRE: the group's master values w[] were loaded ahead by the caller)
+template <bool PRE = false>
+__device__ __forceinline__ void local_update16(const float v[16], uint32_t E, uint32_t f, const WireOut& wo,
+                                               float (&w)[16]) {
+  float m[16];
+  if constexpr (!PRE) {
 #pragma unroll
-  for (int u = 0; u < 16; u += 4) {
-    const float4 a = *reinterpret_cast<const float4*>(wo.um + f + u);
-    w[u] = a.x; w[u + 1] = a.y; w[u + 2] = a.z; w[u + 3] = a.w;
+    for (int u = 0; u < 16; u += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(wo.um + f + u);
+      w[u] = a.x; w[u + 1] = a.y; w[u + 2] = a.z; w[u + 3] = a.w;
+    }
   }
   const bool hm = wo.umom != nullptr;
   if (hm) {
@@ -357,14 +362,14 @@ __device__ __forceinline__ void local_update16(const float v[16], uint32_t E, ui
 // Encode the 16-value group at flat bucket index f (f % 16 == 0) held by this lane: 16-B mantissa store +
 // 1 exponent byte (or, with the fused local update, the update of the group in place). Returns the shard it
 // landed in (-1: updated in place).
-template <bool UPD = false>
-__device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const WireOut& wo) {
+template <bool UPD = false, bool PRE = false>
+__device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const WireOut& wo, float (&wm)[16]) {
   uint32_t mx = 0;
 #pragma unroll
   for (int u = 0; u < 16; ++u) mx = max(mx, __float_as_uint(v[u]) & 0x7FFFFFFFu);
   const uint32_t E = mx >> 23;
   if constexpr (UPD) {
-    local_update16(v, E, f, wo);
+    local_update16<PRE>(v, E, f, wo, wm);
     return -1;
   }
   const int sh = wire_shard_of(f, wo);
@@ -378,17 +383,30 @@ __device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const
   return sh;
 }
 
-// Encode one whole 16-column group of C(row, col..col+15); the owner shard is also written to C in f32.
 template <bool UPD = false>
+__device__ __forceinline__ int wire_store16(const float v[16], uint32_t f, const WireOut& wo) {
+  float wm[16];
+  return wire_store16<UPD, false>(v, f, wo, wm);
+}
+
+// Encode one whole 16-column group of C(row, col..col+15); the owner shard is also written to C in f32.
+template <bool UPD = false, bool PRE = false>
 __device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
-                                           int row, int col) {
+                                           int row, int col, float (&w)[16]) {
   const uint32_t loc = (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
-  const int sh = wire_store16<UPD>(v, wo.off + loc, wo);
+  const int sh = wire_store16<UPD, PRE>(v, wo.off + loc, wo, w);
   if (sh >= 0 && (wo.own == kWireOwnAll || (wo.period > 0 ? sh % wo.period : sh) == wo.own)) {
 #pragma unroll
     for (int u = 0; u < 16; u += 4)
       *reinterpret_cast<float4*>(C + loc + u) = make_float4(v[u], v[u + 1], v[u + 2], v[u + 3]);
   }
+}
+
+template <bool UPD = false>
+__device__ __forceinline__ void wire_epi16(const float v[16], float* __restrict__ C, int64_t ldc, const WireOut& wo,
+                                           int row, int col) {
+  float w[16];
+  wire_epi16<UPD, false>(v, C, ldc, wo, row, col, w);
 }
 
 // Fused bias gradient tail: lanes l, l^16, l^32, l^48 hold the same column over different k rows. Writes
@@ -532,10 +550,38 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
 #pragma unroll
     for (int i = 0; i < kPf && i < MI; ++i) aux_load(i);
   }
+  // fused local update (unsplit wire epilogue): the master values of 16-row block i + 1's groups are loaded while
+  // block i is encoded and updated, instead of one dependent load round trip per block (all CUs run this epilogue
+  // at the same moment, so each round trip is a loaded-HBM latency)
+  constexpr bool kPfUpd = EPI == kEpiWireUpd && !SPLIT;
+  constexpr int UG16 = WTN / 16, URPG = 64 / UG16, UPASS = URPG >= 16 ? 1 : 16 / URPG;
+  float um_pf[kPfUpd ? 2 : 1][kPfUpd ? UPASS : 1][16];
+  auto upd_load = [&](int i, int slot) __attribute__((always_inline)) {
+    if constexpr (kPfUpd) {
+#pragma unroll
+      for (int pass = 0; pass < UPASS; ++pass) {
+        const int rr = pass * URPG + lane / UG16;
+        const int row = row0 + i * 16 + rr, col = col0 + (lane % UG16) * 16;
+        if ((URPG <= 16 || rr < 16) && (!mn_edge || (row < M && col < N))) {
+          const float* q = wo.um + wo.off + (uint32_t)row * (uint32_t)ldc + (uint32_t)col;
+#pragma unroll
+          for (int u = 0; u < 16; u += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(q + u);
+            um_pf[slot][pass][u] = a.x; um_pf[slot][pass][u + 1] = a.y;
+            um_pf[slot][pass][u + 2] = a.z; um_pf[slot][pass][u + 3] = a.w;
+          }
+        }
+      }
+    }
+  };
+  if constexpr (kPfUpd) upd_load(0, 0);
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     if constexpr (kPfAux) {
       if (i + kPf < MI) aux_load(i + kPf);
+    }
+    if constexpr (kPfUpd) {
+      if (i + 1 < MI) upd_load(i + 1, (i + 1) & 1);
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -558,7 +604,8 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
             v[u] = q.x; v[u + 1] = q.y; v[u + 2] = q.z; v[u + 3] = q.w;
           }
           if (!mn_edge || (row0 + i * 16 + rr < M && col0 + cc < N))
-            wire_epi16<EPI == kEpiWireUpd>(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr, col0 + cc);
+            wire_epi16<EPI == kEpiWireUpd, kPfUpd>(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr,
+                                                   col0 + cc, um_pf[kPfUpd ? (i & 1) : 0][kPfUpd ? pass : 0]);
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -809,11 +856,16 @@ __device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint3
 
 // The same with the LDS destination as a wave-uniform base + a compile-time byte offset, added into M0 by the
 // statement itself (1 SALU per piece instead of the compiler's add + the move).
-template <uint32_t OFF>
+template <uint32_t OFF, bool SC1 = false>
 __device__ __forceinline__ void glds16_si(const void* sbase, uint32_t voff, uint32_t lds_base) {
-  asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase),
-               "s"(lds_base), "i"(OFF)
-               : "memory", "scc");
+  if constexpr (SC1)  // bypassing this CU's L1 (the layer chain's handed-off operand: no stale L1 copy can be hit)
+    asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 sc1" ::"v"(voff), "s"(sbase),
+                 "s"(lds_base), "i"(OFF)
+                 : "memory", "scc");
+  else
+    asm volatile("s_add_u32 m0, %2, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase),
+                 "s"(lds_base), "i"(OFF)
+                 : "memory", "scc");
 }
 
 // s_waitcnt vmcnt(VM) lgkmcnt(LGKM) through the compiler's builtin, so that its own wait insertion knows what the wait
@@ -1114,6 +1166,29 @@ struct ChainState {
   int pending;
 };
 
+// one stage's schedule for the tile loop, derived once per stage run from the kernel arguments and passed by value so
+// it lives in SGPRs: the loop never reads the kernel-argument block through a pointer (such reads are vector loads
+// whose compiler-inserted vmcnt(0) would drain the loop's in-flight LDS-DMA and epilogue stores)
+struct ChainRun {
+  unsigned* ctr;
+  int group, ppg, wpg;  // XCD group, its row panels, its static tickets
+  int first, end, tn;   // this stage's ticket range and column tiles
+  int dep;              // > 0: a tile waits until the previous stage's panel counter reaches dep
+  int dep_word0;        // that counter's word for the group's first panel (+ 16 per panel)
+  int sig_word0;        // this stage's counter word for the group's first panel; -1: no consumer stage
+  int nx_end, nx_tn;    // the next stage's ticket end and column tiles (its tickets start at end)
+  int flags;
+};
+__device__ __forceinline__ void chain_rc(const ChainRun& cr, int tn, int k, int& r, int& c) {
+  if (cr.flags & kChainRowsFastest) {
+    r = k % cr.ppg;
+    c = k / cr.ppg;
+  } else {
+    r = k / tn;
+    c = k % tn;
+  }
+}
+
 __device__ __forceinline__ void chain_add(unsigned* ctr, int word) {
   __hip_atomic_fetch_add(ctr + word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1164,13 +1239,12 @@ __device__ __forceinline__ void chain_dep_of(const ChainArgs& ca, int t, int& wo
 // run returns to the chain loop when the next ticket belongs to another stage or is not known ready (chs). WT: the
 // bf16 epilogue stores write through the L2 (a producer stage of the chain).
 template <bool AK, bool BKC, int EPI, typename TC, bool ACCUM, bool SPLIT, bool COLSUM = false, int BN_ = 256,
-          int BM_ = 256, bool OVL = false, bool CHAIN = false, bool WT = false>
+          int BM_ = 256, bool OVL = false, bool CHAIN = false, bool WT = false, bool ASC1 = false>
 __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ B,
                                         int64_t ldb, TC* __restrict__ C, int64_t ldc, const bf16_t* __restrict__ bias,
                                         const TC* __restrict__ aux, int64_t ldaux, int M, int N, int K, int split_k,
                                         float* __restrict__ ws, float* __restrict__ colsum, const WireOut& wo, int v0,
-                                        int vstep, const ChainArgs* ca = nullptr, ChainState* chs = nullptr,
-                                        int stage = 0) {
+                                        int vstep, ChainRun cr = ChainRun{}, ChainState* chs = nullptr) {
   constexpr int BM = BM_, BN = BN_, NT = 256;
   constexpr int A_BYTES = OpTile<BM, NT>::BYTES;
   constexpr int STAGE = A_BYTES + OpTile<BN, NT>::BYTES;
@@ -1219,8 +1293,8 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   auto tile_origin = [&](int v, int& m, int& n) __attribute__((always_inline)) {
     if constexpr (CHAIN) {
       int r, c;
-      chain_tile_rc(*ca, ca->st[stage].tn, v - ca->st[stage].first, r, c);
-      m = ((int)(blockIdx.x & 7) * ca->ppg + r) * BM;
+      chain_rc(cr, cr.tn, v - cr.first, r, c);
+      m = (cr.group * cr.ppg + r) * BM;
       n = c * BN;
     } else {
       const int t1 = xcd_remap(v, tiles * split_k) % tiles;
@@ -1273,7 +1347,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   auto piece = [&](int kt, auto pc) __attribute__((always_inline)) {
     constexpr int p = decltype(pc)::value;
     const uint32_t st = lds0 + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE + wave * 1024;
-    if constexpr (p < GA) glds16_si<p * OpTile<BM, NT>::IB>(a_k0 + kt * a_step, off[p], st);
+    if constexpr (p < GA) glds16_si<p * OpTile<BM, NT>::IB, ASC1>(a_k0 + kt * a_step, off[p], st);
     else glds16_si<A_BYTES + (p - GA) * OpTile<BN, NT>::IB>(b_k0 + kt * b_step, off[p], st);
   };
   // next k-step's fragment r (0..R-1: A rows 0..7, then B columns 0..NJ-1) into set `set`
@@ -1325,31 +1399,48 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 #pragma unroll
   for (int r = 0; r < R; ++r) read_next(smem, 0, 0, r);
 
-  // CHAIN ticket control, run after a K-tile's barrier by every wave (the values live in wave 0 lane 0): at K-tile 1
-  // publish the previous tile (every wave's stores retired: each waited vmcnt(0) before this barrier) and take the
-  // next ticket; at nk - 3 poll its dependency (the dequeue returned by now); at nk - 2 post both to the LDS; at the
-  // last K-tile every wave reads them (chain_decide). The host guarantees nk >= 6.
-  unsigned ch_deq = 0, ch_poll = 0, ch_tgt = 0;
-  int ch_word = -1;
+  // CHAIN ticket control, run after a K-tile's barrier by every wave (wave 0 lane 0 acts; its values go through the
+  // LDS control words so that only the poll result lives in a register across K-tiles): at K-tile 1 publish the
+  // previous tile (every wave's stores retired: each waited vmcnt(0) before this barrier) and take the next ticket
+  // (ctl[0]); at nk - 3 poll its dependency — in this stage on the previous stage's panel, in the next stage on this
+  // stage's panel, further stages left to the chain loop (ctl[2] = -2) — and at nk - 2 post the verdict (ctl[1]); at
+  // the last K-tile every wave reads them (chain_decide). The host guarantees nk >= 6.
+  unsigned ch_poll = 0;
   int* const ch_ctl = reinterpret_cast<int*>(smem + kChainLdsCtl);
   auto chain_hook = [&](int kt) __attribute__((always_inline)) {
     if constexpr (CHAIN) {
       if (kt == 1) {
         if (wave == 0 && lane == 0) {
-          if (chs->pending >= 0) chain_add(ca->ctr, chs->pending);
-          ch_deq = __hip_atomic_fetch_add(ca->ctr + (blockIdx.x & 7) * 16, 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+          if (chs->pending >= 0) chain_add(cr.ctr, chs->pending);
+          ch_ctl[0] = cr.wpg + (int)__hip_atomic_fetch_add(cr.ctr + cr.group * 16, 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
         }
         chs->pending = -1;
       } else if (kt == nk - 3) {
         if (wave == 0 && lane == 0) {
-          chain_dep_of(*ca, (int)(gridDim.x >> 3) + (int)ch_deq, ch_word, ch_tgt);
-          ch_poll = ch_word >= 0 ? chain_poll(ca->ctr, ch_word) : 0u;
+          const int t = ch_ctl[0];
+          int r, c, word = -1, tgt = 0;
+          if (t < cr.end) {
+            if (cr.dep > 0) {
+              chain_rc(cr, cr.tn, t - cr.first, r, c);
+              word = cr.dep_word0 + r * 16;
+              tgt = cr.dep;
+            }
+          } else if (t < cr.nx_end && cr.sig_word0 >= 0) {
+            chain_rc(cr, cr.nx_tn, t - cr.end, r, c);
+            word = cr.sig_word0 + r * 16;
+            tgt = cr.tn;
+          } else {
+            word = -2;
+          }
+          ch_ctl[2] = word;
+          ch_ctl[3] = tgt;
+          if (word >= 0) ch_poll = chain_poll(cr.ctr, word);
         }
       } else if (kt == nk - 2) {
         if (wave == 0 && lane == 0) {
-          ch_ctl[0] = (int)(gridDim.x >> 3) + (int)ch_deq;
-          ch_ctl[1] = ch_word < 0 || ch_poll >= ch_tgt;
+          const int word = ch_ctl[2];
+          ch_ctl[1] = word == -1 || (word >= 0 && ch_poll >= (unsigned)ch_ctl[3]);  // 0: not met or not known
         }
       }
     }
@@ -1358,8 +1449,8 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     if constexpr (CHAIN) {
       ch_next = __builtin_amdgcn_readfirstlane(ch_ctl[0]);
       ch_rdy = __builtin_amdgcn_readfirstlane(ch_ctl[1]);
-      ch_cont = OVL && ch_rdy && ch_next < ca->total && chain_stage_of(*ca, ch_next) == stage;
-      if (ch_cont && ca->st[stage].dep > 0) chain_acquire(ca->flags);
+      ch_cont = OVL && ch_rdy && ch_next < cr.end;
+      if (ch_cont && cr.dep > 0) chain_acquire(cr.flags);
     }
   };
   auto ktile = [&](int kt, auto more_c, auto more2_c) __attribute__((always_inline)) {
@@ -1456,14 +1547,13 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   if constexpr (CHAIN) {
     // this stage's tiles while the next ticket continues it (the OVL transition already fetched its first K-tiles);
     // each finished tile's completion goes to the next tile's K-tile 1 or to the chain loop (chs->pending)
-    const ChainStageArgs& S = ca->st[stage];
     int v = chs->ticket;
     for (bool first = true;; first = false) {
       tile_body(v, first, -1);
-      if (S.signal) {
+      if (cr.sig_word0 >= 0) {
         int r, c;
-        chain_tile_rc(*ca, S.tn, v - S.first, r, c);
-        chs->pending = chain_ready_word(*ca, stage, (int)(blockIdx.x & 7) * ca->ppg + r);
+        chain_rc(cr, cr.tn, v - cr.first, r, c);
+        chs->pending = cr.sig_word0 + r * 16;
       }
       chs->ticket = ch_next;
       chs->ready = ch_rdy;

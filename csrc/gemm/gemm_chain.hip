@@ -15,15 +15,29 @@ using namespace gemm_detail;
 namespace gemm_detail {
 
 // one stage's tile configuration: the persistent 4-wave loop in chain mode
-template <bool AK, bool BKC, int EPI, typename TC, int BN_, bool OVL, bool WT>
+template <bool AK, bool BKC, int EPI, typename TC, int BN_, bool OVL, bool WT, bool ASC1 = false>
 struct ChainCfg {
   __device__ static __forceinline__ void run(const ChainArgs& ca, ChainState* cs, int s) {
     const ChainStageArgs& S = ca.st[s];
     WireOut wo{};
     wo.prio = ca.prio;
-    pl4_run<AK, BKC, EPI, TC, false, false, false, BN_, 256, OVL, true, WT>(
+    ChainRun cr;
+    cr.ctr = ca.ctr;
+    cr.group = (int)(blockIdx.x & 7);
+    cr.ppg = ca.ppg;
+    cr.wpg = (int)(gridDim.x >> 3);
+    cr.first = S.first;
+    cr.end = s + 1 < ca.nstages ? ca.st[s + 1].first : ca.total;
+    cr.tn = S.tn;
+    cr.dep = S.dep;
+    cr.dep_word0 = s > 0 ? chain_ready_word(ca, s - 1, cr.group * ca.ppg) : 0;
+    cr.sig_word0 = S.signal ? chain_ready_word(ca, s, cr.group * ca.ppg) : -1;
+    cr.nx_end = s + 2 < ca.nstages ? ca.st[s + 2].first : ca.total;
+    cr.nx_tn = s + 1 < ca.nstages ? ca.st[s + 1].tn : 1;
+    cr.flags = ca.flags;
+    pl4_run<AK, BKC, EPI, TC, false, false, false, BN_, 256, OVL, true, WT, ASC1>(
         S.A, S.lda, S.B, S.ldb, reinterpret_cast<TC*>(S.C), S.ldc, S.bias, reinterpret_cast<const TC*>(S.aux),
-        S.ldaux, S.M, S.N, S.K, 1, nullptr, nullptr, wo, 0, 0, &ca, cs, s);
+        S.ldaux, S.M, S.N, S.K, 1, nullptr, nullptr, wo, 0, 0, cr, cs);
   }
 };
 
@@ -106,6 +120,10 @@ using BwdData = ChainCfg<true, true, kEpiReluMask, bf16_t, 256, true, true>;
 // diagnostic (FAN_CHAIN_WT=0, unsafe): plain producer stores
 using FwdHiddenP = ChainCfg<true, false, kEpiBiasRelu, bf16_t, 256, true, false>;
 using BwdDataP = ChainCfg<true, true, kEpiReluMask, bf16_t, 256, true, false>;
+// diagnostic (FAN_CHAIN_ASC1=1): the A operand's LDS-DMA bypasses L1 (sc1) and no acquire
+using FwdHiddenS = ChainCfg<true, false, kEpiBiasRelu, bf16_t, 256, true, true, true>;
+using FwdLogitsS = ChainCfg<true, false, kEpiBias, float, 128, false, false, true>;
+using BwdDataS = ChainCfg<true, true, kEpiReluMask, bf16_t, 256, true, true, true>;
 
 int env_int(const char* name, int dflt) {
   const char* e = std::getenv(name);
@@ -135,7 +153,7 @@ int gemm_chain_counter_words(int n, int M) { return chain_ctr_words(n, M / kPane
 int gemm_chain_max_stages() { return kChainMaxStages; }
 
 bool gemm_chain_supported(const GemmArgs* a, int n, int kind) {
-  if (n < 2 || n > kChainMaxStages) return false;
+  if (n < 1 || n > kChainMaxStages) return false;
   for (int i = 0; i < n; ++i) {
     const GemmArgs& g = a[i];
     if (stage_cfg(g, kind, i == n - 1) < 0 || g.M != a[0].M) return false;
@@ -161,7 +179,8 @@ void launch_gemm_chain(const GemmArgs* a, int n, int kind, unsigned* counters, h
   static const int diag_flags = (env_int("FAN_CHAIN_ACQ", 1) == 0 ? kChainNoAcquire : 0) |
                                 (env_int("FAN_CHAIN_ORDER", 0) == 1 ? kChainRowsFastest : 0);
   static const bool plain = env_int("FAN_CHAIN_WT", 1) == 0;
-  ca.flags = diag_flags;
+  static const bool asc1 = env_int("FAN_CHAIN_ASC1", 0) == 1;
+  ca.flags = diag_flags | (asc1 ? kChainNoAcquire : 0);
   int first = 0;
   for (int i = 0; i < n; ++i) {
     const GemmArgs& g = a[i];
@@ -186,8 +205,11 @@ void launch_gemm_chain(const GemmArgs* a, int n, int kind, unsigned* counters, h
     first += ca.ppg * S.tn;
   }
   ca.total = first;
-  auto k = kind == kChainFwd ? (plain ? gemm_chain_kernel<FwdHiddenP, FwdLogits> : gemm_chain_kernel<FwdHidden, FwdLogits>)
-                             : (plain ? gemm_chain_kernel<BwdDataP, BwdDataP> : gemm_chain_kernel<BwdData, BwdData>);
+  auto k = kind == kChainFwd
+               ? (asc1 ? gemm_chain_kernel<FwdHiddenS, FwdLogitsS>
+                       : plain ? gemm_chain_kernel<FwdHiddenP, FwdLogits> : gemm_chain_kernel<FwdHidden, FwdLogits>)
+               : (asc1 ? gemm_chain_kernel<BwdDataS, BwdDataS>
+                       : plain ? gemm_chain_kernel<BwdDataP, BwdDataP> : gemm_chain_kernel<BwdData, BwdData>);
   FAN_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
   hipLaunchKernelGGL(k, kNumCU, 256, kChainLds, s, ca);
   FAN_HIP_CHECK(hipGetLastError());

@@ -279,7 +279,7 @@ def linear_chain(kind: int, a0, ws, outs, biases=None, auxes=None, epis=None, ke
     kind CHAIN_FWD: a0 = X, ws[i] = W_i [K][N], outs[i] = layer outputs (bf16, the last may be f32 logits), biases,
     epis[i] = EPI_BIAS_RELU / EPI_BIAS. kind CHAIN_BWD_DATA: a0 = dZ, ws[i] = W [N][K] used transposed, outs[i] = dX
     (bf16), auxes[i] = the activations whose ReLU mask applies (EPI_RELU_MASK)."""
-    if not (chain_enabled() and a0.is_cuda and a0.dtype == torch.bfloat16 and 2 <= len(ws) <= 8):
+    if not (chain_enabled() and a0.is_cuda and a0.dtype == torch.bfloat16 and 1 <= len(ws) <= 8):
         return False
     n = len(ws)
     biases = list(biases) if biases is not None else [None] * n

@@ -112,3 +112,19 @@ def test_bench_prints_the_headline_when_an_extra_hangs(tmp_path):
     rec = recs[0]
     assert rec["extra"]["aborted_in"] == "extra uncompressed" and rec["value"] > 0 and rec["n_gpus"] == 2
     assert "config4" in rec["extra"] and rec["extra"]["dist"] is None
+
+
+def test_uncompressed_speedup_guard():
+    """extra.uncompressed.speedup_vs_best_uncompressed is withheld when it would not measure the codec: ranks
+    time-sharing one GPU, or an uncompressed arm dominated by its own P2P flag-wait stalls."""
+    import bench
+
+    arms = {"p2p_raw_f32_mesh": {"ms_per_step": 4.0, "p2p_stall_ms_per_step": 0.5}, "rccl_f32": {"skipped": "x"}}
+    sp, note = bench._uncompressed_speedup(arms, 2.0, ["a", "b", "c"])
+    assert sp == 2.0 and "fastest" in note
+    sp, note = bench._uncompressed_speedup(arms, 2.0, ["a", "a", "a"])
+    assert sp is None and "share a GPU" in note
+    arms["p2p_raw_f32_mesh"]["p2p_stall_ms_per_step"] = 3.0
+    sp, note = bench._uncompressed_speedup(arms, 2.0, ["a", "b"])
+    assert sp is None and "stall" in note
+    assert bench._uncompressed_speedup({"rccl_f32": {"skipped": "x"}}, 2.0, [None])[0] is None
