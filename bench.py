@@ -80,6 +80,9 @@ def parse_args(argv=None):
     ap.add_argument("--transport", default="native", choices=["torch", "native", "p2p"],
                     help="torch/native: RCCL collectives; p2p: direct HIP-IPC peer writes + stream flags "
                          "(C++ engine only)")
+    ap.add_argument("--p2p-flags", default="cp", choices=["cp", "kernel"],
+                    help="fixed schedule, p2p transport: flag writes/waits as command-processor packets or as kernels "
+                         "(system-scope release store, bounded in-kernel spin)")
     ap.add_argument("--p2p-copy", default="kernel", choices=["kernel", "sdma"],
                     help="--schedule fixed over --transport p2p: pure copies on CUs (kernel) or the copy engines")
     ap.add_argument("--shard-update", type=int, default=-1, choices=[-1, 0, 1],
@@ -264,7 +267,7 @@ def main(argv=None):
 
     def build(name, kind, algo="mesh", rings=1, transport="auto", gemm="persistent", sdma=False, fused=None,
               force=False, ring_sub=0, epi=None, engine=None, sizes=None, mdtype=None, bias=True,
-              relu="hidden", shard=None):
+              relu="hidden", shard=None, kflag=False):
         """Engine + model + trainer of one arm. kind: bfp | raw | rccl | local; transport: native | p2p | torch |
         auto (the world-1 / CPU default); engine: python | native (default: the run's)."""
         comm = None
@@ -279,6 +282,7 @@ def main(argv=None):
             if comm is None:
                 raise RuntimeError(f"P2P transport unavailable: {ctx['p2p_err']}")
             comm.sdma = sdma
+            comm.kernel_flags = kflag
         elif force and cuda and impl == "native":  # world-1 split: the multi-rank path over a 1-rank RCCL group
             t = NativeTransport(force_collectives=True)
         eng = make_engine(t, kind, rounding=a.rounding, algo=algo, rings=rings, force_comm=force or a.force_dist,
@@ -296,6 +300,7 @@ def main(argv=None):
         info = {"compress": kind, "algo": algo, "rings": getattr(eng, "rings", 0) if eng is not None else 0,
                 "transport": (getattr(t, "name", transport) if comm is None else "p2p") if multi or force else "none",
                 "gemm_inflight": tr.gemm_inflight, "copy": ("sdma" if sdma else "kernel") if comm is not None else None,
+                "flags": ("kernel" if kflag else "cp") if comm is not None else None,
                 "ring_sub": int(getattr(eng, "ring_sub", 1)) if algo == "ring" else None,
                 "epilogue_stream": ("compute" if getattr(eng, "epilogue_on_producer", False) else "comm")
                 if eng is not None and not getattr(eng, "inline", True) else "inline",
@@ -335,6 +340,7 @@ def main(argv=None):
         held["engine"] = setup.engine
         if setup.info.get("copy") is not None and ctx["p2p"] is not None:  # the arm's copy path (shared comm)
             ctx["p2p"].sdma = setup.info["copy"] == "sdma"
+            ctx["p2p"].kernel_flags = setup.info.get("flags") == "kernel"
         try:
             return _run(setup, mb, seed, warmup, steps, tag, graph_ok, trace, wait_s)
         finally:
@@ -465,6 +471,11 @@ def main(argv=None):
             # bf16 weights into the layer's next weight buffer (no deferred epilogue, 1/N of the update pass per rank)
             arms.append(dict(name="rccl_mesh_shard", kind="bfp", algo="mesh", transport="native", shard=True))
             arms.append(dict(name="p2p_mesh_shard", kind="bfp", algo="mesh", transport="p2p", shard=True))
+            # the flag writes / waits as kernels (system-scope release store, bounded in-kernel spin + acquire) instead
+            # of command-processor packets: the CP-independent synchronisation path (p2p_comm.h, kernel flags)
+            arms.append(dict(name="p2p_mesh_kflag", kind="bfp", algo="mesh", transport="p2p", kflag=True))
+            arms.append(dict(name="p2p_mesh_shard_kflag", kind="bfp", algo="mesh", transport="p2p", shard=True,
+                             kflag=True))
             # each request's decode + SGD epilogue on the comm stream as soon as its all-gather lands (overlapping the
             # rest of the backward) instead of on the compute stream after the last backward GEMM
             arms.append(dict(name="rccl_mesh_epicomm", kind="bfp", algo="mesh", transport="native", epi="comm"))
@@ -476,6 +487,10 @@ def main(argv=None):
                              fallback=True))
         else:
             arms.append(dict(name=f"{impl}_{a.algo}", kind="bfp", algo=a.algo, rings=a.rings, transport="torch"))
+        only = [x for x in os.environ.get("FAN_AB_ARMS", "").split(",") if x]
+        if only:  # diagnostics: the A/B over the named arms only (in the listed order), the fallback kept
+            arms = [next(x for x in arms if x["name"] == n) for n in only if any(x["name"] == n for x in arms)] + [
+                x for x in arms if x.get("fallback")]
         schedule_ab = []
         arm_gates = {}
         kept = []  # (record, setup) of the fastest exact arms of stage 1, fastest first (at most --ab2-top)
@@ -490,7 +505,7 @@ def main(argv=None):
             try:
                 setup = build(spec["name"], spec["kind"], algo=spec.get("algo", "mesh"), rings=spec.get("rings", 1),
                               transport=spec["transport"], gemm=spec.get("gemm", "persistent"),
-                              sdma=spec.get("sdma", False),
+                              sdma=spec.get("sdma", False), kflag=spec.get("kflag", False),
                               ring_sub=spec.get("ring_sub", 1), epi=spec.get("epi"), engine=spec.get("engine"),
                               shard=spec.get("shard", False))
                 rec.update(setup.info)
@@ -599,6 +614,7 @@ def main(argv=None):
         main_setup = build("main", a.compress, algo=a.algo, rings=a.rings, transport=transport,
                            gemm=a.gemm_inflight, force=a.force_dist and impl == "native" and transport == "auto",
                            sdma=a.p2p_copy == "sdma" and transport == "p2p",
+                           kflag=a.p2p_flags == "kernel" and transport == "p2p",
                            shard=None if a.shard_update < 0 else bool(a.shard_update))
         if multi and main_setup.engine is not None:
             gate_rec = gate.allreduce_exactness(main_setup.engine)
@@ -680,6 +696,7 @@ def main(argv=None):
                 "p2p_release": ({0: "none", 1: "block", 2: "thread", 3: "cp"}[_release_mode()]
                                 if info["copy"] is not None else None),
                 "p2p_cross_device": bool(ctx["p2p"].cross_device) if ctx["p2p"] is not None else None,
+                "p2p_flags": info.get("flags"),
                 "hip_graph": graphed,
                 "fused_sgd": True,
                 # world 1: dW's BFP round trip + SGD inside the bwd-weight GEMM epilogue (no separate update pass)

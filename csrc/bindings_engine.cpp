@@ -22,6 +22,26 @@ void register_engine(pybind11::module_& m) {
   m.def("nccl_version", &nccl_version);
   m.def("p2p_release_event_needed", &p2p_release_event_needed,
         "whether a P2P round records the system-scope release event before its flags (release mode, copy-engine bytes)");
+  m.def(
+      "p2p_round_flags",
+      [](int rank, int world, uint64_t seq, const std::vector<int>& to, const std::vector<int>& from,
+         const std::vector<uint64_t>& last_sent) {
+        FAN_CHECK((int)last_sent.size() == world, "p2p_round_flags: last_sent needs one entry per rank");
+        const RoundFlags r = p2p_round_flags(rank, world, seq, to, from, last_sent);
+        auto conv = [](const std::vector<FlagRef>& v) {
+          std::vector<std::tuple<int, int, uint64_t>> o;
+          for (const FlagRef& f : v) o.emplace_back(f.peer, f.word, f.value);
+          return o;
+        };
+        py::dict d;
+        d["credit_waits"] = conv(r.credit_waits);
+        d["ready_writes"] = conv(r.ready_writes);
+        d["ready_waits"] = conv(r.ready_waits);
+        d["ack_writes"] = conv(r.ack_writes);
+        return d;
+      },
+      "the flag words one P2P round touches (peer, word, value): credit waits, ready writes, ready waits, acks -- "
+      "the protocol the CP and kernel-flag arms both execute");
   m.def("p2p_coalesce_copies",
         [](const std::vector<std::tuple<uint64_t, uint64_t, uint64_t>>& segs) {
           std::vector<P2PCopy> in;
@@ -79,6 +99,10 @@ void register_engine(pybind11::module_& m) {
            },
            "diagnostics: this rank's receive arena as a uint8 tensor (no copy)")
       .def("set_timing", &P2PComm::set_timing, "time every flag wait with device events (stall counters)")
+      .def_property("kernel_flags", &P2PComm::kernel_flags, &P2PComm::set_kernel_flags,
+                    "flag writes / waits as kernels (system-scope release store / bounded spin + acquire) instead of "
+                    "command-processor packets; switch between rounds only")
+      .def("kernel_flag_error", &P2PComm::kernel_flag_error, "1 when a kernel-flag wait gave up after its bound")
       .def("stats",
            [](P2PComm& c) {
              P2PComm::Stats t;
@@ -93,6 +117,8 @@ void register_engine(pybind11::module_& m) {
              d["ready_stall_ms"] = t.ready_stall_ms;
              d["credit_stall_ms"] = t.credit_stall_ms;
              d["bytes_to_peer"] = t.bytes_to_peer;
+             d["kernel_flags"] = c.kernel_flags();
+             d["kernel_flag_error"] = c.kernel_flag_error();
              return d;
            },
            "device-side stall counters: flag waits (ready / credit), their device time when timed, bytes per peer")

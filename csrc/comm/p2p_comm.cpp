@@ -53,6 +53,7 @@ P2PComm::P2PComm(int rank, int world, int device, size_t slot_bytes, int depth)
   }
   FAN_CHECK(slot_ > kTrailerBytes, "slot_bytes must exceed the 256-B verify trailer");
   if (const char* c = std::getenv("FAN_P2P_COPY")) sdma_ = !std::strcmp(c, "sdma");
+  if (const char* c = std::getenv("FAN_P2P_FLAGS")) kflags_ = !std::strcmp(c, "kernel");
   FAN_HIP_CHECK(hipSetDevice(device));
   // Arena and flags UNCACHED (see the memory-ordering argument in p2p_comm.h): peers write them over xGMI, so no
   // line of them may sit in this GPU's (per-XCD, non-coherent) L2 when the reader consumes a new message.
@@ -105,13 +106,37 @@ bool p2p_release_event_needed(int mode, bool copy_engine_bytes) {
   return mode == 3 || copy_engine_bytes;
 }
 
+RoundFlags p2p_round_flags(int rank, int world, uint64_t seq, const std::vector<int>& to, const std::vector<int>& from,
+                           const std::vector<uint64_t>& last_sent_in_slot) {
+  RoundFlags r;
+  for (int p : to) {
+    if (last_sent_in_slot[p]) r.credit_waits.push_back({rank, world + p, last_sent_in_slot[p]});
+    r.ready_writes.push_back({p, rank, seq});
+  }
+  for (int q : from) {
+    r.ready_waits.push_back({rank, q, seq});
+    r.ack_writes.push_back({q, world + rank, seq});
+  }
+  return r;
+}
+
 void P2PComm::release_before_flags(hipStream_t s) {
   if (p2p_release_event_needed(p2p_release_mode(), nonkernel_pending_)) FAN_HIP_CHECK(hipEventRecord(rel_ev_, s));
   nonkernel_pending_ = false;
 }
 
-void P2PComm::wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool credit) {
-  (credit ? credit_waits_ : ready_waits_)++;
+void P2PComm::write_flags(hipStream_t s, const std::vector<FlagOp>& w) {
+  if (w.empty()) return;
+  if (kflags_) {
+    launch_flag_write(w, s);
+    return;
+  }
+  for (const FlagOp& f : w) FAN_HIP_CHECK(hipStreamWriteValue64(s, f.first, f.second, 0));
+}
+
+void P2PComm::wait_flags(hipStream_t s, const std::vector<FlagOp>& w, bool credit) {
+  if (w.empty()) return;
+  (credit ? credit_waits_ : ready_waits_) += w.size();
   TimedWait* t = nullptr;
   if (timing_) {
     if (tw_used_ == tw_.size()) {
@@ -124,8 +149,23 @@ void P2PComm::wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool cred
     t->credit = credit;
     FAN_HIP_CHECK(hipEventRecord(t->ev[0], s));
   }
-  FAN_HIP_CHECK(hipStreamWaitValue64(s, flag, value, hipStreamWaitValueGte));
+  if (kflags_) {
+    if (kflag_err_ == nullptr) {
+      FAN_HIP_CHECK(hipMalloc(&kflag_err_, sizeof(unsigned)));
+      FAN_HIP_CHECK(hipMemset(kflag_err_, 0, sizeof(unsigned)));
+    }
+    launch_flag_wait(w, kflag_err_, s);
+  } else {
+    for (const FlagOp& f : w) FAN_HIP_CHECK(hipStreamWaitValue64(s, f.first, f.second, hipStreamWaitValueGte));
+  }
   if (t) FAN_HIP_CHECK(hipEventRecord(t->ev[1], s));
+}
+
+unsigned P2PComm::kernel_flag_error() const {
+  if (kflag_err_ == nullptr) return 0;
+  unsigned v = 0;
+  FAN_HIP_CHECK(hipMemcpy(&v, kflag_err_, sizeof(v), hipMemcpyDeviceToHost));
+  return v;
 }
 
 P2PComm::Stats P2PComm::stats(bool wait) {
@@ -225,6 +265,7 @@ P2PComm::~P2PComm() {
     hipEventDestroy(t.ev[1]);
   }
   if (rel_ev_) hipEventDestroy(rel_ev_);
+  if (kflag_err_) hipFree(kflag_err_);
   hipFree(flags_);
   hipFree(arena_);
 }
@@ -322,8 +363,6 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       FAN_CHECK(p != rank_, "p2p: self-send");
       FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
       if (!any) {
-        const uint64_t prev = last_sent_[par][p];
-        if (prev) wait_flag(s, flags_ + world_ + p, prev, true);
         any = true;
         dests.push_back(p);
       }
@@ -333,12 +372,12 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       off += (op.bytes + 15) / 16 * 16;
     }
   }
+  const RoundFlags sf = p2p_round_flags(rank_, world_, q, dests, {}, last_sent_[par]);
+  wait_flags(s, flag_ptrs(sf.credit_waits), true);
   copy(out, s);
   release_before_flags(s);
-  for (int p : dests) {
-    FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, q, 0));  // "ready from rank_" at p
-    last_sent_[par][p] = q;
-  }
+  write_flags(s, flag_ptrs(sf.ready_writes));  // "ready from rank_" at each destination
+  for (int p : dests) last_sent_[par][p] = q;
   // receives: wait for every source's ready flag, one copy-out launch, then acknowledge (frees the slots)
   std::vector<P2PCopy> in;
   std::vector<int> srcs;
@@ -349,7 +388,6 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       if (op.peer != src || op.bytes == 0) continue;
       FAN_CHECK(src != rank_, "p2p: self-receive");
       if (!any) {
-        wait_flag(s, flags_ + src, q, false);
         any = true;
         srcs.push_back(src);
       }
@@ -358,70 +396,54 @@ void P2PComm::sendrecv(const std::vector<P2POp>& sends, const std::vector<P2POp>
       off += (op.bytes + 15) / 16 * 16;
     }
   }
+  const RoundFlags rf = p2p_round_flags(rank_, world_, q, {}, srcs, last_sent_[par]);
+  wait_flags(s, flag_ptrs(rf.ready_waits), false);
   copy(in, s);
-  for (int src : srcs) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[src] + world_ + rank_, q, 0));
+  write_flags(s, flag_ptrs(rf.ack_writes));
 }
 
-P2PComm::Round P2PComm::begin(hipStream_t s) {
-  FAN_CHECK(!aborted_, "p2p transport aborted");
-  Round r{++seq_};
-  const int par = (int)(r.seq % depth_);
-  for (int p = 0; p < world_; ++p) {
-    if (p == rank_) continue;
-    FAN_CHECK(peer_arena_[p] != nullptr, "p2p: peer not connected");
-    const uint64_t prev = last_sent_[par][p];
-    if (prev) wait_flag(s, flags_ + world_ + p, prev, true);
-  }
-  return r;
-}
-
-void P2PComm::publish(const Round& r, hipStream_t s) {
-  const int par = (int)(r.seq % depth_);
-  release_before_flags(s);
-  for (int p = 0; p < world_; ++p) {
-    if (p == rank_) continue;
-    FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, r.seq, 0));  // "ready from rank_" at p
-    last_sent_[par][p] = r.seq;
-  }
-}
-
-void P2PComm::wait(const Round& r, hipStream_t s) {
+std::vector<int> P2PComm::others() const {
+  std::vector<int> v;
   for (int p = 0; p < world_; ++p)
-    if (p != rank_) wait_flag(s, flags_ + p, r.seq, false);
+    if (p != rank_) v.push_back(p);
+  return v;
 }
 
-void P2PComm::release(const Round& r, hipStream_t s) {
-  for (int p = 0; p < world_; ++p)
-    if (p != rank_) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + world_ + rank_, r.seq, 0));
+std::vector<P2PComm::FlagOp> P2PComm::flag_ptrs(const std::vector<FlagRef>& refs) const {
+  std::vector<FlagOp> out;
+  for (const FlagRef& f : refs) out.push_back({(f.peer == rank_ ? flags_ : peer_flags_[f.peer]) + f.word, f.value});
+  return out;
 }
+
+P2PComm::Round P2PComm::begin(hipStream_t s) { return begin_to(others(), s); }
+void P2PComm::publish(const Round& r, hipStream_t s) { publish_to(r, others(), s); }
+void P2PComm::wait(const Round& r, hipStream_t s) { wait_from(r, others(), s); }
+void P2PComm::release(const Round& r, hipStream_t s) { release_from(r, others(), s); }
 
 P2PComm::Round P2PComm::begin_to(const std::vector<int>& to, hipStream_t s) {
   FAN_CHECK(!aborted_, "p2p transport aborted");
   Round r{++seq_};
-  const int par = (int)(r.seq % depth_);
-  for (int p : to) {
+  for (int p : to)
     FAN_CHECK(p != rank_ && p >= 0 && p < world_ && peer_arena_[p] != nullptr, "p2p: bad or unconnected peer");
-    const uint64_t prev = last_sent_[par][p];
-    if (prev) wait_flag(s, flags_ + world_ + p, prev, true);
-  }
+  // credit flow control: every peer acknowledged the previous message in the slot this round reuses
+  wait_flags(s, flag_ptrs(p2p_round_flags(rank_, world_, r.seq, to, {}, last_sent_[r.seq % depth_]).credit_waits), true);
   return r;
 }
 
 void P2PComm::publish_to(const Round& r, const std::vector<int>& to, hipStream_t s) {
   const int par = (int)(r.seq % depth_);
   release_before_flags(s);
-  for (int p : to) {
-    FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + rank_, r.seq, 0));
-    last_sent_[par][p] = r.seq;
-  }
+  write_flags(s, flag_ptrs(p2p_round_flags(rank_, world_, r.seq, to, {}, last_sent_[par]).ready_writes));
+  for (int p : to) last_sent_[par][p] = r.seq;
 }
 
 void P2PComm::wait_from(const Round& r, const std::vector<int>& from, hipStream_t s) {
-  for (int p : from) wait_flag(s, flags_ + p, r.seq, false);
+  wait_flags(s, flag_ptrs(p2p_round_flags(rank_, world_, r.seq, {}, from, last_sent_[r.seq % depth_]).ready_waits),
+             false);
 }
 
 void P2PComm::release_from(const Round& r, const std::vector<int>& from, hipStream_t s) {
-  for (int p : from) FAN_HIP_CHECK(hipStreamWriteValue64(s, peer_flags_[p] + world_ + rank_, r.seq, 0));
+  write_flags(s, flag_ptrs(p2p_round_flags(rank_, world_, r.seq, {}, from, last_sent_[r.seq % depth_]).ack_writes));
 }
 
 void P2PComm::copy(const std::vector<P2PCopy>& segs, hipStream_t s) {

@@ -44,6 +44,13 @@
 // holds every CU the copy still runs).
 // abort() releases every stream parked on this rank's flags (poison value) so a dead peer cannot hang the GPU;
 // the communicator then refuses further calls.
+// Kernel flags (set_kernel_flags, FAN_P2P_FLAGS=kernel; the A/B's *_kflag arms): the flag writes and waits run as
+// tiny kernels instead of command-processor packets — a one-workgroup kernel stores each ready / ack word with a
+// system-scope release (sc0 sc1), and a one-workgroup kernel spins (relaxed system-scope loads + s_sleep, bounded:
+// past ~8 s it records an error and gives up) until every awaited word reaches its sequence number, then acquires at
+// system scope; the consuming kernel follows it in stream order (the consumer spins in-kernel).
+// The CP-independent path in case command-processor polling of another GPU's uncached word is slow or misbehaves on
+// xGMI; it costs a kernel launch per flag batch. abort()'s poison values release these spins too.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -60,6 +67,11 @@ struct P2PCopy {
 };
 // All segments in one (or few) kernel launches; segments 16-B aligned, sizes multiples of 16 B.
 void launch_multi_copy(const std::vector<P2PCopy>& segs, hipStream_t stream);
+// Kernel flags (P2PComm::set_kernel_flags): store each word's value with a system-scope release / spin until every
+// word reaches its value (bounded; *err = 1 when a spin gave up), then a system-scope acquire. One launch per batch
+// of up to 16 words.
+void launch_flag_write(const std::vector<std::pair<uint64_t*, uint64_t>>& w, hipStream_t stream);
+void launch_flag_wait(const std::vector<std::pair<uint64_t*, uint64_t>>& w, unsigned* err, hipStream_t stream);
 // Segments merged into contiguous runs (source and destination both continue the previous segment); empty ones
 // dropped. The copy-engine path issues one command per run.
 std::vector<P2PCopy> coalesce_copies(const std::vector<P2PCopy>& segs);
@@ -67,6 +79,24 @@ std::vector<P2PCopy> coalesce_copies(const std::vector<P2PCopy>& segs);
 // (cp); in the in-kernel modes only when bytes of the round were moved outside a peer-storing kernel (copy engines,
 // hipMemcpyAsync fallback), since no kernel released those.
 bool p2p_release_event_needed(int mode, bool copy_engine_bytes);
+
+// The flag words one round touches (pure host logic, unit-tested on CPU: tests/test_p2p_host_logic.py). Flag block of
+// every rank: words [0, world) "ready from src", [world, 2 world) "ack from dst". A round with sequence number seq
+// sending to `to` and receiving from `from`:
+//   credit_waits: own word world + p >= the sequence last sent to p in this round's slot (seq % depth), if any
+//   ready_writes: peer p's word rank := seq (after the payload)
+//   ready_waits:  own word q >= seq (before reading q's message)
+//   ack_writes:   peer q's word world + rank := seq (after the consumer: frees the slot for q)
+struct FlagRef {
+  int peer;    // whose flag block (== rank for an own word)
+  int word;
+  uint64_t value;
+};
+struct RoundFlags {
+  std::vector<FlagRef> credit_waits, ready_writes, ready_waits, ack_writes;
+};
+RoundFlags p2p_round_flags(int rank, int world, uint64_t seq, const std::vector<int>& to, const std::vector<int>& from,
+                           const std::vector<uint64_t>& last_sent_in_slot);
 
 class P2PComm : public Comm {
  public:
@@ -125,6 +155,12 @@ class P2PComm : public Comm {
   uint8_t* src_tag(const Round& r, int from, int k) const {
     return slot_ptr(arena_, from, r.seq) + payload_bytes() + 16 * (size_t)k;
   }
+  // flag writes / waits as kernels instead of command-processor packets (see the header comment); switch only
+  // between rounds (the A/B flips it per arm after the previous arm's requests finished)
+  bool kernel_flags() const { return kflags_; }
+  void set_kernel_flags(bool on) { kflags_ = on; }
+  // a kernel-flag wait gave up after its spin bound (0: never); host read, for diagnostics
+  unsigned kernel_flag_error() const;
   // pure copies (see the header comment): CU kernel or copy engines
   void move(const std::vector<P2PCopy>& segs, hipStream_t s);
   bool sdma() const { return sdma_; }
@@ -183,8 +219,15 @@ class P2PComm : public Comm {
   std::vector<std::vector<uint64_t>> last_sent_;  // per slot index (seq % depth): last sequence sent to each peer
   uint64_t seq_ = 0;
   bool aborted_ = false;
+  // flag operations of one round step, batched: one command-processor packet per word, or one kernel for all
+  using FlagOp = std::pair<uint64_t*, uint64_t>;
+  std::vector<FlagOp> flag_ptrs(const std::vector<FlagRef>& refs) const;
+  std::vector<int> others() const;
+  void write_flags(hipStream_t s, const std::vector<FlagOp>& w);
+  void wait_flags(hipStream_t s, const std::vector<FlagOp>& w, bool credit);
+  bool kflags_ = false;
+  unsigned* kflag_err_ = nullptr;  // device word: a kernel-flag wait gave up
   // stall accounting
-  void wait_flag(hipStream_t s, uint64_t* flag, uint64_t value, bool credit);
   bool timing_ = false;
   uint64_t ready_waits_ = 0, credit_waits_ = 0;
   struct TimedWait {

@@ -35,6 +35,66 @@ __global__ void __launch_bounds__(256) multi_copy_kernel(Segs s, int rel) {
 
 }  // namespace
 
+namespace {
+
+constexpr int kMaxFlags = 16;
+constexpr uint32_t kFlagSpinLimit = 1u << 22;  // s_sleep 2 + an uncached (remote) load per trip: several seconds
+struct FlagOps {
+  uint64_t* p[kMaxFlags];
+  uint64_t v[kMaxFlags];
+  int n;
+};
+
+// lane i publishes word i: a system-scope release (this kernel follows the round's payload kernels in stream order;
+// in release modes block / thread they released their peer stores themselves, in mode cp the release event does) and
+// a system-coherent store, so the peer's spin or command processor sees the value once the payload is visible
+__global__ void __launch_bounds__(64) flag_write_kernel(FlagOps f) {
+  const int i = threadIdx.x;
+  if (i < f.n) __hip_atomic_store(f.p[i], f.v[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// lane i spins on word i (relaxed system-scope loads of this rank's uncached flag block, s_sleep between), then the
+// wave acquires at system scope: the next kernel of the stream, which reads the arena slot, starts after this one
+__global__ void __launch_bounds__(64) flag_wait_kernel(FlagOps f, unsigned* err) {
+  const int i = threadIdx.x;
+  if (i < f.n) {
+    for (uint32_t spins = 0; __hip_atomic_load(f.p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < f.v[i];) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kFlagSpinLimit) {  // a dead or aborted peer that nobody poisoned: give up (error), no hang
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+template <class K, class... X>
+void launch_flag_batches(K kernel, const std::vector<std::pair<uint64_t*, uint64_t>>& w, hipStream_t stream,
+                         X... extra) {
+  for (size_t first = 0; first < w.size(); first += kMaxFlags) {
+    FlagOps f{};
+    f.n = 0;
+    for (size_t k = first; k < w.size() && f.n < kMaxFlags; ++k) {
+      f.p[f.n] = w[k].first;
+      f.v[f.n] = w[k].second;
+      ++f.n;
+    }
+    hipLaunchKernelGGL(kernel, 1, 64, 0, stream, f, extra...);
+    FAN_HIP_CHECK(hipGetLastError());
+  }
+}
+
+}  // namespace
+
+void launch_flag_write(const std::vector<std::pair<uint64_t*, uint64_t>>& w, hipStream_t stream) {
+  launch_flag_batches(flag_write_kernel, w, stream);
+}
+
+void launch_flag_wait(const std::vector<std::pair<uint64_t*, uint64_t>>& w, unsigned* err, hipStream_t stream) {
+  launch_flag_batches(flag_wait_kernel, w, stream, err);
+}
+
 void launch_multi_copy(const std::vector<P2PCopy>& segs, hipStream_t stream) {
   for (size_t first = 0; first < segs.size(); first += kMaxSeg) {
     Segs s{};

@@ -62,6 +62,29 @@ def test_bench_two_ranks_p2p_one_gpu(tmp_path):
     assert ex["extras_s"] < 240 and ex["run_s"] < 400, (ex["extras_s"], ex["run_s"])
 
 
+@pytest.mark.parametrize("flags,queues", [("cp", "1"), ("kernel", "1"), ("kernel", "4")])
+def test_bench_two_ranks_hw_queues_and_kernel_flags(tmp_path, flags, queues):
+    """Each rank with ONE hardware queue (GPU_MAX_HW_QUEUES=1: every stream of the process, compute and comm, in one
+    in-order queue, so a flag wait parks the rank's GEMMs behind it) and the flag writes / waits either as command-
+    processor packets or as kernels (--p2p-flags kernel): the fixed-schedule step must neither deadlock nor lose
+    exactness -- the gate passes, the replicas stay bit-identical, no kernel-flag wait reaches its bound. (A peer's
+    ready write is queued before that rank's own waits in every round -- p2p_round_flags -- so one queue per rank
+    cannot close a cycle.)"""
+    os.environ["GPU_MAX_HW_QUEUES"] = queues
+    try:
+        r, recs = _bench(tmp_path, "--schedule", "fixed", "--p2p-flags", flags, "--extra-budget", "0", timeout=300)
+    finally:
+        os.environ.pop("GPU_MAX_HW_QUEUES", None)
+    assert r.returncode == 0 and len(recs) == 1, (r.stdout[-2000:], r.stderr[-4000:])
+    ex = recs[0]["extra"]
+    d = ex["dist"]
+    assert d["replicas_identical"] is True and d["allreduce_exact"] is True, d
+    assert ex["engine_counters"]["direct_rounds"] > 0
+    assert recs[0]["config"].get("p2p_flags", "cp") == flags, recs[0]["config"]
+    if flags == "kernel":
+        assert ex["p2p_stats"]["kernel_flag_error"] == 0, ex["p2p_stats"]
+
+
 def test_bench_gate_rejects_a_corrupted_peer_slot(tmp_path):
     """Every engine flips a byte of the first message it receives, after that message's ready flag was raised
     (fault site p2p_recv): the owner reduces a wrong shard and every rank decodes the same wrong sum (the replicas

@@ -40,10 +40,13 @@ def _run(world, algo, rings, m=40000, max_slice=2048, mode="plain"):
     if mode == "sdma":
         for c in comms:
             c.sdma = True
+    if mode.startswith("kflag"):  # flag writes / waits as kernels instead of command-processor packets
+        for c in comms:
+            c.kernel_flags = True
     rng = np.random.default_rng(100 + world)
     grads = [rng.standard_normal(m).astype(np.float32) for _ in range(world)]
     res, errs = [None] * world, [None] * world
-    verify = mode in ("verify", "fault", "stream_verify", "block_verify")
+    verify = mode in ("verify", "fault", "stream_verify", "block_verify", "kflag_verify")
     fault = "p2p_recv:0:flip" if mode == "fault" else None
     engines = [NativeAllReduce(None, codec="bfp_rne", algo=algo, rings=rings, max_slice_elems=max_slice,
                                comm=comms[r], verify=verify, fault=fault, ring_sub=3 if stream else 1)
@@ -72,7 +75,8 @@ def _run(world, algo, rings, m=40000, max_slice=2048, mode="plain"):
                 s.synchronize()
                 cn = eng.counters()
                 res[r] = (out.cpu().numpy(), None if out_p is None else out_p.cpu().numpy(), L,
-                          cn["direct_rounds"], [list(o) for o in eng.orders], cn["verified_rows"])
+                          cn["direct_rounds"], [list(o) for o in eng.orders], cn["verified_rows"],
+                          comms[r].kernel_flag_error())
         except Exception as e:  # noqa: BLE001
             errs[r] = e
 
@@ -107,8 +111,10 @@ def _check(world, algo, rings, mode="plain"):
         return {"ok": not why, "why": why, "rings": 0}
     out = {"ok": True, "why": [], "rings": len(res[0][4]), "release_mode": _ext.require().p2p_release_mode()}
     for r in range(world):
-        o, o_p, _, direct, orders, verified = res[r]
-        if mode in ("verify", "stream_verify", "block_verify") and verified <= 0:
+        o, o_p, _, direct, orders, verified, kerr = res[r]
+        if kerr:
+            out["why"].append(f"rank {r}: a kernel-flag wait gave up")
+        if mode in ("verify", "stream_verify", "block_verify", "kflag_verify") and verified <= 0:
             out["why"].append(f"rank {r}: verify mode checked no message")
         if not np.array_equal(o[:m], ref[:m]):
             out["why"].append(f"rank {r}: {algo} x{rings} differs from the simulator")
@@ -169,6 +175,15 @@ def test_direct_p2p_in_kernel_release_bit_exact(world, algo, rings, mode):
     "thread" = a system fence per wave): same sums, bit for bit, also with verify mode checking every message."""
     rec = _child(world, algo, rings, mode)
     assert rec["release_mode"] == (1 if mode.startswith("block") else 2), rec
+
+
+@pytest.mark.parametrize("world,algo,rings", [(3, "mesh", 1), (4, "ring", 3), (8, "mesh", 1)])
+@pytest.mark.parametrize("mode", ["kflag", "kflag_verify"])
+def test_direct_p2p_kernel_flags_bit_exact(world, algo, rings, mode):
+    """Kernel flags (P2PComm.kernel_flags): each round's flag writes are one kernel's system-scope release stores and
+    its waits one kernel's bounded spin + acquire -- the CP-independent path, same flag words (p2p_round_flags),
+    same sums bit for bit, no wait reaching its bound."""
+    _child(world, algo, rings, mode)
 
 
 @pytest.mark.parametrize("algo,rings", [("mesh", 1), ("ring", 2)])
