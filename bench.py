@@ -147,6 +147,33 @@ def _free_port() -> int:
     return port
 
 
+def _device_count() -> int:
+    """GPUs visible to this process, counted without initialising the HIP runtime (torch's count on this image)."""
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001
+        return 0
+
+
+def colocated_hw_queues(nranks: int, env) -> str | None:
+    """Hardware queues per rank when several ranks share one GPU (the one-GPU rehearsals of a multi-GPU run).
+
+    Every HIP stream of a process is served by one of that process's hardware queues (up to GPU_MAX_HW_QUEUES, 4 by
+    default, beside the null stream's): ranks that build several engines (the schedule A/B) reach 5 queues each,
+    and with 3 ranks on one GPU that is more user queues than the GPU maps at once. The command processor then
+    time-slices the processes' queues, and a rank whose flag wait (a command-processor wait or a kernel-flag spin)
+    is resident while the peer that must write the flag is switched out loses a time slice per hand-off: 50-840 ms
+    kernels and a 1254 ms/step arm in the 3-rank trace (profiles/r6_hw_queue_oversubscription.txt). Capped at 2 per
+    rank (3 with the null stream's) the co-located ranks stay mapped together. None: one GPU per rank (the driver's
+    multi-GPU run: nothing to share), an explicit GPU_MAX_HW_QUEUES, or no GPU."""
+    if "GPU_MAX_HW_QUEUES" in env:
+        return None
+    n = _device_count()
+    return "2" if 0 < n < nranks else None
+
+
 def self_launch(a, argv) -> int | None:
     """--gpus N > 1 without a torch.distributed environment: run N ranks under torch.distributed.run as a child
     process (this process never touches the GPU) and return its exit code; None when no launch is needed."""
@@ -154,6 +181,11 @@ def self_launch(a, argv) -> int | None:
         return None
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / CUDA-tensor sharing across processes)
+    hwq = colocated_hw_queues(a.gpus, env)
+    if hwq is not None:
+        env["GPU_MAX_HW_QUEUES"] = hwq
+        print(f"[bench] {a.gpus} ranks share {_device_count()} GPU(s): GPU_MAX_HW_QUEUES={hwq} per rank",
+              file=sys.stderr, flush=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
     print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)

@@ -128,3 +128,19 @@ def test_uncompressed_speedup_guard():
     sp, note = bench._uncompressed_speedup(arms, 2.0, ["a", "b"])
     assert sp is None and "stall" in note
     assert bench._uncompressed_speedup({"rccl_f32": {"skipped": "x"}}, 2.0, [None])[0] is None
+
+
+def test_colocated_ranks_cap_hw_queues(monkeypatch):
+    """Ranks sharing a GPU get GPU_MAX_HW_QUEUES=2 from the self-launcher (queue oversubscription across processes
+    time-slices their flag hand-offs); one GPU per rank, or an explicit setting, is left alone."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    monkeypatch.setattr(bench, "_device_count", lambda: 1)
+    assert bench.colocated_hw_queues(3, {}) == "2"
+    assert bench.colocated_hw_queues(3, {"GPU_MAX_HW_QUEUES": "4"}) is None
+    assert bench.colocated_hw_queues(1, {}) is None
+    monkeypatch.setattr(bench, "_device_count", lambda: 8)
+    assert bench.colocated_hw_queues(8, {}) is None and bench.colocated_hw_queues(16, {}) == "2"
+    monkeypatch.setattr(bench, "_device_count", lambda: 0)  # CPU: nothing to cap
+    assert bench.colocated_hw_queues(2, {}) is None
