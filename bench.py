@@ -166,12 +166,19 @@ def colocated_hw_queues(nranks: int, env) -> str | None:
     time-slices the processes' queues, and a rank whose flag wait (a command-processor wait or a kernel-flag spin)
     is resident while the peer that must write the flag is switched out loses a time slice per hand-off: 50-840 ms
     kernels and a 1254 ms/step arm in the 3-rank trace (profiles/r6_hw_queue_oversubscription.txt). Capped at 2 per
-    rank (3 with the null stream's) the co-located ranks stay mapped together. None: one GPU per rank (the driver's
-    multi-GPU run: nothing to share), an explicit GPU_MAX_HW_QUEUES, or no GPU."""
-    if "GPU_MAX_HW_QUEUES" in env:
+    rank (3 with the null stream's) the co-located ranks stay mapped together (the same A/B: that arm 4.3-4.6 ms/step
+    at 2 or 1 queues per rank). A smaller inherited GPU_MAX_HW_QUEUES is kept (the GPU boxes export 4, HIP's default).
+    None: one GPU per rank (the driver's multi-GPU run: nothing to share), FAN_KEEP_HW_QUEUES=1, or no GPU."""
+    if env.get("FAN_KEEP_HW_QUEUES") == "1":
         return None
     n = _device_count()
-    return "2" if 0 < n < nranks else None
+    if not 0 < n < nranks:
+        return None
+    try:
+        cur = int(env.get("GPU_MAX_HW_QUEUES") or 4)
+    except ValueError:
+        cur = 4
+    return "2" if cur > 2 else None
 
 
 def self_launch(a, argv) -> int | None:

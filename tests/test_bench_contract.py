@@ -132,13 +132,15 @@ def test_uncompressed_speedup_guard():
 
 def test_colocated_ranks_cap_hw_queues(monkeypatch):
     """Ranks sharing a GPU get GPU_MAX_HW_QUEUES=2 from the self-launcher (queue oversubscription across processes
-    time-slices their flag hand-offs); one GPU per rank, or an explicit setting, is left alone."""
+    time-slices their flag hand-offs); one GPU per rank, a smaller setting or FAN_KEEP_HW_QUEUES=1 is left alone."""
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
 
     monkeypatch.setattr(bench, "_device_count", lambda: 1)
     assert bench.colocated_hw_queues(3, {}) == "2"
-    assert bench.colocated_hw_queues(3, {"GPU_MAX_HW_QUEUES": "4"}) is None
+    assert bench.colocated_hw_queues(3, {"GPU_MAX_HW_QUEUES": "4"}) == "2"  # the boxes export HIP's default
+    assert bench.colocated_hw_queues(3, {"GPU_MAX_HW_QUEUES": "1"}) is None  # a smaller setting is kept
+    assert bench.colocated_hw_queues(3, {"FAN_KEEP_HW_QUEUES": "1"}) is None
     assert bench.colocated_hw_queues(1, {}) is None
     monkeypatch.setattr(bench, "_device_count", lambda: 8)
     assert bench.colocated_hw_queues(8, {}) is None and bench.colocated_hw_queues(16, {}) == "2"

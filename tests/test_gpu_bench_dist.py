@@ -70,11 +70,16 @@ def test_bench_two_ranks_hw_queues_and_kernel_flags(tmp_path, flags, queues):
     exactness -- the gate passes, the replicas stay bit-identical, no kernel-flag wait reaches its bound. (A peer's
     ready write is queued before that rank's own waits in every round -- p2p_round_flags -- so one queue per rank
     cannot close a cycle.)"""
-    os.environ["GPU_MAX_HW_QUEUES"] = queues
+    saved = {k: os.environ.get(k) for k in ("GPU_MAX_HW_QUEUES", "FAN_KEEP_HW_QUEUES")}
+    os.environ.update(GPU_MAX_HW_QUEUES=queues, FAN_KEEP_HW_QUEUES="1")  # exactly this many (no co-location cap)
     try:
         r, recs = _bench(tmp_path, "--schedule", "fixed", "--p2p-flags", flags, "--extra-budget", "0", timeout=300)
     finally:
-        os.environ.pop("GPU_MAX_HW_QUEUES", None)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     assert r.returncode == 0 and len(recs) == 1, (r.stdout[-2000:], r.stderr[-4000:])
     ex = recs[0]["extra"]
     d = ex["dist"]
