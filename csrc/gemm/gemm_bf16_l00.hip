@@ -1,6 +1,6 @@
 // bf16 GEMM instantiations for A MN-contiguous, B MN-contiguous: the 128-wide tiles (the 256x256 tiles, by far the
 // largest instantiation set, compile in parallel in gemm_bf16_l00_t256.hip).
-#include "gemm/gemm_bf16_kernel.h"
+#include "gemm/gemm_bf16_launch.h"
 
 namespace fan {
 namespace gemm_detail {

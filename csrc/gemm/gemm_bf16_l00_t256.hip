@@ -1,6 +1,6 @@
 // bf16 GEMM instantiations for A MN-contiguous, B MN-contiguous: 256x256 tiles (one-role, pipelined 8-wave and 4-wave
 // main loops).
-#include "gemm/gemm_bf16_kernel.h"
+#include "gemm/gemm_bf16_launch.h"
 
 namespace fan {
 namespace gemm_detail {

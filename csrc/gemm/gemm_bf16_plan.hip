@@ -1,6 +1,6 @@
 // bf16 GEMM planner + dispatch. The kernel template lives in gemm_bf16_kernel.h; each operand layout is
 // instantiated in its own translation unit (gemm_bf16_l*.hip) so the ~200 kernels build in parallel.
-#include "gemm/gemm_bf16_kernel.h"
+#include "gemm/gemm_bf16_launch.h"
 
 #include <cstdio>
 #include <map>
