@@ -56,7 +56,9 @@ def test_bench_two_ranks_p2p_one_gpu(tmp_path):
     assert c4["bfp_mesh_p2p"]["algo_bw_GBps"] > 0 and c4["bfp_ring_p2p"]["algo_bw_GBps"] > 0, c4
     assert c4["raw_f32_mesh_p2p"]["algo_bw_GBps"] > 0 and "skipped" in c4["rccl_f32"], c4
     un = ex["uncompressed"]
-    assert un["p2p_raw_f32_mesh"]["ms_per_step"] > 0 and un["speedup_vs_best_uncompressed"] > 0, un
+    assert un["p2p_raw_f32_mesh"]["ms_per_step"] > 0, un
+    # both ranks on one GPU: the speedup would time the shared GPU, not the codec -> withheld, with the reason
+    assert un["speedup_vs_best_uncompressed"] is None and "share a GPU" in un["speedup_note"], un
     c5 = ex["config5"]  # BERT-base backward + per-layer all-reduce over the headline's transport
     assert c5["t_compute_ms"] > 0 and c5["t_comm_ms"] > 0 and c5["t_overlap_ms"] > 0 and c5["transport"] == "p2p", c5
     assert ex["extras_s"] < 240 and ex["run_s"] < 400, (ex["extras_s"], ex["run_s"])
