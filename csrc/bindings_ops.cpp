@@ -338,9 +338,6 @@ void register_gemm(pybind11::module_& m) {
   m.def("gemm_set_ovl", [](int on) { gemm_ovl_flag().store(on); },
         "256x256 bf16 plans on the persistent loop with overlapped tile transitions (pl4_run OVL)");
   m.def("gemm_ovl", []() { return gemm_ovl_flag().load(); });
-  m.def("gemm_set_kstagger", [](int code) { gemm_kstagger_flag().store(code); },
-        "K-start stagger of the 4-wave GEMM loops: step | starts << 8 | selector << 16 (0 off)");
-  m.def("gemm_kstagger", []() { return gemm_kstagger_flag().load(); });
   m.def("gemm_set_reduce4", [](int on) { gemm_reduce4_flag().store(on); },
         "split-K wire / fused-update reduce: 4 values per lane (1) or one 16-value group per lane (0)");
   m.def("gemm_reduce4", []() { return gemm_reduce4_flag().load(); });

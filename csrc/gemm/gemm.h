@@ -92,9 +92,6 @@ std::atomic<int>& gemm_ovl_flag();
 // split-K wire / fused-update reduce: lane-contiguous form, 4 values per lane (1, default) or one 16-value group per
 // lane (0) (FAN_GEMM_REDUCE4, gemm_set_reduce4); bit-identical either way
 std::atomic<int>& gemm_reduce4_flag();
-// K-start stagger of the 4-wave pipelined loops (FAN_GEMM_KSTAGGER, gemm_set_kstagger; code of
-// gemm_detail::kstagger_of: step | distinct starts << 8 | selector << 16; 0 off)
-std::atomic<int>& gemm_kstagger_flag();
 // diagnostic builds (-DFAN_GEMM_STAMPS): device buffer for the one-role loop's s_memtime stamps (nullptr: off)
 void gemm_set_stamp_buffer(void* p);
 void* gemm_stamp_buffer();

@@ -282,24 +282,7 @@ struct WireOut {
   // > 0: the 4-wave persistent loops run their waves at this s_setprio level (gemm_prio_flag): a kernel of another
   // stream sharing the CU (the all-reduce's copy / reduce / SGD kernels) then issues only in the GEMM wave's stalls
   int prio;
-  // != 0: K-start stagger of the 4-wave loops (gemm_kstagger_flag, see kstagger_of): bits 0-7 the step in K-tiles,
-  // bits 8-15 the number of distinct starts, bits 16-17 what selects the start (0 row panel, 1 column panel, 2 both)
-  int kstg;
 };
-
-// K-tile rotation of the output tile at (m0 / BM, n0 / BN) = (tm, tn): the tile's K loop runs K-tiles kst, kst + 1,
-// ..., nk - 1, 0, ..., kst - 1. In one K-tile every workgroup of a plain loop reads the same K-slice of its rows — with
-// 8-KiB rows (K = 4096 bf16) addresses equal modulo 8 KiB — while workgroups with different starts spread their
-// reads over the L2's channels (the library's hand-written NT kernel staggers its K start per workgroup: Tensile's
-// StaggerU). The same products in another k order: a staggered GEMM is deterministic, not bit-identical to an
-// unstaggered one.
-__device__ __forceinline__ int kstagger_of(int code, int tm, int tn, int nk) {
-  if (code == 0) return 0;
-  const int step = code & 255, mod = (code >> 8) & 255, key = (code >> 16) & 3;
-  const int sel = key == 0 ? tm : key == 1 ? tn : tm + tn;
-  const int s = (mod > 0 ? sel % mod : 0) * step;
-  return nk > 0 ? s % nk : 0;
-}
 
 // flat index -> (shard, position); f < 2^31, shard >= 256: the float estimate is off by at most one
 __device__ __forceinline__ int wire_shard_of(uint32_t f, const WireOut& wo) {
@@ -1158,7 +1141,6 @@ struct ChainArgs {
   int panels;  // row panels of the pass (M / 256)
   unsigned* ctr;
   int prio;
-  int kstg;   // K-start stagger code (WireOut::kstg)
   int flags;  // diagnostic builds of the schedule (kChainNoAcquire: unsafe; kChainRowsFastest)
 };
 constexpr int kChainNoAcquire = 1;    // skip the consumer's acquire (diagnostic A/B only: visibility not guaranteed)
@@ -1326,7 +1308,6 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   // CHAIN: the next ticket, whether its dependency is met, whether this run continues with it (same stage, OVL)
   int ch_next = 0, ch_rdy = 0;
   bool ch_cont = false;
-  int ks_cur = 0;  // K-start stagger (kstagger_of) of the tile whose operand offsets are loaded
   auto tile_body = [&](int v, bool first, int vn) __attribute__((always_inline)) {
   const int ksplit = CHAIN ? 0 : xcd_remap(v, tiles * split_k) / tiles;
   int m0, n0;
@@ -1334,13 +1315,6 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   const int k_per = K / split_k;
   const int kbeg = ksplit * k_per;
   const int nk = k_per / BK;
-  // K-start stagger: K-tile kt of the loop is the split's K-tile keff(kt) (the LDS stage still follows kt)
-  ks_cur = kstagger_of(wo.kstg, m0 / BM, n0 / BN, nk);
-  const int kst = ks_cur;
-  auto keff = [&](int kt) __attribute__((always_inline)) {
-    const int e = kt + kst;
-    return e >= nk ? e - nk : e;
-  };
 
   // fused bias gradient: as gemm_pl_kernel (waves wm == 0; spread over the tile rows without split-K)
   const int im = SPLIT ? 0 : m0 / BM;
@@ -1370,14 +1344,11 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 
   // glds piece p (0..G-1) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
   // the accumulator array in scratch memory)
-  // (ks_cur: the K-start stagger of the tile whose offsets off[] holds — the next tile's for the OVL prefetch)
   auto piece = [&](int kt, auto pc) __attribute__((always_inline)) {
     constexpr int p = decltype(pc)::value;
     const uint32_t st = lds0 + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE + wave * 1024;
-    int ke = kt + ks_cur;
-    if (ke >= nk) ke -= nk;
-    if constexpr (p < GA) glds16_si<p * OpTile<BM, NT>::IB, ASC1>(a_k0 + ke * a_step, off[p], st);
-    else glds16_si<A_BYTES + (p - GA) * OpTile<BN, NT>::IB>(b_k0 + ke * b_step, off[p], st);
+    if constexpr (p < GA) glds16_si<p * OpTile<BM, NT>::IB, ASC1>(a_k0 + kt * a_step, off[p], st);
+    else glds16_si<A_BYTES + (p - GA) * OpTile<BN, NT>::IB>(b_k0 + kt * b_step, off[p], st);
   };
   // next k-step's fragment r (0..R-1: A rows 0..7, then B columns 0..NJ-1) into set `set`
   auto read_next = [&](const char* st, int ks, int set, int r) __attribute__((always_inline)) {
@@ -1484,7 +1455,7 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
   };
   auto ktile = [&](int kt, auto more_c, auto more2_c) __attribute__((always_inline)) {
     const char* st = smem + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE;
-    const bool csk = do_colsum && keff(kt) >= cs0 && keff(kt) < cs1;
+    const bool csk = do_colsum && kt >= cs0 && kt < cs1;
     FAN_STAMP(0);
     if constexpr (STAGES == 2) {
       constexpr bool kLast = OVL && !decltype(more_c)::value && !decltype(more2_c)::value;
@@ -1494,7 +1465,6 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
       auto next_offsets = [&](int vnn) __attribute__((always_inline)) {
         int m1, n1;
         tile_origin(vnn, m1, n1);
-        ks_cur = kstagger_of(wo.kstg, m1 / BM, n1 / BN, nk);
 #pragma unroll
         for (int p = 0; p < GA; ++p) off[p] = piece_off<AK, BM, NT>(lda, m1, wave, lane, p);
 #pragma unroll

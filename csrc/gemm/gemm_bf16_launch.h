@@ -199,7 +199,6 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
   };
   wo.off = (uint32_t)a.wire_off;
   wo.prio = gemm_prio_flag().load(std::memory_order_relaxed);
-  wo.kstg = gemm_kstagger_flag().load(std::memory_order_relaxed);
 
   if (sk > 1) {
     // f32 partial slabs ws[k][M][N] (+ bias-gradient partials ws[sk*M*N + p*N]), then an ordered reduce that

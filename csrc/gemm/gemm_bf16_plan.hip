@@ -51,15 +51,6 @@ std::atomic<int>& gemm_ovl_flag() {
   return flag;
 }
 
-std::atomic<int>& gemm_kstagger_flag() {
-  static std::atomic<int> flag{[] {
-    // K-start stagger code of the 4-wave loops (kstagger_of in gemm_bf16_kernel.h; 0: off)
-    const char* e = getenv("FAN_GEMM_KSTAGGER");
-    return e ? (int)strtol(e, nullptr, 0) : 0;
-  }()};
-  return flag;
-}
-
 std::atomic<int>& gemm_reduce4_flag() {
   static std::atomic<int> flag{[] {
     const char* e = getenv("FAN_GEMM_REDUCE4");

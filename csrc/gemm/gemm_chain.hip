@@ -21,7 +21,6 @@ struct ChainCfg {
     const ChainStageArgs& S = ca.st[s];
     WireOut wo{};
     wo.prio = ca.prio;
-    wo.kstg = ca.kstg;
     ChainRun cr;
     cr.ctr = ca.ctr;
     cr.group = (int)(blockIdx.x & 7);
@@ -176,7 +175,6 @@ void launch_gemm_chain(const GemmArgs* a, int n, int kind, unsigned* counters, h
   ca.ppg = ca.panels / kNumXCD;
   ca.ctr = counters;
   ca.prio = gemm_prio_flag().load(std::memory_order_relaxed);
-  ca.kstg = gemm_kstagger_flag().load(std::memory_order_relaxed);  // the per-GEMM launches' k order
   // diagnostic schedule variants (A/B probes only): FAN_CHAIN_ACQ=0 skips the acquire, FAN_CHAIN_ORDER=1 rows-fastest
   static const int diag_flags = (env_int("FAN_CHAIN_ACQ", 1) == 0 ? kChainNoAcquire : 0) |
                                 (env_int("FAN_CHAIN_ORDER", 0) == 1 ? kChainRowsFastest : 0);

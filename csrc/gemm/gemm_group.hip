@@ -21,7 +21,6 @@ PlProblem<TC> problem_of(const GemmArgs& a, const WireOut& wo) {
 WireOut wire_of(const GemmArgs& a) {
   WireOut wo{};
   wo.prio = gemm_prio_flag().load(std::memory_order_relaxed);
-  wo.kstg = gemm_kstagger_flag().load(std::memory_order_relaxed);
   if (a.wire) {
     wo.p = a.wire;
     wo.shard = a.wire_shard;
