@@ -34,7 +34,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
           int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period, int64_t wire_off,
           const c10::optional<at::Tensor>& upd_master, const c10::optional<at::Tensor>& upd_lp,
           const c10::optional<at::Tensor>& upd_mom, double upd_lr, double upd_grad_scale, double upd_weight_decay,
-          double upd_momentum, bool upd_nesterov) {
+          double upd_momentum, bool upd_nesterov, bool defer_colsum) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "A and B dtype mismatch");
   GemmArgs g{};
@@ -110,6 +110,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
       }
       g.upd = SgdParams{(float)upd_lr, (float)upd_grad_scale, (float)upd_weight_decay, (float)upd_momentum,
                         upd_nesterov ? 1 : 0};
+      g.defer_colsum = defer_colsum && g.colsum != nullptr;
     }
   }
   if (A.scalar_type() == at::kBFloat16) {
@@ -318,8 +319,13 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("upd_master") = pybind11::none(), pybind11::arg("upd_lp") = pybind11::none(),
         pybind11::arg("upd_mom") = pybind11::none(), pybind11::arg("upd_lr") = 0.0,
         pybind11::arg("upd_grad_scale") = 1.0, pybind11::arg("upd_weight_decay") = 0.0,
-        pybind11::arg("upd_momentum") = 0.0, pybind11::arg("upd_nesterov") = false);
+        pybind11::arg("upd_momentum") = 0.0, pybind11::arg("upd_nesterov") = false,
+        pybind11::arg("defer_colsum") = false);
   m.def("gemm_supported", &gemm_supported);
+  m.def("gemm_flush_colsum", []() { return gemm_flush_colsum(fan_stream()); },
+        "launch the bias-gradient reduces queued on the current stream by defer_colsum GEMMs; returns how many");
+  m.def("gemm_pending_colsum", []() { return gemm_pending_colsum(fan_stream()); },
+        "bias-gradient reduces queued on the current stream");
   m.def("gemm_wgrad_group", &gemm_wgrad_group,
         "up to 8 bwd-weight GEMMs (+ fused bias gradients, f32 or BFP wire epilogue) in one dispatch",
         pybind11::arg("Xs"), pybind11::arg("dYs"), pybind11::arg("Cs"), pybind11::arg("colsums"),

@@ -65,6 +65,10 @@ struct GemmArgs {
   bf16_t* upd_lp = nullptr;
   float* upd_mom = nullptr;
   SgdParams upd{};
+  // fused update with colsum on an unsplit plan: the bias-gradient reduce is queued on the stream instead of launched
+  // (the next split-K wire reduce of the stream runs it in its first blocks, gemm_flush_colsum what is left); the
+  // partials in `workspace` must stay untouched until then (the caller gives such a GEMM a workspace of its own)
+  bool defer_colsum = false;
 };
 
 struct GemmPlan {
@@ -77,6 +81,10 @@ GemmPlan gemm_bf16_plan(int M, int N, int K, int split_k, int tile_bm = 0, int t
 // Returns false if the shape is not supported by the MFMA path (caller must then error out).
 bool gemm_bf16_supported(const GemmArgs& a);
 void launch_gemm_bf16(const GemmArgs& a, hipStream_t stream);
+// launches the bias-gradient reduces queued on the stream (GemmArgs::defer_colsum) as grouped launches; returns how
+// many ran. gemm_pending_colsum: how many are queued.
+int gemm_flush_colsum(hipStream_t stream);
+int gemm_pending_colsum(hipStream_t stream);
 
 // 256x256 tiles: main-loop selection (0 one-role, 2 pipelined by layout / K, 3 pipelined 4-wave, 5 8-wave).
 std::atomic<int>& gemm_main_loop_flag();

@@ -1705,6 +1705,20 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Bias-gradient reduces of several GEMMs (colsum_reduce_group_kernel, splitk_reduce_wire4_kernel QCS).
+struct ColsumGroup {
+  const float* part[kMaxGroup];
+  float* colsum[kMaxGroup];
+  WireOut wo[kMaxGroup];
+  int parts[kMaxGroup];
+  int N[kMaxGroup];
+  int first[kMaxGroup + 1];
+  int n;
+};
+template <bool WIRE, bool UPD>
+__device__ __forceinline__ void colsum_reduce_block(const float* __restrict__ part, int parts,
+                                                    float* __restrict__ colsum, int N, const WireOut& wo, int blk);
+
 // The fused update of 4 values of a group (flat index f, f % 4 == 0; shared exponent E): local_update16's operations
 // on a quarter of the group.
 __device__ __forceinline__ void local_update4(float v[4], uint32_t E, uint32_t f, const WireOut& wo) {
@@ -1728,13 +1742,28 @@ __device__ __forceinline__ void local_update4(float v[4], uint32_t E, uint32_t f
 // value is summed in split order, encoded, rounded and updated as there: bit-identical. The bias partials (colsum)
 // are reduced per 16-column group after the loop, as there. (M * N / 4 is a multiple of 4 — N % 16 == 0 — and the
 // grid's thread count too, so a quad's lanes are always all in or all out of range.)
-template <bool UPD, int SK = 0>
+// QCS: the launch also runs bias-gradient reduces that earlier fused-update GEMMs of the stream queued (qcs, in its
+// first qcs.first[qcs.n] blocks: one launch less per queued reduce, GemmArgs::defer_colsum).
+template <bool UPD, int SK = 0, bool QCS = false>
 __global__ void __launch_bounds__(256)
     splitk_reduce_wire4_kernel(const float* __restrict__ ws, int split_k, float* __restrict__ C, int64_t ldc, int M,
-                               int N, float* __restrict__ colsum, WireOut wo) {
+                               int N, float* __restrict__ colsum, WireOut wo, ColsumGroup qcs) {
+  int bid = (int)blockIdx.x, nb = (int)gridDim.x;
+  if constexpr (QCS) {
+    const int nq = qcs.first[qcs.n];
+    if (bid < nq) {
+      int i = 0;
+      while (i + 1 < qcs.n && bid >= qcs.first[i + 1]) ++i;
+      colsum_reduce_block<true, true>(qcs.part[i], qcs.parts[i], qcs.colsum[i], qcs.N[i], qcs.wo[i],
+                                      bid - qcs.first[i]);
+      return;
+    }
+    bid -= nq;
+    nb -= nq;
+  }
   if constexpr (SK > 0) split_k = SK;
   const int64_t slab = (int64_t)M * N, quads = slab / 4;
-  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = bid * (int64_t)blockDim.x + threadIdx.x, step = (int64_t)nb * blockDim.x;
   for (int64_t q = t0; q < quads; q += step) {
     const int64_t e = q * 4;
     const int row = (int)(e / N), col = (int)(e % N);
@@ -1796,7 +1825,7 @@ __global__ void __launch_bounds__(256)
 // Ordered reduce of bias-gradient partial slabs part[p * N + n], p < parts, into colsum[n]; WIRE: also encodes the
 // bias segment of the [W | b] bucket (flat wo.bias_off + n). One block per 64 columns: 16 lanes x float4 columns by
 // 16 part classes (p % 16), each summed in p order, then the classes summed in class order (deterministic).
-template <bool WIRE, bool UPD = false>
+template <bool WIRE, bool UPD>
 __device__ __forceinline__ void colsum_reduce_block(const float* __restrict__ part, int parts,
                                                     float* __restrict__ colsum, int N, const WireOut& wo, int blk) {
   __shared__ float4 red[16][16];
@@ -1839,23 +1868,15 @@ __global__ void __launch_bounds__(256)
   colsum_reduce_block<WIRE, UPD>(part, parts, colsum, N, wo, (int)blockIdx.x);
 }
 
-// The grouped GEMM's bias gradients: problem i's blocks [first[i], first[i + 1]) reduce its partial slabs.
-struct ColsumGroup {
-  const float* part[kMaxGroup];
-  float* colsum[kMaxGroup];
-  WireOut wo[kMaxGroup];
-  int parts[kMaxGroup];
-  int N[kMaxGroup];
-  int first[kMaxGroup + 1];
-  int n;
-};
-
-template <bool WIRE>
+// Bias gradients of several GEMMs in one launch — the grouped GEMM's problems, or the bias-gradient reduces that
+// fused-update bwd-weight GEMMs queued (GemmArgs::defer_colsum): entry i's blocks [first[i], first[i + 1]) reduce its
+// partial slabs, the same ordered reduce as colsum_reduce_kernel (bit-identical).
+template <bool WIRE, bool UPD = false>
 __global__ void __launch_bounds__(256) colsum_reduce_group_kernel(ColsumGroup g) {
   const int b = (int)blockIdx.x;
   int i = 0;
   while (i + 1 < g.n && b >= g.first[i + 1]) ++i;
-  colsum_reduce_block<WIRE>(g.part[i], g.parts[i], g.colsum[i], g.N[i], g.wo[i], b - g.first[i]);
+  colsum_reduce_block<WIRE, UPD>(g.part[i], g.parts[i], g.colsum[i], g.N[i], g.wo[i], b - g.first[i]);
 }
 
 }  // namespace gemm_detail

@@ -177,6 +177,20 @@ void launch_colsum_reduce(const float* part, int parts, const GemmArgs& a, const
   hipLaunchKernelGGL((colsum_reduce_kernel<WIRE, UPD>), cdiv_i(a.N, 64), 256, 0, s, part, parts, a.colsum, a.N, wo);
 }
 
+// Bias-gradient reduces queued by fused-update GEMMs (GemmArgs::defer_colsum), per stream, in issue order: the next
+// split-K wire reduce of the stream runs them in its first blocks, gemm_flush_colsum launches what is left
+// (gemm_bf16_plan.hip holds the queue).
+struct PendingColsum {
+  const float* part;
+  int parts;
+  float* colsum;
+  int N;
+  WireOut wo;
+};
+void push_pending_colsum(hipStream_t s, const PendingColsum& p);
+// up to kMaxGroup of the stream's queued reduces (oldest first) as a group (n == 0: none); removes them from the queue
+ColsumGroup take_pending_colsum(hipStream_t s);
+
 // The split counts the planner and tuner use as compile-time constants of the slab reduce (others: runtime count).
 template <typename F>
 void with_split_count(int sk, F&& f) {
@@ -209,11 +223,17 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
     if constexpr (is_wire_epi(EPI)) {
       const size_t items = (size_t)a.M * a.N / 16 + (a.colsum ? a.N / 16 : 0);
       const bool lane4 = gemm_reduce4_flag().load(std::memory_order_relaxed) != 0;
+      // the stream's queued bias-gradient reduces ride along in the first blocks (one launch less each)
+      const ColsumGroup q = lane4 ? take_pending_colsum(s) : ColsumGroup{};
       with_split_count(sk, [&](auto skc) {
-        if (lane4)
+        if (lane4 && q.n > 0)
+          hipLaunchKernelGGL((splitk_reduce_wire4_kernel<EPI == kEpiWireUpd, decltype(skc)::value, true>),
+                             stream_grid((size_t)a.M * a.N / 4) + q.first[q.n], 256, 0, s, (const float*)a.workspace,
+                             sk, (float*)a.C, a.ldc, a.M, a.N, a.colsum, wo, q);
+        else if (lane4)
           hipLaunchKernelGGL((splitk_reduce_wire4_kernel<EPI == kEpiWireUpd, decltype(skc)::value>),
                              stream_grid((size_t)a.M * a.N / 4), 256, 0, s, (const float*)a.workspace, sk, (float*)a.C,
-                             a.ldc, a.M, a.N, a.colsum, wo);
+                             a.ldc, a.M, a.N, a.colsum, wo, q);
         else
           hipLaunchKernelGGL((splitk_reduce_wire_kernel<EPI == kEpiWireUpd, decltype(skc)::value>),
                              stream_grid(items), 256, 0, s, (const float*)a.workspace, sk, (float*)a.C, a.ldc, a.M,
@@ -229,10 +249,18 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
         launch_colsum_reduce<false>((const float*)a.workspace + (size_t)sk * a.M * a.N, parts, a, wo, s);
     }
   } else {
-    // bias-gradient partials at ws[p * N] (pipelined loop): ordered reduce (+ the bias segment's wire encode)
+    // bias-gradient partials at ws[p * N] (pipelined loop): ordered reduce (+ the bias segment's wire encode); a
+    // fused-update GEMM may queue it instead (defer_colsum: its partials stay in a workspace of their own)
     const int parts = launch_main<BM, BN, WM, WN, AK, BKC, EPI, TC, ACCUM, false>(a, sk, wo, s);
-    if (parts > 0)
+    if (parts > 0) {
+      if constexpr (EPI == kEpiWireUpd) {
+        if (a.defer_colsum) {
+          push_pending_colsum(s, PendingColsum{(const float*)a.workspace, parts, a.colsum, a.N, wo});
+          return;
+        }
+      }
       launch_colsum_reduce<is_wire_epi(EPI), EPI == kEpiWireUpd>((const float*)a.workspace, parts, a, wo, s);
+    }
   }
 }
 

@@ -2,6 +2,7 @@
 // instantiated in its own translation unit (gemm_bf16_l*.hip) so the ~200 kernels build in parallel.
 #include "gemm/gemm_bf16_launch.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -30,6 +31,60 @@ extern template void launch_tile<false, true>(const GemmArgs&, int, int, int, in
 extern template void launch_tile<true, false>(const GemmArgs&, int, int, int, int, hipStream_t);
 extern template void launch_tile<true, true>(const GemmArgs&, int, int, int, int, hipStream_t);
 }  // namespace gemm_detail
+
+namespace gemm_detail {
+namespace {
+std::mutex g_pend_mu;
+std::map<hipStream_t, std::vector<PendingColsum>>& pend_map() {
+  static std::map<hipStream_t, std::vector<PendingColsum>> m;
+  return m;
+}
+}  // namespace
+
+void push_pending_colsum(hipStream_t s, const PendingColsum& p) {
+  std::lock_guard<std::mutex> g(g_pend_mu);
+  pend_map()[s].push_back(p);
+}
+
+ColsumGroup take_pending_colsum(hipStream_t s) {
+  ColsumGroup g{};
+  std::lock_guard<std::mutex> lk(g_pend_mu);
+  auto it = pend_map().find(s);
+  if (it == pend_map().end() || it->second.empty()) return g;
+  auto& v = it->second;
+  const int n = (int)std::min<size_t>(v.size(), kMaxGroup);
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    g.part[i] = v[i].part;
+    g.parts[i] = v[i].parts;
+    g.colsum[i] = v[i].colsum;
+    g.N[i] = v[i].N;
+    g.wo[i] = v[i].wo;
+    g.first[i] = blocks;
+    blocks += cdiv_i(v[i].N, 64);
+  }
+  g.first[n] = blocks;
+  g.n = n;
+  v.erase(v.begin(), v.begin() + n);
+  return g;
+}
+}  // namespace gemm_detail
+
+int gemm_flush_colsum(hipStream_t s) {
+  int ran = 0;
+  for (;;) {
+    const gemm_detail::ColsumGroup g = gemm_detail::take_pending_colsum(s);
+    if (g.n == 0) return ran;
+    hipLaunchKernelGGL((gemm_detail::colsum_reduce_group_kernel<true, true>), g.first[g.n], 256, 0, s, g);
+    ran += g.n;
+  }
+}
+
+int gemm_pending_colsum(hipStream_t s) {
+  std::lock_guard<std::mutex> g(gemm_detail::g_pend_mu);
+  auto it = gemm_detail::pend_map().find(s);
+  return it == gemm_detail::pend_map().end() ? 0 : (int)it->second.size();
+}
 
 std::atomic<int>& gemm_prio_flag() {
   static std::atomic<int> flag{[] {

@@ -200,16 +200,17 @@ class MLP:
         if self._relu_at(self.L - 1):  # ReLU on the classifier output (reference fuse_type 2/3)
             self.dz[self.L].mul_(self.logits > 0)
 
-    def backward_weight(self, i: int, wire=None, update=None):
+    def backward_weight(self, i: int, wire=None, update=None, defer_colsum=False):
         """dW (+ db) of layer i into the gradient bucket. ``wire`` (GPU bf16 only): the all-reduce engine's
         prepack target — dW is BFP-encoded straight into the wire shards by the GEMM epilogue. ``update`` (with
         ``wire``, single-rank engine): a :class:`~fpga_ai_nic_amd.ops.gemm.LocalUpdate` — the epilogue applies the
         decoded gradient to this layer's weights in place instead of storing the wire (the layer's bwd-data GEMM,
-        which reads the weights, must already be enqueued)."""
+        which reads the weights, must already be enqueued). ``defer_colsum`` (with ``update``): the bias part may be
+        queued on the stream (ops/gemm.py :func:`~fpga_ai_nic_amd.ops.gemm.flush_colsum` completes it)."""
         l = self.layers[i]
         if wire is not None:
             G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw, bias_grad=l.gb if self.bias else None, wire=wire,
-                                update=update)
+                                update=update, defer_colsum=defer_colsum)
         elif not self.bias:
             G.linear_bwd_weight(self.act[i], self.dz[i + 1], l.gw)
         elif l.gw.is_cuda and self.dtype == torch.bfloat16:  # bias gradient fused into the bwd-weight GEMM

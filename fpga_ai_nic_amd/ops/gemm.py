@@ -53,7 +53,8 @@ def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
 
 
 def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux=None, accumulate=False,
-         split_k: int | None = None, tile: tuple | None = None, colsum=None, wire=None, update=None):
+         split_k: int | None = None, tile: tuple | None = None, colsum=None, wire=None, update=None,
+         defer_colsum: bool = False):
     """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
     ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only).
     ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N]).
@@ -63,11 +64,16 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     bwd-weight only.
     ``update`` (with ``wire``, single-rank engine): a :class:`LocalUpdate` — the encoded groups are not stored but
     decoded in registers and applied by SGD to the bucket planes in place (the fused local update, see
-    csrc/gemm/gemm_bf16_kernel.h WireOut::um)."""
+    csrc/gemm/gemm_bf16_kernel.h WireOut::um).
+    ``defer_colsum`` (with ``update`` and ``colsum``): the bias-gradient reduce of an unsplit plan is queued on the
+    stream instead of launched — the next split-K wire reduce of the stream runs it in its first blocks, and
+    :func:`flush_colsum` launches what is left in one grouped launch (the partials get a workspace of their own);
+    ``colsum`` and the bias update are only complete after that."""
     if wire is not None:
         if not C.is_cuda or A.dtype != torch.bfloat16 or not a_t or b_t:
             raise ValueError("wire epilogue: bf16 GPU bwd-weight layout only")
-        _bf16(_ext.require(), A, a_t, B, b_t, C, EPI_WIRE, None, None, False, split_k, tile, colsum, wire, update)
+        _bf16(_ext.require(), A, a_t, B, b_t, C, EPI_WIRE, None, None, False, split_k, tile, colsum, wire, update,
+              defer_colsum=defer_colsum)
         return C
     if update is not None:
         raise ValueError("update needs the wire epilogue")
@@ -187,7 +193,36 @@ class LocalUpdate:
                     upd_nesterov=self.nesterov)
 
 
-def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, wire, update=None):
+_defer_ws: dict = {}
+
+
+def _colsum_ws(Cx, device, colsum, numel):
+    """Workspace of a deferred bias-gradient reduce (one per stream and colsum tensor): its partials must outlive
+    the later GEMMs of the stream until the queued reduce runs."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream, colsum.data_ptr())
+    t = _defer_ws.get(key)
+    if t is None or t.numel() < numel:
+        if t is not None:
+            Cx.gemm_flush_colsum()  # a queued reduce may still read the buffer being replaced
+        t = torch.empty(numel, dtype=torch.float32, device=device)
+        _defer_ws[key] = t
+    return t
+
+
+def flush_colsum() -> int:
+    """Launch the bias-gradient reduces queued on the current stream by ``defer_colsum`` GEMMs (one grouped launch
+    per 8); returns how many ran."""
+    if not torch.cuda.is_available():
+        return 0
+    return int(_ext.require().gemm_flush_colsum())
+
+
+def pending_colsum() -> int:
+    return int(_ext.require().gemm_pending_colsum()) if torch.cuda.is_available() else 0
+
+
+def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, wire, update=None,
+          defer_colsum=False):
     """bf16 MFMA GEMM launch with its plan: explicit (tile / split_k given), tuned on the device on a shape's first
     call (ops/gemm_tune.py), or the static planner's. With a fused ``update`` the tuner's trial launches store the
     wire instead (an update is not re-runnable); the chosen plan then runs once more with the update."""
@@ -207,10 +242,12 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
     def run(plan, waves=0, upd=None):
         bm, bn, sk = plan  # launch exactly this tile (re-planning with an explicit split_k differs)
         need = _bf16_ws_floats(M, N, sk, bm, colsum)
-        ws = _workspace(C.device, need) if need else None
+        defer = bool(defer_colsum and upd is not None and colsum is not None and sk == 1)
+        ws = (_colsum_ws(Cx, C.device, colsum, need) if defer else _workspace(C.device, need)) if need else None
         if wire is not None:
             Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, bm, bn, colsum, waves, buf, int(shard),
-                    int(own), int(codec), period, woff, **(upd.kwargs() if upd is not None else {}))
+                    int(own), int(codec), period, woff, **(upd.kwargs() if upd is not None else {}),
+                    defer_colsum=defer)
         else:
             Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, bm, bn, colsum, waves)
 
@@ -304,10 +341,12 @@ def linear_bwd_data(dz, w, out, relu_input=None):
     return gemm(dz, False, w, True, out, EPI_NONE)
 
 
-def linear_bwd_weight(x, dz, out, accumulate=False, bias_grad=None, wire=None, update=None):
+def linear_bwd_weight(x, dz, out, accumulate=False, bias_grad=None, wire=None, update=None, defer_colsum=False):
     """dW = Xᵀ · dZ (f32 out); with ``bias_grad`` also db = colsum(dZ), fused into the same kernel; with
     ``wire`` dW is written BFP-encoded into the all-reduce wire buffer instead (see :func:`gemm`); with ``update``
-    (single-rank engine) the encoded dW updates the weights in place instead."""
+    (single-rank engine) the encoded dW updates the weights in place instead (``defer_colsum``: the bias part
+    queued, see :func:`gemm`)."""
     if wire is not None:
-        return gemm(x, True, dz, False, out, EPI_WIRE, colsum=bias_grad, wire=wire, update=update)
+        return gemm(x, True, dz, False, out, EPI_WIRE, colsum=bias_grad, wire=wire, update=update,
+                    defer_colsum=defer_colsum)
     return gemm(x, True, dz, False, out, EPI_NONE, accumulate=accumulate, colsum=bias_grad)

@@ -117,6 +117,10 @@ class DataParallelTrainer:
         self.fused_update = (fu and self.prepack and bool(getattr(engine, "inline", False))
                              and getattr(engine, "codec", "") == "bfp_rne")
         self.fused_updates = 0
+        # fused update: the layers' bias-gradient reduces of unsplit bwd-weight plans are queued and run by the next
+        # split-K wire reduce of the backward, or all in one grouped launch after it (FAN_DEFER_COLSUM=0: one launch
+        # each, right after its GEMM; bit-identical either way)
+        self.defer_colsum = os.environ.get("FAN_DEFER_COLSUM", "1") != "0"
         # layer-chain launches (ops/gemm.py linear_chain, FAN_GEMM_CHAIN): the forward at every world size; the
         # bwd-data chain only with the fused world-1 update — with a multi-rank engine each layer's all-reduce is
         # issued right after its own bwd-weight GEMM and overlaps that layer's bwd-data GEMM, which a chain of the
@@ -233,7 +237,7 @@ class DataParallelTrainer:
                                             weight_decay=self.wd, momentum=self.momentum, nesterov=self.nesterov)
                         # (the bwd-weight GEMMs of layers >= 1 on a second stream, beside the next GEMM, measured 1.5-2 %
                         # slower: profiles/r3_fused_update_ab.txt)
-                        m.backward_weight(i, wire=tgt, update=upd)
+                        m.backward_weight(i, wire=tgt, update=upd, defer_colsum=self.defer_colsum)
                         self.fused_updates += 1
                     else:
                         m.backward_weight(i, wire=tgt)
@@ -262,6 +266,8 @@ class DataParallelTrainer:
                     self.times["bwd_first"] += t1 - t0
                     self.times["bwd"] += t1 - t0
                     t0 = t1
+            if self.fused_updates and self.defer_colsum and self.cuda:
+                G.flush_colsum()  # the bias updates still queued (every layer's lands before the next forward)
         finally:
             # the grid GEMM form must not outlive this backward (an exception in between would leave every later
             # GEMM of the process on one workgroup per tile while records report the persistent form)
