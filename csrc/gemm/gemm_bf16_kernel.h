@@ -550,12 +550,17 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
 #pragma unroll
     for (int i = 0; i < kPf && i < MI; ++i) aux_load(i);
   }
-  // fused local update (unsplit wire epilogue): the master values of 16-row block i + 1's groups are loaded while
+  // fused local update (unsplit wire epilogue): the master values of 16-row block i + kUpf's groups are loaded while
   // block i is encoded and updated, instead of one dependent load round trip per block (all CUs run this epilogue
   // at the same moment, so each round trip is a loaded-HBM latency)
   constexpr bool kPfUpd = EPI == kEpiWireUpd && !SPLIT;
   constexpr int UG16 = WTN / 16, URPG = 64 / UG16, UPASS = URPG >= 16 ? 1 : 16 / URPG;
-  float um_pf[kPfUpd ? 2 : 1][kPfUpd ? UPASS : 1][16];
+#ifndef FAN_GEMM_UPD_PF
+// row blocks of master weights loaded ahead of the one being updated (2: profiles/r6_upd_prefetch_depth_ab.txt)
+#define FAN_GEMM_UPD_PF 2
+#endif
+  constexpr int kUpf = FAN_GEMM_UPD_PF, US = kPfUpd ? kUpf + 1 : 1;
+  float um_pf[US][kPfUpd ? UPASS : 1][16];
   auto upd_load = [&](int i, int slot) __attribute__((always_inline)) {
     if constexpr (kPfUpd) {
 #pragma unroll
@@ -574,14 +579,17 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
       }
     }
   };
-  if constexpr (kPfUpd) upd_load(0, 0);
+  if constexpr (kPfUpd) {
+#pragma unroll
+    for (int d = 0; d < kUpf && d < MI; ++d) upd_load(d, d % US);
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     if constexpr (kPfAux) {
       if (i + kPf < MI) aux_load(i + kPf);
     }
     if constexpr (kPfUpd) {
-      if (i + 1 < MI) upd_load(i + 1, (i + 1) & 1);
+      if (i + kUpf < MI) upd_load(i + kUpf, (i + kUpf) % US);
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -605,7 +613,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[MI][NJ], char* sme
           }
           if (!mn_edge || (row0 + i * 16 + rr < M && col0 + cc < N))
             wire_epi16<EPI == kEpiWireUpd, kPfUpd>(v, reinterpret_cast<float*>(C), ldc, wo, row0 + i * 16 + rr,
-                                                   col0 + cc, um_pf[kPfUpd ? (i & 1) : 0][kPfUpd ? pass : 0]);
+                                                   col0 + cc, um_pf[kPfUpd ? i % US : 0][kPfUpd ? pass : 0]);
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
