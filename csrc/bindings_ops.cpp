@@ -34,7 +34,7 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
           int64_t wire_shard, int64_t wire_own, int64_t wire_codec, int64_t wire_period, int64_t wire_off,
           const c10::optional<at::Tensor>& upd_master, const c10::optional<at::Tensor>& upd_lp,
           const c10::optional<at::Tensor>& upd_mom, double upd_lr, double upd_grad_scale, double upd_weight_decay,
-          double upd_momentum, bool upd_nesterov, bool defer_colsum) {
+          double upd_momentum, bool upd_nesterov, bool defer_colsum, bool defer_reduce) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "A and B dtype mismatch");
   GemmArgs g{};
@@ -59,6 +59,9 @@ void gemm(const at::Tensor& A, bool a_t, const at::Tensor& B, bool b_t, at::Tens
   g.tile_bm = (int)tile_bm;
   g.tile_bn = (int)tile_bn;
   g.tile_waves = (int)tile_waves;
+  g.defer_reduce = defer_reduce;
+  TORCH_CHECK(!defer_reduce || (epilogue == kEpiBias && C.scalar_type() == at::kFloat && !colsum && !accumulate),
+              "defer_reduce: the f32 bias epilogue only (the softmax folds the slabs)");
   if (colsum) {
     TORCH_CHECK(colsum->is_cuda() && colsum->is_contiguous() && colsum->scalar_type() == at::kFloat &&
                     colsum->numel() >= g.N,
@@ -296,6 +299,23 @@ void softmax_xent(const at::Tensor& logits, const at::Tensor& labels, at::Tensor
                       fan_stream());
 }
 
+void softmax_xent_slabs(const at::Tensor& ws, int64_t sk, const at::Tensor& bias, at::Tensor& logits,
+                        const at::Tensor& labels, at::Tensor& dlogits, at::Tensor& loss_rows, double grad_scale) {
+  TORCH_CHECK(ws.is_cuda() && bias.is_cuda() && logits.is_cuda() && labels.is_cuda() && dlogits.is_cuda() &&
+                  loss_rows.is_cuda(), "GPU tensors");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.is_contiguous() && logits.scalar_type() == at::kFloat &&
+                  bias.scalar_type() == at::kBFloat16 && bias.is_contiguous(), "f32 slabs / logits, bf16 bias");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && loss_rows.scalar_type() == at::kFloat,
+              "int32 labels, f32 loss rows");
+  const int M = (int)logits.size(0), Cc = (int)logits.size(1);
+  TORCH_CHECK(dlogits.size(0) == M && dlogits.size(1) == Cc && bias.numel() >= Cc, "shapes");
+  TORCH_CHECK(sk >= 1 && ws.numel() >= sk * (int64_t)M * Cc, "workspace holds sk slabs of M x C");
+  launch_softmax_xent_slabs(ws.data_ptr<float>(), (int)sk, reinterpret_cast<const bf16_t*>(bias.data_ptr()),
+                            logits.data_ptr<float>(), ld_of(logits), labels.data_ptr<int32_t>(), dcode(dlogits),
+                            dlogits.data_ptr(), ld_of(dlogits), loss_rows.data_ptr<float>(), M, Cc,
+                            (float)grad_scale, fan_stream());
+}
+
 void col_sum(const at::Tensor& x, at::Tensor& out, double scale, bool accumulate, at::Tensor& workspace) {
   TORCH_CHECK(x.is_cuda() && out.is_cuda() && workspace.is_cuda(), "GPU tensors");
   const int M = (int)x.size(0), N = (int)x.size(1);
@@ -320,7 +340,7 @@ void register_gemm(pybind11::module_& m) {
         pybind11::arg("upd_mom") = pybind11::none(), pybind11::arg("upd_lr") = 0.0,
         pybind11::arg("upd_grad_scale") = 1.0, pybind11::arg("upd_weight_decay") = 0.0,
         pybind11::arg("upd_momentum") = 0.0, pybind11::arg("upd_nesterov") = false,
-        pybind11::arg("defer_colsum") = false);
+        pybind11::arg("defer_colsum") = false, pybind11::arg("defer_reduce") = false);
   m.def("gemm_supported", &gemm_supported);
   m.def("gemm_flush_colsum", []() { return gemm_flush_colsum(fan_stream()); },
         "launch the bias-gradient reduces queued on the current stream by defer_colsum GEMMs; returns how many");
@@ -372,6 +392,8 @@ void register_gemm(pybind11::module_& m) {
 
 void register_nn(pybind11::module_& m) {
   m.def("softmax_xent", &softmax_xent, "fused softmax + cross-entropy fwd/bwd");
+  m.def("softmax_xent_slabs", &softmax_xent_slabs,
+        "softmax + cross-entropy over the classifier GEMM's unreduced split-K slabs (+ bias; logits written)");
   m.def("col_sum", &col_sum, "bias-gradient column sum");
   m.def("col_sum_workspace_floats", [](int64_t M, int64_t N) { return (int64_t)col_sum_workspace_floats((int)M, (int)N); });
 }

@@ -69,6 +69,9 @@ struct GemmArgs {
   // (the next split-K wire reduce of the stream runs it in its first blocks, gemm_flush_colsum what is left); the
   // partials in `workspace` must stay untouched until then (the caller gives such a GEMM a workspace of its own)
   bool defer_colsum = false;
+  // split-K plans of the f32 bias epilogue: the slab reduce is NOT launched — the caller consumes the slabs itself
+  // (the classifier's softmax folds them: launch_softmax_xent_slabs)
+  bool defer_reduce = false;
 };
 
 struct GemmPlan {

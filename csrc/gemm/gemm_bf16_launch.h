@@ -240,6 +240,7 @@ void launch_typed(const GemmArgs& a, int sk, hipStream_t s) {
                              a.N, a.colsum, wo);
       });
     } else {
+      if (a.defer_reduce) return;  // the caller folds the slabs (GemmArgs::defer_reduce)
       with_split_count(sk, [&](auto skc) {
         hipLaunchKernelGGL((splitk_reduce_kernel<EPI, TC, ACCUM, decltype(skc)::value>),
                            stream_grid((size_t)a.M * a.N / 4), 256, 0, s, (const float*)a.workspace, sk, (TC*)a.C,

@@ -123,6 +123,81 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// The classifier GEMM's split-K partial slabs folded in (ws[k][M][C], k < sk; the GEMM ran with defer_reduce): each
+// logit is the slabs' sum in split order plus the bias — the arithmetic of the GEMM's own slab reduce
+// (splitk_reduce_kernel with the bias epilogue), so the logits (also written out) are bit-identical and the reduce
+// launch disappears. Then as softmax_xent_reg_kernel.
+template <typename TOUT, int NCH>
+__global__ void __launch_bounds__(256)
+    softmax_xent_slab_kernel(const float* __restrict__ ws, int sk, const bf16_t* __restrict__ bias,
+                             float* __restrict__ logits, int64_t ld, const int32_t* __restrict__ labels,
+                             TOUT* __restrict__ dlogits, int64_t ldd, float* __restrict__ loss_rows, int M, int C,
+                             float grad_scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int64_t slab = (int64_t)M * C;
+  const float* x = ws + (int64_t)row * C;
+  const int lab = labels[row];
+  float v[NCH][8];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < C) {
+      ld8<float>(x + c, v[k]);
+      for (int q = 1; q < sk; ++q) {
+        float t[8];
+        ld8<float>(x + q * slab + c, t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += t[j];
+      }
+      float b[8];
+      ld8<bf16_t>(bias + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] += b[j];
+      st8<float>(logits + (int64_t)row * ld + c, v[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = -INFINITY;
+    }
+  }
+  // the label's logit from the registers: lane (lab / 8) % 64 of chunk lab / 512 holds it
+  float xl = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if ((k * 64 + lane) * 8 + j == lab) xl = v[k][j];
+  xl = wave_sum(xl);
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, v[k][j]);
+  const float gm = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[k][j] = __expf(v[k][j] - gm);
+      s += v[k][j];
+    }
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  if (lane == 0) loss_rows[row] = gm + __logf(s) - xl;
+  TOUT* d = dlogits + (int64_t)row * ldd;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c >= C) continue;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (v[k][j] * inv - (c + j == lab ? 1.f : 0.f)) * grad_scale;
+    st8<TOUT>(d + c, o);
+  }
+}
+
 // One wave per row; 4 waves per block. VEC: 8 values per lane access (C, ld, ldd % 8 == 0); otherwise one value
 // per lane access (any class count, e.g. a 10-class head).
 template <typename TIN, typename TOUT, bool VEC>
@@ -266,6 +341,27 @@ void launch_softmax_xent(int in_dtype, const void* logits, int64_t ld, const int
     FAN_SMX(bf16_t, float)
   }
 #undef FAN_SMX
+  FAN_HIP_CHECK(hipGetLastError());
+}
+
+bool softmax_xent_slabs_supported(int C) { return C % 8 == 0 && C <= 2048; }
+
+void launch_softmax_xent_slabs(const float* ws, int sk, const bf16_t* bias, float* logits, int64_t ld,
+                               const int32_t* labels, int out_dtype, void* dlogits, int64_t ldd, float* loss_rows,
+                               int M, int C, float grad_scale, hipStream_t s) {
+  FAN_CHECK(softmax_xent_slabs_supported(C) && ld % 8 == 0 && ldd % 8 == 0 && sk >= 1,
+            "softmax_xent over split-K slabs: C % 8 == 0, C <= 2048, ld / ldd % 8 == 0");
+  const int grid = (M + 3) / 4;
+  const int nch = (C + 511) / 512;
+#define FAN_SMS(TO)                                                                                            \
+  {                                                                                                            \
+    auto k = nch == 1 ? softmax_xent_slab_kernel<TO, 1> : nch == 2 ? softmax_xent_slab_kernel<TO, 2>           \
+           : nch == 3 ? softmax_xent_slab_kernel<TO, 3> : softmax_xent_slab_kernel<TO, 4>;                     \
+    hipLaunchKernelGGL(k, grid, 256, 0, s, ws, sk, bias, logits, ld, labels, (TO*)dlogits, ldd, loss_rows, M, C, \
+                       grad_scale);                                                                            \
+  }
+  if (out_dtype == kBF16) FAN_SMS(bf16_t) else FAN_SMS(float)
+#undef FAN_SMS
   FAN_HIP_CHECK(hipGetLastError());
 }
 

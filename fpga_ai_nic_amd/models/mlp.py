@@ -169,10 +169,15 @@ class MLP:
         self._act_mb = mb
 
     # ------------------------------------------------------------------ compute
-    def forward_layer(self, i: int):
+    def forward_layer(self, i: int, fold_logits: bool = False):
+        """Layer i's forward GEMM. ``fold_logits`` (training, last layer): a split-K classifier GEMM leaves its slabs
+        for :meth:`loss_backward`'s softmax to fold (one launch less; the logits are written there)."""
         l = self.layers[i]
         out = self.act[i + 1] if i + 1 < self.L else self.logits
-        G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i))
+        self._slabs = None
+        if fold_logits and i + 1 == self.L and out.is_cuda and self.dtype == torch.bfloat16 and not self._relu_at(i):
+            self._slabs = {}
+        G.linear_fwd(self.act[i], l.w, self._bias_of(l), out, relu=self._relu_at(i), defer_reduce=self._slabs)
 
     def forward_chain(self) -> bool:
         """Every layer's forward GEMM as ONE layer-chain launch (GPU bf16; ops/gemm.py linear_chain); False when the
@@ -196,7 +201,12 @@ class MLP:
                               [self.dz[i] for i in idx], auxes=[self.act[i] for i in idx], key=("bwd", id(self)))
 
     def loss_backward(self, labels, grad_scale: float):
-        NN.softmax_xent(self.logits, labels, self.dz[self.L], self.loss_rows, grad_scale)
+        slabs, self._slabs = getattr(self, "_slabs", None), None
+        if slabs:  # the classifier GEMM's split-K slabs, folded here (forward_layer fold_logits)
+            NN.softmax_xent_slabs(slabs, self._bias_of(self.layers[-1]), self.logits, labels, self.dz[self.L],
+                                  self.loss_rows, grad_scale)
+        else:
+            NN.softmax_xent(self.logits, labels, self.dz[self.L], self.loss_rows, grad_scale)
         if self._relu_at(self.L - 1):  # ReLU on the classifier output (reference fuse_type 2/3)
             self.dz[self.L].mul_(self.logits > 0)
 

@@ -54,7 +54,7 @@ def choose_split_k(M: int, N: int, K: int, target_wg: int = 256) -> int:
 
 def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux=None, accumulate=False,
          split_k: int | None = None, tile: tuple | None = None, colsum=None, wire=None, update=None,
-         defer_colsum: bool = False):
+         defer_colsum: bool = False, defer_reduce: dict | None = None):
     """C = op(A)·op(B) with a fused epilogue. a_t: A given as [K][M]; b_t: B given as [N][K].
     ``tile=(BM, BN)`` / ``split_k`` override the kernel planner (bf16 only).
     ``colsum`` (f32 [N]): also write sum_k B(k, n) — the fused bias gradient of bwd-weight (bf16, B [K][N]).
@@ -68,7 +68,10 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
     ``defer_colsum`` (with ``update`` and ``colsum``): the bias-gradient reduce of an unsplit plan is queued on the
     stream instead of launched — the next split-K wire reduce of the stream runs it in its first blocks, and
     :func:`flush_colsum` launches what is left in one grouped launch (the partials get a workspace of their own);
-    ``colsum`` and the bias update are only complete after that."""
+    ``colsum`` and the bias update are only complete after that.
+    ``defer_reduce`` (a dict; f32 ``EPI_BIAS`` output, bf16 operands): when the plan splits K, the slab reduce is not
+    launched and C is NOT written — the dict receives ``ws`` (the slabs, [sk][M][N] f32) and ``sk`` for a consumer
+    that folds them (:func:`fpga_ai_nic_amd.ops.nn.softmax_xent_slabs`); it stays empty when C was written."""
     if wire is not None:
         if not C.is_cuda or A.dtype != torch.bfloat16 or not a_t or b_t:
             raise ValueError("wire epilogue: bf16 GPU bwd-weight layout only")
@@ -96,7 +99,8 @@ def gemm(A, a_t: bool, B, b_t: bool, C, epilogue: int = EPI_NONE, bias=None, aux
                       split_k, tile, colsum, None)
                 C.copy_(Ct)
                 return C
-            _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, None)
+            _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, None,
+                  defer_reduce=defer_reduce)
             return C
         M = A.shape[1] if a_t else A.shape[0]
         K = A.shape[0] if a_t else A.shape[1]
@@ -209,6 +213,17 @@ def _colsum_ws(Cx, device, colsum, numel):
     return t
 
 
+def _slab_ws(device, numel):
+    """Workspace of a GEMM whose split-K slabs a later kernel folds (defer_reduce): one per stream, not shared with
+    the GEMMs that run before that consumer."""
+    key = ("slabs", device, torch.cuda.current_stream(device).cuda_stream)
+    t = _defer_ws.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(numel, dtype=torch.float32, device=device)
+        _defer_ws[key] = t
+    return t
+
+
 def flush_colsum() -> int:
     """Launch the bias-gradient reduces queued on the current stream by ``defer_colsum`` GEMMs (one grouped launch
     per 8); returns how many ran."""
@@ -222,7 +237,7 @@ def pending_colsum() -> int:
 
 
 def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile, colsum, wire, update=None,
-          defer_colsum=False):
+          defer_colsum=False, defer_reduce=None):
     """bf16 MFMA GEMM launch with its plan: explicit (tile / split_k given), tuned on the device on a shape's first
     call (ops/gemm_tune.py), or the static planner's. With a fused ``update`` the tuner's trial launches store the
     wire instead (an update is not re-runnable); the chosen plan then runs once more with the update."""
@@ -239,24 +254,33 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
         period = int(wire[4]) if len(wire) > 4 else 0
         woff = int(wire[5]) if len(wire) > 5 else 0
 
-    def run(plan, waves=0, upd=None):
+    def run(plan, waves=0, upd=None, final=False):
         bm, bn, sk = plan  # launch exactly this tile (re-planning with an explicit split_k differs)
         need = _bf16_ws_floats(M, N, sk, bm, colsum)
         defer = bool(defer_colsum and upd is not None and colsum is not None and sk == 1)
-        ws = (_colsum_ws(Cx, C.device, colsum, need) if defer else _workspace(C.device, need)) if need else None
+        # (not in the tuner's trial launches: their timing must include the reduce)
+        dred = bool(final and defer_reduce is not None and sk > 1 and epilogue == EPI_BIAS and colsum is None
+                    and C.dtype == torch.float32 and not accumulate)
+        if dred:
+            ws = _slab_ws(C.device, need)
+        else:
+            ws = (_colsum_ws(Cx, C.device, colsum, need) if defer else _workspace(C.device, need)) if need else None
         if wire is not None:
             Cx.gemm(A, a_t, B, b_t, C, EPI_WIRE, None, None, False, sk, ws, bm, bn, colsum, waves, buf, int(shard),
                     int(own), int(codec), period, woff, **(upd.kwargs() if upd is not None else {}),
                     defer_colsum=defer)
         else:
-            Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, bm, bn, colsum, waves)
+            Cx.gemm(A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, sk, ws, bm, bn, colsum, waves,
+                    defer_reduce=dred)
+            if dred:
+                defer_reduce.update(ws=ws, sk=sk)
 
     from . import gemm_tune
 
     T = gemm_tune.tuner()
     if (tile is not None or split_k is not None or not T.enabled or accumulate
             or torch.cuda.is_current_stream_capturing() or _shares_storage(C, A, B, aux, bias)):
-        run(tuple(static[:3]), tw, update)
+        run(tuple(static[:3]), tw, update, final=True)
         return
     # a fused-update call shares the key of the wire call (the tuner's trial launches store the wire either way): the
     # fused and the unfused schedule of one shape then run the SAME plan, so their dW rounding — and the weights they
@@ -270,7 +294,7 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
         if update is not None:
             run(plan, 0, update)
     else:
-        run(plan, 0, update)
+        run(plan, 0, update, final=True)
 
 
 # ---------------------------------------------------------------------------------------------------------------
@@ -329,9 +353,10 @@ def linear_chain(kind: int, a0, ws, outs, biases=None, auxes=None, epis=None, ke
                                           dry_run))
 
 
-def linear_fwd(x, w, b, out, relu: bool):
-    """Y = X · W + b (ReLU)."""
-    return gemm(x, False, w, False, out, EPI_BIAS_RELU if relu else EPI_BIAS, bias=b)
+def linear_fwd(x, w, b, out, relu: bool, defer_reduce: dict | None = None):
+    """Y = X · W + b (ReLU); ``defer_reduce`` (no ReLU): see :func:`gemm`."""
+    return gemm(x, False, w, False, out, EPI_BIAS_RELU if relu else EPI_BIAS, bias=b,
+                defer_reduce=None if relu else defer_reduce)
 
 
 def linear_bwd_data(dz, w, out, relu_input=None):

@@ -22,6 +22,15 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, dlogits: torch.Tens
     dlogits.copy_((p * grad_scale).to(dlogits.dtype))
 
 
+def softmax_xent_slabs(slabs: dict, bias: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor,
+                       dlogits: torch.Tensor, loss_rows: torch.Tensor, grad_scale: float):
+    """:func:`softmax_xent` over the classifier GEMM's unreduced split-K slabs (``slabs`` from ``ops.gemm.gemm``'s
+    ``defer_reduce``): logits = the slabs' sum in split order + bias, as the GEMM's own reduce computes them (also
+    written to ``logits``), then the fused softmax + cross-entropy — one launch instead of two."""
+    _ext.require().softmax_xent_slabs(slabs["ws"], int(slabs["sk"]), bias, logits, labels, dlogits, loss_rows,
+                                      float(grad_scale))
+
+
 def col_sum(x: torch.Tensor, out: torch.Tensor, scale: float = 1.0, accumulate: bool = False):
     """out[n] (+)= scale * sum_m x[m][n] (bias gradient)."""
     if x.is_cuda:

@@ -121,6 +121,9 @@ class DataParallelTrainer:
         # split-K wire reduce of the backward, or all in one grouped launch after it (FAN_DEFER_COLSUM=0: one launch
         # each, right after its GEMM; bit-identical either way)
         self.defer_colsum = os.environ.get("FAN_DEFER_COLSUM", "1") != "0"
+        # a split-K classifier GEMM leaves its slabs to the softmax-xent kernel, which folds them (FAN_FOLD_LOGITS=0:
+        # the GEMM's own slab reduce launch; bit-identical either way)
+        self.fold_logits = os.environ.get("FAN_FOLD_LOGITS", "1") != "0"
         # layer-chain launches (ops/gemm.py linear_chain, FAN_GEMM_CHAIN): the forward at every world size; the
         # bwd-data chain only with the fused world-1 update — with a multi-rank engine each layer's all-reduce is
         # issued right after its own bwd-weight GEMM and overlaps that layer's bwd-data GEMM, which a chain of the
@@ -174,7 +177,7 @@ class DataParallelTrainer:
             if not chained:
                 for i in range(m.L):
                     self._wait_layer(i)  # layer i's weights updated (reference: per-layer wait, sw:757-787)
-                    m.forward_layer(i)
+                    m.forward_layer(i, fold_logits=self.fold_logits and self.cuda)
             self.last_handle = None
         if self.profile:
             self._sync()
