@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(256)
 // logit is the slabs' sum in split order plus the bias — the arithmetic of the GEMM's own slab reduce
 // (splitk_reduce_kernel with the bias epilogue), so the logits (also written out) are bit-identical and the reduce
 // launch disappears. Then as softmax_xent_reg_kernel.
-template <typename TOUT, int NCH>
+template <typename TOUT, int NCH, int SK>
 __global__ void __launch_bounds__(256)
     softmax_xent_slab_kernel(const float* __restrict__ ws, int sk, const bf16_t* __restrict__ bias,
                              float* __restrict__ logits, int64_t ld, const int32_t* __restrict__ labels,
@@ -144,12 +144,16 @@ __global__ void __launch_bounds__(256)
   for (int k = 0; k < NCH; ++k) {
     const int c = (k * 64 + lane) * 8;
     if (c < C) {
+      // (SK > 0: the split count at compile time, so every slab's load is in flight before the first add)
+      float t[SK > 1 ? SK - 1 : 1][8];
       ld8<float>(x + c, v[k]);
-      for (int q = 1; q < sk; ++q) {
-        float t[8];
-        ld8<float>(x + q * slab + c, t);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[k][j] += t[j];
+      for (int q = 1; q < (SK > 0 ? SK : sk); ++q) ld8<float>(x + q * slab + c, t[SK > 0 ? q - 1 : 0]);
+#pragma unroll
+      for (int q = 1; q < (SK > 0 ? SK : sk); ++q) {
+        if constexpr (SK == 0) ld8<float>(x + q * slab + c, t[0]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += t[SK > 0 ? q - 1 : 0][j];
       }
       float b[8];
       ld8<bf16_t>(bias + c, b);
@@ -353,15 +357,24 @@ void launch_softmax_xent_slabs(const float* ws, int sk, const bf16_t* bias, floa
             "softmax_xent over split-K slabs: C % 8 == 0, C <= 2048, ld / ldd % 8 == 0");
   const int grid = (M + 3) / 4;
   const int nch = (C + 511) / 512;
-#define FAN_SMS(TO)                                                                                            \
+#define FAN_SMS_K(TO, SKC)                                                                                     \
   {                                                                                                            \
-    auto k = nch == 1 ? softmax_xent_slab_kernel<TO, 1> : nch == 2 ? softmax_xent_slab_kernel<TO, 2>           \
-           : nch == 3 ? softmax_xent_slab_kernel<TO, 3> : softmax_xent_slab_kernel<TO, 4>;                     \
+    auto k = nch == 1 ? softmax_xent_slab_kernel<TO, 1, SKC> : nch == 2 ? softmax_xent_slab_kernel<TO, 2, SKC> \
+           : nch == 3 ? softmax_xent_slab_kernel<TO, 3, SKC> : softmax_xent_slab_kernel<TO, 4, SKC>;           \
     hipLaunchKernelGGL(k, grid, 256, 0, s, ws, sk, bias, logits, ld, labels, (TO*)dlogits, ldd, loss_rows, M, C, \
                        grad_scale);                                                                            \
   }
-  if (out_dtype == kBF16) FAN_SMS(bf16_t) else FAN_SMS(float)
+#define FAN_SMS(TO)                \
+  if (sk == 2) FAN_SMS_K(TO, 2)    \
+  else if (sk == 4) FAN_SMS_K(TO, 4) \
+  else FAN_SMS_K(TO, 0)
+  if (out_dtype == kBF16) {
+    FAN_SMS(bf16_t)
+  } else {
+    FAN_SMS(float)
+  }
 #undef FAN_SMS
+#undef FAN_SMS_K
   FAN_HIP_CHECK(hipGetLastError());
 }
 
