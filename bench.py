@@ -689,10 +689,10 @@ def main(argv=None):
         # The reference-batch cell runs after the headline, with its own settle phase (both cells are measured alike);
         # a short step, so a longer window (a host hiccup is then a smaller share of it).
         ref_steps = max(a.steps, REF_STEPS) if cuda else a.steps
-        e2, _, _, _, _ = run(main_setup, a.ref_mb, 4321, a.warmup, ref_steps, "ref")
+        e2, _, _, _, g2 = run(main_setup, a.ref_mb, 4321, a.warmup, ref_steps, "ref", graph_ok=True)
         ref = {"mb_per_gpu": a.ref_mb, "global_batch": a.ref_mb * world, "steps": ref_steps,
                "samples_per_s": round(a.ref_mb * world * ref_steps / e2, 2),
-               "ms_per_step": round(e2 / ref_steps * 1e3, 4)}
+               "ms_per_step": round(e2 / ref_steps * 1e3, 4), "hip_graph": g2}
     tr = run(main_setup, mb, 1234, 1, a.steps, "traced", trace=True)[3] if can_trace else None
 
     def record(dist_rec, extras_s, aborted=None):

@@ -279,7 +279,7 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
 
     T = gemm_tune.tuner()
     if (tile is not None or split_k is not None or not T.enabled or accumulate
-            or torch.cuda.is_current_stream_capturing() or _shares_storage(C, A, B, aux, bias)):
+            or _shares_storage(C, A, B, aux, bias)):
         run(tuple(static[:3]), tw, update, final=True)
         return
     # a fused-update call shares the key of the wire call (the tuner's trial launches store the wire either way): the
@@ -287,6 +287,11 @@ def _bf16(Cx, A, a_t, B, b_t, C, epilogue, bias, aux, accumulate, split_k, tile,
     # train — stay bit-identical (a split-K or tile change alters the summation order)
     k = T.key(M, N, K, a_t, b_t, epilogue, colsum is not None, 0 if wire is None else 1, C.device)
     plan = T.lookup(k)
+    if torch.cuda.is_current_stream_capturing():
+        # a HIP-graph capture records the plan this shape was tuned to in the eager steps before it (no trial
+        # launches while capturing); an untuned shape takes the static plan
+        run(plan if plan is not None else tuple(static[:3]), 0, update, final=True)
+        return
     if plan is None and not T.worth_tuning(M, N, static, C.device):
         plan = T.keep_static(k, static)
     if plan is None:
