@@ -269,9 +269,11 @@ class DataParallelTrainer:
                     self.times["bwd_first"] += t1 - t0
                     self.times["bwd"] += t1 - t0
                     t0 = t1
-            if self.fused_updates and self.defer_colsum and self.cuda:
-                G.flush_colsum()  # the bias updates still queued (every layer's lands before the next forward)
         finally:
+            # the bias updates still queued (every layer's lands before the next forward; after an exception too, so
+            # no queued reduce is left for an unrelated later GEMM of the stream to run)
+            if self.fused_updates and self.defer_colsum and self.cuda:
+                G.flush_colsum()
             # the grid GEMM form must not outlive this backward (an exception in between would leave every later
             # GEMM of the process on one workgroup per tile while records report the persistent form)
             self._gemm_grid(False)
