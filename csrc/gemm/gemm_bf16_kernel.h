@@ -876,28 +876,6 @@ __device__ __forceinline__ void glds16_si(const void* sbase, uint32_t voff, uint
                  : "memory", "scc");
 }
 
-#ifdef FAN_GEMM_BUFLDS
-// Diagnostic builds (-DFAN_GEMM_BUFLDS): the same LDS-DMA piece as a MUBUF buffer_load_dwordx4 ... lds (the form the
-// library's NT kernel uses) — a raw buffer resource per operand (base = the operand's K origin, no range check), the
-// lane offset in voffset and the K-tile's byte offset in soffset instead of a per-K-tile 64-bit base.
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4_t raw_rsrc(const void* p) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  i32x4_t r;
-  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-  r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xFFFFu));  // stride 0
-  r.z = -1;                                                                     // num_records: no range check
-  r.w = 0x00020000;                                                             // gfx9 raw-buffer word 3
-  return r;
-}
-template <uint32_t OFF>
-__device__ __forceinline__ void bufl16_si(i32x4_t rsrc, uint32_t voff, uint32_t soff, uint32_t lds_base) {
-  asm volatile("s_add_u32 m0, %3, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rsrc),
-               "s"(soff), "s"(lds_base), "i"(OFF)
-               : "memory", "scc");
-}
-#endif
-
 // s_waitcnt vmcnt(VM) lgkmcnt(LGKM) through the compiler's builtin, so that its own wait insertion knows what the wait
 // leaves outstanding: after an asm wait (opaque to it) it re-waits, lgkmcnt(N) by lgkmcnt(N), in front of the first use
 // of every fragment read already complete — ~16 extra s_waitcnt per K-tile of the 4-wave loop. The empty asm keeps
@@ -1374,19 +1352,9 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
 
   // glds piece p (0..G-1) of K-tile kt into stage kt & 1 (the lambdas are forced inline: an out-of-line call puts
   // the accumulator array in scratch memory)
-#ifdef FAN_GEMM_BUFLDS
-  const i32x4_t rs_a = raw_rsrc(a_k0), rs_b = raw_rsrc(b_k0);
-#endif
   auto piece = [&](int kt, auto pc) __attribute__((always_inline)) {
     constexpr int p = decltype(pc)::value;
     const uint32_t st = lds0 + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE + wave * 1024;
-#ifdef FAN_GEMM_BUFLDS
-    if constexpr (!ASC1) {
-      if constexpr (p < GA) bufl16_si<p * OpTile<BM, NT>::IB>(rs_a, off[p], (uint32_t)(kt * a_step), st);
-      else bufl16_si<A_BYTES + (p - GA) * OpTile<BN, NT>::IB>(rs_b, off[p], (uint32_t)(kt * b_step), st);
-      return;
-    }
-#endif
     if constexpr (p < GA) glds16_si<p * OpTile<BM, NT>::IB, ASC1>(a_k0 + kt * a_step, off[p], st);
     else glds16_si<A_BYTES + (p - GA) * OpTile<BN, NT>::IB>(b_k0 + kt * b_step, off[p], st);
   };
