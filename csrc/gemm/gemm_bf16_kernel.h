@@ -1095,7 +1095,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 __device__ __forceinline__ void mfma_acc(f32x4& acc, const s16x8& a, const s16x8& b) {
+#ifdef FAN_GEMM_NOMFMA  // diagnostic builds only: the main loop without its MFMAs (operands still read; timing)
+  asm volatile("" : "+a"(acc) : "v"(a), "v"(b));
+#else
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------------------
