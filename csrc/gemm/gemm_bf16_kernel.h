@@ -876,24 +876,6 @@ __device__ __forceinline__ void glds16_si(const void* sbase, uint32_t voff, uint
                  : "memory", "scc");
 }
 
-#ifdef FAN_GEMM_EDMA  // diagnostic two-barrier schedule of pl4_run (see ktile): its constants, in MFMAs of a k-step
-#ifndef FAN_EDMA_QA
-#define FAN_EDMA_QA 36  // k-step 0: barrier A before this MFMA
-#endif
-#ifndef FAN_EDMA_DSP
-#define FAN_EDMA_DSP 3  // DMA-piece spacing from barrier A on
-#endif
-#ifndef FAN_EDMA_QB
-#define FAN_EDMA_QB 26  // k-step 1: barrier B before this MFMA
-#endif
-#ifndef FAN_EDMA_RSP0
-#define FAN_EDMA_RSP0 2  // k-step 0: fragment-read spacing
-#endif
-#ifndef FAN_EDMA_RSP1
-#define FAN_EDMA_RSP1 2  // k-step 1: fragment-read spacing after barrier B
-#endif
-#endif
-
 // s_waitcnt vmcnt(VM) lgkmcnt(LGKM) through the compiler's builtin, so that its own wait insertion knows what the wait
 // leaves outstanding: after an asm wait (opaque to it) it re-waits, lgkmcnt(N) by lgkmcnt(N), in front of the first use
 // of every fragment read already complete — ~16 extra s_waitcnt per K-tile of the 4-wave loop. The empty asm keeps
@@ -1487,46 +1469,6 @@ __device__ __forceinline__ void pl4_run(const bf16_t* __restrict__ A, int64_t ld
     const char* st = smem + (STAGES == 2 ? kt & 1 : kt % 3) * STAGE;
     const bool csk = do_colsum && kt >= cs0 && kt < cs1;
     FAN_STAMP(0);
-#ifdef FAN_GEMM_EDMA
-    // Diagnostic builds (-DFAN_GEMM_EDMA, parameter sweep of round 5's two-barrier schedule): barrier A in k-step 0
-    // once this wave's reads of K-tile kt's k-step-1 fragments retired frees stage kt & 1, and K-tile kt + 2's DMA
-    // spreads over the rest of k-step 0 and the start of k-step 1; barrier B in k-step 1 (counted vmcnt) waits for
-    // K-tile kt + 1, whose k-step-0 fragments are read after it. Same products, same k order (bit-identical).
-    if constexpr (STAGES == 2 && !CHAIN && !COLSUM && (decltype(more_c)::value || decltype(more2_c)::value)) {
-      constexpr bool MORE = decltype(more_c)::value, MORE2 = decltype(more2_c)::value;
-      constexpr int QA = FAN_EDMA_QA, DS = FAN_EDMA_DSP, QB = FAN_EDMA_QB, R0 = FAN_EDMA_RSP0, R1 = FAN_EDMA_RSP1;
-      constexpr int P0r = (Q - 2 - QA) / DS + 1, P0 = P0r < G ? P0r : G;   // pieces of kt + 2 in k-step 0
-      constexpr int N1r = (QB - 1 + DS - 1) / DS, N1 = N1r < G - P0 ? N1r : G - P0;  // in k-step 1 before B
-      constexpr int NB = P0 + N1;
-      static_assert(R0 * (R - 1) < QA && QA < Q && QB >= 1 && QB + R1 * (R - 1) < Q && NB <= 63, "EDMA schedule");
-      const char* st1 = smem + ((kt + 1) & 1) * STAGE;
-      static_for<Q>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        if constexpr (q % R0 == 0 && q / R0 < R) read_next(st, 1, 1, q / R0);
-        if constexpr (MORE2 && q == QA) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-        }
-        if constexpr (MORE2 && q > QA && (q - QA - 1) % DS == 0 && (q - QA - 1) / DS < P0)
-          piece(kt + 2, std::integral_constant<int, (q - QA - 1) / DS>{});
-        mfma_acc(acc[q / NJ][q % NJ], fa[0][q / NJ], fb[0][q % NJ]);
-      });
-      static_for<Q>([&](auto qc) __attribute__((always_inline)) {
-        constexpr int q = decltype(qc)::value;
-        if constexpr (MORE2 && q >= 1 && (q - 1) % DS == 0 && P0 + (q - 1) / DS < G)
-          piece(kt + 2, std::integral_constant<int, P0 + (q - 1) / DS>{});
-        if constexpr (MORE && q == QB) {
-          if (OVL && kt == 0 && !first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MORE2 ? NB : 0) : "memory");
-          __builtin_amdgcn_s_barrier();
-        }
-        if constexpr (MORE && q >= QB && (q - QB) % R1 == 0 && (q - QB) / R1 < R) read_next(st1, 0, 0, (q - QB) / R1);
-        mfma_acc(acc[q / NJ][q % NJ], fa[1][q / NJ], fb[1][q % NJ]);
-      });
-      if constexpr (MORE) waitcnt_known<63, 0>();
-      return;
-    }
-#endif
     if constexpr (STAGES == 2) {
       constexpr bool kLast = OVL && !decltype(more_c)::value && !decltype(more2_c)::value;
       // the last K-tile: this tile's offsets are dead (its last DMA went out two K-tiles ago); the next tile's
