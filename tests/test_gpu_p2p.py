@@ -102,6 +102,10 @@ def _worker(rank, world, port, q):
             eng.trace(True)
             comm.reset_stats()
             eng.allreduce(g, out, n_valid=m).synchronize(30)
+            torch.cuda.synchronize()
+            # the peer's own request (and so its last flag writes) completed before the snapshot: without this the
+            # snapshot can catch the peer's final flag one round behind (ranks time-share the GPU)
+            dist.barrier()
             st = comm.stats()
             dbg = eng.debug_status()
             eng.trace(False)
