@@ -114,9 +114,12 @@ def _worker(rank, world, port, q):
             ok["stall_counters"] = (st["ready_waits"] == 2 * (world - 1) and st["timed_waits"] >= st["ready_waits"]
                                     and st["ready_stall_ms"] >= 0.0 and st["bytes_to_peer"][peer] == 2 * sb
                                     and st["bytes_to_peer"][rank] == 0)
-            ok["debug_status"] = (dbg["world"] == world and len(dbg["slots"]) == 8 and "p2p" in dbg
-                                  and dbg["p2p"]["flags"][peer] == comm.sequence
-                                  and dbg["peer_bytes"][peer] >= 2 * sb and dbg["comm_error"] == "")
+            ok["debug_status"] = (dbg["world"] == world and len(dbg["slots"]) == 8 and "p2p" in dbg)
+            ok["debug_flags"] = dbg["p2p"].get("flags") is not None and dbg["p2p"]["flags"][peer] == comm.sequence
+            ok["debug_peer_bytes"] = dbg["peer_bytes"][peer] >= 2 * sb
+            ok["debug_comm_error"] = dbg["comm_error"] == ""
+            if not all(ok[k] for k in ("debug_flags", "debug_peer_bytes", "debug_comm_error")):
+                ok["debug_detail"] = (dbg.get("p2p"), dbg["peer_bytes"], dbg["comm_error"], comm.sequence, 2 * sb)
             w0 = rng.standard_normal(m).astype(np.float32)
             ref_w, _ = O.sgd(w0, ref[:m], 0.5)
             for defer in (False, True):
@@ -160,7 +163,8 @@ def test_p2p_two_processes_one_gpu():
         pass
     for rank, (ok, seq) in res.items():
         assert "error" not in ok, ok
-        assert all(ok.values()), (rank, ok)
+        bad = {k: v for k, v in ok.items() if not v or k == "debug_detail"}
+        assert all(ok.values()), f"rank {rank}: {bad}"
     assert res[0][1] == res[1][1], "ranks issued different numbers of collectives"
 
 
