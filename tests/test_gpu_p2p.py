@@ -103,11 +103,12 @@ def _worker(rank, world, port, q):
             comm.reset_stats()
             eng.allreduce(g, out, n_valid=m).synchronize(30)
             torch.cuda.synchronize()
-            # the peer's own request (and so its last flag writes) completed before the snapshot: without this the
-            # snapshot can catch the peer's final flag one round behind (ranks time-share the GPU)
+            # the snapshot sits between two barriers: the peer's last flag writes of this request have landed, and the
+            # peer cannot raise the NEXT request's flags (one sequence ahead) before this rank has read them
             dist.barrier()
             st = comm.stats()
             dbg = eng.debug_status()
+            dist.barrier()
             eng.trace(False)
             sb = eng.wire_bytes(L) // (2 * (world - 1)) if world > 1 else 0
             peer = (rank + 1) % world
